@@ -1,0 +1,117 @@
+// common.h — shared device helpers for libfltee_agg (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fltee_agg.h"
+
+// One record of the wire / HBM layout: parameters.rs:3-10 Weight(u32 idx, f32 val),
+// little-endian, 8 bytes.  Kept as a u64 in registers: low word = idx, high = val bits.
+__device__ __forceinline__ uint32_t rec_idx(uint64_t r) { return (uint32_t)r; }
+__device__ __forceinline__ float rec_val(uint64_t r) { return __uint_as_float((uint32_t)(r >> 32)); }
+__device__ __forceinline__ uint64_t make_rec(uint32_t idx, float val) {
+    return ((uint64_t)__float_as_uint(val) << 32) | idx;
+}
+
+// Counter-based generators shared with the oracle (oracle/fltee_oracle.c):
+// Philox4x32-10 and the lowbias32 mixer.  Same constants, same stream ids.
+#define FLTEE_STREAM_DP 0x44504E5Au
+#define FLTEE_STREAM_LAPLACE 0x4C41504Cu
+#define FLTEE_STREAM_SAMPLE 0x534D504Cu
+
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t shuffle_step_key(uint32_t seed, uint32_t ilog,
+                                                              uint32_t jlog) {
+    return mix32(mix32(seed) + ((ilog << 8) | jlog) * 0x9E3779B9u);
+}
+
+__host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+#define FLTEE_CHECK_LAUNCH(st)                                            \
+    do {                                                                  \
+        if (hipGetLastError() != hipSuccess) return FLTEE_ERROR_UNEXPECTED; \
+    } while (0)
+
+static inline size_t next_pow2_sz(size_t x) {
+    size_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+static inline uint32_t log2_pow2(size_t x) {
+    uint32_t l = 0;
+    while (((size_t)1 << l) < x) ++l;
+    return l;
+}
+
+// ---- kernel launchers (implemented in the k_*.hip files) ------------------
+namespace fltee {
+
+// k_accumulate.hip
+hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,
+                                   const float *client_coef, bool accumulate, uint32_t *status,
+                                   hipStream_t s);
+hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float coef, float *out,
+                                   bool accumulate, uint32_t *status, hipStream_t s);
+hipError_t launch_scale(float *out, size_t d, float coef, hipStream_t s);
+hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint32_t *status,
+                              hipStream_t s);
+
+// k_bitonic.hip
+hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s);
+
+// k_fold.hip
+hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *dst,
+                                hipStream_t s);
+hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
+                       uint32_t *status, hipStream_t s);
+hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
+                          hipStream_t s);
+hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,
+                                 uint32_t *status, hipStream_t s);
+hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,
+                               float *out, size_t d, bool accumulate, hipStream_t s);
+
+// k_nips19.hip
+hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t *r,
+                            hipStream_t s);
+hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, size_t d,
+                               size_t tf, size_t m, uint64_t *dst, hipStream_t s);
+hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float *out,
+                                 hipStream_t s);
+
+// k_dp.hip
+hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,
+                           uint64_t seed, hipStream_t s);
+hipError_t launch_client_clip_coef(const void *rec, size_t n, size_t k, float clipping,
+                                   float *coef, hipStream_t s);
+hipError_t launch_apply_clip(void *rec, size_t n, size_t k, const float *coef, hipStream_t s);
+
+// k_aes.hip
+void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
+hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
+                          size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
+                          hipStream_t s);
+
+}  // namespace fltee

@@ -1,0 +1,413 @@
+// ecalls.hip — the four ECALLs of Enclave.edl on an MI355X (host side).
+//
+// State machine restated from secure_aggregation/enclave/src/lib.rs:
+//   FL_CONFIG_MAP (lib.rs:83-91, fl_config.rs)      -> g_cfg
+//   SESSION_KEYS (lib.rs:93-101, session_key_store) -> g_keys (id set; the key is
+//                                                      a pure function of the id)
+//   single TCS (Enclave.config.xml:6)               -> api_mutex()
+// The data path runs on the eid's GPU: "Loading" = H2D of the ciphertext,
+// "Decryption" = AES-128-CTR kernel, "Aggregation" = engine.hip + DP noise.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "common.h"
+#include "engine.h"
+
+namespace fltee {
+
+std::recursive_mutex &api_mutex() {
+    static std::recursive_mutex mu;
+    return mu;
+}
+
+struct FLConfig {  // fl_config.rs:29-44
+    std::vector<uint32_t> client_ids;
+    size_t d = 0, k = 0;
+    float sigma = 0, clipping = 0, alpha = 0, ratio = 0;
+    uint32_t alg = 0, round = 0;
+    uint8_t verbose = 0, dp = 0;
+    std::set<uint32_t> sampled;  // current_sampled_clients (HashSet)
+};
+
+static std::map<uint32_t, FLConfig> g_cfg;
+static std::set<uint32_t> g_keys;
+static bool g_have_keys = false;
+static std::vector<int> g_eid_dev;  // eid - 1 -> hip device
+
+void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
+
+static inline double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static size_t f32_to_usize_sat(float x) {
+    if (!(x > 0.0f)) return 0;
+    if (x >= 18446744073709551616.0f) return SIZE_MAX;
+    return (size_t)x;
+}
+
+// sgx_rand::sample reservoir (common.rs:101-105) driven by Philox4x32-10.
+static void sample_client_ids(const std::vector<uint32_t> &ids, size_t amount, uint64_t seed,
+                              std::vector<uint32_t> &out) {
+    const size_t take = std::min(amount, ids.size());
+    out.assign(ids.begin(), ids.begin() + take);
+    if (take != amount) return;
+    uint64_t counter = 0;
+    auto draw = [&]() {
+        uint32_t c[4] = {(uint32_t)counter, (uint32_t)(counter >> 32), 0u, FLTEE_STREAM_SAMPLE};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        ++counter;
+        return ((uint64_t)c[1] << 32) | c[0];
+    };
+    for (size_t i = 0; i + amount < ids.size(); ++i) {
+        const uint64_t range = (uint64_t)(i + 1 + amount);
+        const uint64_t zone = UINT64_MAX - UINT64_MAX % range;
+        uint64_t v;
+        do { v = draw(); } while (v >= zone);
+        const uint64_t kk = v % range;
+        if (kk < amount) out[kk] = ids[amount + i];
+    }
+}
+
+static DeviceCtx *eid_ctx(fltee_eid_t eid) {
+    if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return nullptr;
+    const int dev = g_eid_dev[eid - 1];
+    if (hipSetDevice(dev) != hipSuccess) return nullptr;
+    DeviceCtx *c = device_ctx(dev);
+    if (c && !c->stream) {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    }
+    return c;
+}
+
+static uint32_t check_uploaded(const FLConfig &cfg, const uint32_t *ids, size_t n) {
+    if (n != cfg.sampled.size()) {  // lib.rs:269-272
+        std::printf("[VERIFICATION ERROR] Uploaded client id is not matched for secure sampled one.\n");
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (!cfg.sampled.count(ids[i])) {
+            std::printf("[VERIFICATION ERROR] Uploaded client id is not matched for secure sampled one.\n");
+            return FLTEE_ERROR_INVALID_PARAMETER;
+        }
+    return FLTEE_SUCCESS;
+}
+
+// H2D + GPU AES-CTR decrypt of n slices of bpc bytes -> c->records (n * (bpc/8) records)
+static uint32_t load_and_decrypt(DeviceCtx *c, const uint32_t *ids, size_t n, const uint8_t *enc,
+                                 size_t bpc, float *t_load, float *t_dec) {
+    const size_t rpc = bpc / 8;
+    const double t0 = now_s();
+    if (!c->cipher.reserve(n * bpc) || !c->records.reserve(n * rpc * 8) ||
+        !c->round_keys.reserve(n * 44 * 4))
+        return FLTEE_ERROR_OUT_OF_MEMORY;
+    if (n * bpc && hipMemcpyAsync(c->cipher.ptr, enc, n * bpc, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (t_load) *t_load = (float)(now_s() - t0);
+
+    const double t1 = now_s();
+    std::vector<uint32_t> rk(n * 44);
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t key[16] = {0};  // session_key_store.rs:21-22
+        key[4] = (uint8_t)(ids[i] >> 24);
+        key[5] = (uint8_t)(ids[i] >> 16);
+        key[6] = (uint8_t)(ids[i] >> 8);
+        key[7] = (uint8_t)ids[i];
+        aes128_expand_key(key, &rk[i * 44]);
+    }
+    if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (launch_aes_ctr((const uint8_t *)c->cipher.ptr, n, bpc, rpc, (const uint32_t *)c->round_keys.ptr,
+                       (uint8_t *)c->records.ptr, c->stream) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (t_dec) *t_dec = (float)(now_s() - t1);
+    return FLTEE_SUCCESS;
+}
+
+static uint32_t read_status(DeviceCtx *c, uint32_t *st) {
+    if (hipMemcpyAsync(st, c->status, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    return FLTEE_SUCCESS;
+}
+
+// Aggregate c->records (n clients x rpc records) with alg into the device out
+// buffer (c->ws_b reused is unsafe: use records tail) and run the exact
+// fallbacks the status word asks for.
+static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t rpc, size_t d,
+                                  size_t k_req, size_t batch, float *d_out) {
+    fltee_device_opts o;
+    std::memset(&o, 0, sizeof o);
+    o.k_req = k_req;
+    o.batch = batch;
+    const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
+                      alg == FLTEE_ALG_NON_OBLIVIOUS;
+    if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
+    if (alg == FLTEE_ALG_NIPS19) o.seed = next_seed();
+    size_t halo = n;
+    for (int attempt = 0; attempt < 6; ++attempt) {
+        if (hipMemsetAsync(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        o.fold_halo = halo;
+        uint32_t st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, c->stream, c->status);
+        if (st != FLTEE_SUCCESS) return st;
+        uint32_t dev_st = 0;
+        if (read_status(c, &dev_st)) return FLTEE_ERROR_UNEXPECTED;
+        if (dev_st == 0) return FLTEE_SUCCESS;
+        if (dev_st & FLTEE_DEV_ERR_INDEX_RANGE) return FLTEE_ERROR_INVALID_PARAMETER;  // enclave panic
+        if (dev_st & FLTEE_DEV_ERR_DENSE_ORDER) {  // not dense after all: scatter semantics
+            o.flags &= ~FLTEE_OPT_DENSE;
+            continue;
+        }
+        if (dev_st & FLTEE_DEV_ERR_FOLD_OVERFLOW) {
+            if (flat) {  // a client repeated an index: exact sequential sweep
+                const float coef = 1.0f / (float)n;
+                if (alg == FLTEE_ALG_PATH_ORAM) {
+                    // range already validated by the first pass (no INDEX_RANGE bit)
+                }
+                if (aggregate_sparse_sequential(c->records.ptr, n * rpc, d, coef, d_out, false, c->stream))
+                    return FLTEE_ERROR_UNEXPECTED;
+                return hipStreamSynchronize(c->stream) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+            }
+            halo = halo * 4 + 16;  // a run longer than the halo: widen it
+            continue;
+        }
+        return FLTEE_ERROR_UNEXPECTED;
+    }
+    return FLTEE_ERROR_INVALID_PARAMETER;
+}
+
+}  // namespace fltee
+
+using namespace fltee;
+
+extern "C" const char *fltee_version(void) { return "fltee-mi355x 0.1 (gfx950)"; }
+
+extern "C" fltee_status_t fltee_device_init(int hip_device, fltee_eid_t *eid) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (!eid) return FLTEE_ERROR_INVALID_PARAMETER;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || hip_device < 0 || hip_device >= count)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (hipSetDevice(hip_device) != hipSuccess || !device_ctx(hip_device)) return FLTEE_ERROR_UNEXPECTED;
+    g_eid_dev.push_back(hip_device);
+    *eid = (fltee_eid_t)g_eid_dev.size();
+    return FLTEE_SUCCESS;
+}
+
+extern "C" fltee_status_t fltee_device_fini(fltee_eid_t eid) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
+    const int dev = g_eid_dev[eid - 1];
+    g_eid_dev[eid - 1] = -1;
+    if (hipSetDevice(dev) == hipSuccess) (void)hipDeviceSynchronize();
+    return FLTEE_SUCCESS;
+}
+
+// lib.rs:113-180
+extern "C" fltee_status_t ecall_fl_init(fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id,
+                                        const uint32_t *client_ids, size_t client_size,
+                                        size_t num_of_parameters, size_t num_of_sparse_parameters,
+                                        float sigma, float clipping, float alpha,
+                                        float sampling_ratio, uint32_t aggregation_alg,
+                                        uint8_t verbose, uint8_t dp) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
+    if (!retval) return FLTEE_ERROR_INVALID_PARAMETER;
+    FLConfig cfg;
+    cfg.client_ids.assign(client_ids, client_ids + client_size);
+    cfg.d = num_of_parameters;
+    cfg.k = num_of_sparse_parameters;
+    cfg.sigma = sigma;
+    cfg.clipping = clipping;
+    cfg.alpha = alpha;
+    cfg.ratio = sampling_ratio;
+    cfg.alg = aggregation_alg;
+    cfg.verbose = verbose;
+    cfg.dp = dp;
+    cfg.round = 0;
+    if (!g_have_keys && verbose) std::printf("[FLTEE] remote attestation mock\n");
+    for (size_t i = 0; i < client_size; ++i) g_keys.insert(client_ids[i]);  // lib.rs:163-174
+    g_have_keys = true;
+    g_cfg[fl_id] = std::move(cfg);
+    if (verbose) std::printf("[FLTEE] make fl config id %u\n", fl_id);
+    *retval = FLTEE_SUCCESS;
+    return FLTEE_SUCCESS;
+}
+
+// lib.rs:182-219
+extern "C" fltee_status_t ecall_start_round(fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id,
+                                            uint32_t round, size_t sample_size,
+                                            uint32_t *sampled_client_ids) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
+    if (!retval) return FLTEE_ERROR_INVALID_PARAMETER;
+    auto it = g_cfg.find(fl_id);
+    if (it == g_cfg.end()) { *retval = FLTEE_ERROR_UNEXPECTED; return FLTEE_SUCCESS; }
+    FLConfig &cfg = it->second;
+    if (cfg.round != round) { *retval = FLTEE_ERROR_INVALID_PARAMETER; return FLTEE_SUCCESS; }
+    std::memset(sampled_client_ids, 0, sample_size * 4);  // [out] zero-fill
+    const size_t calc = f32_to_usize_sat((float)cfg.client_ids.size() * cfg.ratio);
+    if (calc != sample_size) { *retval = FLTEE_ERROR_INVALID_PARAMETER; return FLTEE_SUCCESS; }
+    std::vector<uint32_t> sampled;
+    sample_client_ids(cfg.client_ids, calc, next_seed(), sampled);
+    std::copy(sampled.begin(), sampled.end(), sampled_client_ids);
+    cfg.sampled = std::set<uint32_t>(sampled.begin(), sampled.end());
+    if (cfg.verbose)
+        std::printf("[FLTEE] sampling for round %u is done and store %zu/%zu client ids.\n", round,
+                    sample_size, cfg.client_ids.size());
+    *retval = FLTEE_SUCCESS;
+    return FLTEE_SUCCESS;
+}
+
+// lib.rs:221-423
+extern "C" fltee_status_t ecall_secure_aggregation(
+    fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id, uint32_t round,
+    const uint32_t *client_ids, size_t client_size, const uint8_t *encrypted_parameters_data,
+    size_t encrypted_parameters_size, size_t num_of_parameters, size_t num_of_sparse_parameters,
+    uint32_t aggregation_alg, float *updated_parameters_data, float *execution_time_results) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (!retval) return FLTEE_ERROR_INVALID_PARAMETER;
+    DeviceCtx *c = eid_ctx(eid);
+    if (!c) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
+    const size_t d = num_of_parameters;
+    std::memset(updated_parameters_data, 0, d * sizeof(float));  // Enclave_t.c:626
+    std::memset(execution_time_results, 0, 3 * sizeof(float));
+    auto fail = [&](uint32_t st) { *retval = st; return FLTEE_SUCCESS; };
+    auto it = g_cfg.find(fl_id);
+    if (it == g_cfg.end()) return fail(FLTEE_ERROR_UNEXPECTED);
+    FLConfig &cfg = it->second;
+    if (cfg.round != round || cfg.alg != aggregation_alg) return fail(FLTEE_ERROR_INVALID_PARAMETER);
+    const size_t n = client_size;
+    if (n == 0) return fail(FLTEE_ERROR_INVALID_PARAMETER);  // lib.rs:305 would divide by zero
+    if (uint32_t st = check_uploaded(cfg, client_ids, n)) return fail(st);
+    for (size_t i = 0; i < n; ++i)
+        if (!g_keys.count(client_ids[i])) return fail(FLTEE_ERROR_UNEXPECTED);  // lib.rs:319-322
+    switch (aggregation_alg) {  // lib.rs:359-397 (6 and 7 are not dispatched here: panic)
+    case FLTEE_ALG_ADVANCED: case FLTEE_ALG_NIPS19: case FLTEE_ALG_BASELINE:
+    case FLTEE_ALG_NON_OBLIVIOUS: case FLTEE_ALG_PATH_ORAM: break;
+    default: return fail(FLTEE_ERROR_INVALID_PARAMETER);
+    }
+    const size_t bpc = encrypted_parameters_size / n;  // lib.rs:305-306
+    if (bpc % 8) return fail(FLTEE_ERROR_INVALID_PARAMETER);  // (records must stay 8-B aligned)
+    const size_t rpc = bpc / 8;
+    if (aggregation_alg == FLTEE_ALG_ADVANCED && n * num_of_sparse_parameters > n * rpc)
+        return fail(FLTEE_ERROR_INVALID_PARAMETER);  // advanced.rs:72 out-of-bounds panic
+
+    uint32_t st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data, bpc,
+                                   &execution_time_results[0], &execution_time_results[1]);
+    if (st) return fail(st);
+
+    const double t2 = now_s();
+    float *d_out = nullptr;
+    if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
+    d_out = (float *)c->outbuf.ptr;
+    st = aggregate_records(c, aggregation_alg, n, rpc, d, num_of_sparse_parameters, 0, d_out);
+    if (!st && cfg.dp) {  // lib.rs:399-408
+        if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
+            st = FLTEE_ERROR_UNEXPECTED;
+    }
+    if (!st && hipMemcpyAsync(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        st = FLTEE_ERROR_UNEXPECTED;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
+    if (st) {
+        std::memset(updated_parameters_data, 0, d * sizeof(float));
+        return fail(st);
+    }
+    execution_time_results[2] = (float)(now_s() - t2);
+    if (cfg.verbose)
+        std::printf("[FLTEE CLOCK] Loading %.6f Decryption %.6f Aggregation %.6f seconds\n",
+                    execution_time_results[0], execution_time_results[1], execution_time_results[2]);
+    cfg.round += 1;  // lib.rs:421
+    *retval = FLTEE_SUCCESS;
+    return FLTEE_SUCCESS;
+}
+
+// lib.rs:425-592
+extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
+    fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id, uint32_t round,
+    size_t optimal_num_of_clients, const uint32_t *client_ids, size_t client_size,
+    const uint8_t *encrypted_parameters_data_ptr, size_t num_of_parameters,
+    size_t num_of_sparse_parameters, uint32_t aggregation_alg, float *updated_parameters_data,
+    float *execution_time_results) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (!retval) return FLTEE_ERROR_INVALID_PARAMETER;
+    DeviceCtx *c = eid_ctx(eid);
+    if (!c) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
+    const size_t d = num_of_parameters, k = num_of_sparse_parameters, n = client_size;
+    std::memset(updated_parameters_data, 0, d * sizeof(float));
+    std::memset(execution_time_results, 0, 3 * sizeof(float));
+    auto fail = [&](uint32_t st) { *retval = st; return FLTEE_SUCCESS; };
+    auto it = g_cfg.find(fl_id);
+    if (it == g_cfg.end()) return fail(FLTEE_ERROR_UNEXPECTED);
+    FLConfig &cfg = it->second;
+    if (cfg.round != round || cfg.alg != aggregation_alg) return fail(FLTEE_ERROR_INVALID_PARAMETER);
+    if (n == 0 || optimal_num_of_clients == 0) return fail(FLTEE_ERROR_INVALID_PARAMETER);
+    if (uint32_t st = check_uploaded(cfg, client_ids, n)) return fail(st);
+    for (size_t i = 0; i < n; ++i)
+        if (!g_keys.count(client_ids[i])) return fail(FLTEE_ERROR_UNEXPECTED);
+
+    float t_load = 0, t_dec = 0;
+    const double t1 = now_s();
+    uint32_t st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data_ptr, k * 8, &t_load, &t_dec);
+    if (st) return fail(st);
+    execution_time_results[0] = t_load;
+    float *d_out = nullptr;
+    if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
+    d_out = (float *)c->outbuf.ptr;
+    st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
+    if (!st && cfg.dp) {  // lib.rs:586-588
+        if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
+            st = FLTEE_ERROR_UNEXPECTED;
+    }
+    if (!st && hipMemcpyAsync(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        st = FLTEE_ERROR_UNEXPECTED;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
+    if (st) {
+        std::memset(updated_parameters_data, 0, d * sizeof(float));
+        return fail(st);
+    }
+    execution_time_results[1] = (float)(now_s() - t1) - t_load;  // decrypt + aggregate
+    cfg.round += 1;
+    *retval = FLTEE_SUCCESS;
+    return FLTEE_SUCCESS;
+}
+
+extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n,
+                                               const void *d_cipher, size_t bytes_per_client,
+                                               void *d_records, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c || bytes_per_client % 8) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (!c->round_keys.reserve(n * 44 * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
+    std::vector<uint32_t> rk(n * 44);
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t key[16] = {0};
+        key[4] = (uint8_t)(client_ids[i] >> 24);
+        key[5] = (uint8_t)(client_ids[i] >> 16);
+        key[6] = (uint8_t)(client_ids[i] >> 8);
+        key[7] = (uint8_t)client_ids[i];
+        aes128_expand_key(key, &rk[i * 44]);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (launch_aes_ctr((const uint8_t *)d_cipher, n, bytes_per_client, bytes_per_client / 8,
+                       (const uint32_t *)c->round_keys.ptr, (uint8_t *)d_records, s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    // rk lives on this stack frame: wait for the (tiny) copy + kernel
+    return hipStreamSynchronize(s) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+}
+
+// CPU self-test hook: one AES-128 block with the library's tables (no GPU).
+namespace fltee { void aes128_encrypt_block_host(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]); }
+extern "C" void fltee_debug_aes_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+    fltee::aes128_encrypt_block_host(key, in, out);
+}

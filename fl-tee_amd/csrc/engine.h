@@ -1,0 +1,42 @@
+// engine.h — per-device state and the internal aggregation entry points.
+#pragma once
+#include <mutex>
+
+#include "common.h"
+
+namespace fltee {
+
+constexpr int kMaxDevices = 64;
+
+struct Buffer {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t bytes);  // grow-only hipMalloc
+};
+
+struct DeviceCtx {
+    bool ready = false;
+    int device = -1;
+    uint32_t *status = nullptr;  // library-owned device status word
+    Buffer ws_a, ws_b, ws_mat, ws_r, ws_coef, ws_rec;  // aggregation scratch
+    Buffer cipher, records, round_keys, outbuf;         // ECALL staging
+    hipStream_t stream = nullptr;                        // ECALL stream
+};
+
+// One process-wide lock: the enclave had a single TCS (Enclave.config.xml:6).
+std::recursive_mutex &api_mutex();
+
+DeviceCtx *device_ctx(int dev);
+DeviceCtx *current_ctx();
+uint64_t next_seed();
+void set_debug_seed(uint64_t seed);
+float nips19_threshold(size_t d, size_t k, size_t n);
+
+fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,
+                         const fltee_device_opts &o, hipStream_t s, uint32_t *status);
+fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
+                                           float *out, bool acc, hipStream_t s);
+size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);
+bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);
+
+}  // namespace fltee

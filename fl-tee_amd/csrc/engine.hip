@@ -1,0 +1,341 @@
+// engine.hip — device-side orchestration of the aggregation algorithms.
+//
+// fltee_aggregate_device() is the aggregation of ecall_secure_aggregation
+// (lib.rs:355-408) on records already decrypted into HBM: the dispatcher on
+// aggregation_alg (lib.rs:359-397), optional DP noise (lib.rs:399-408), with
+// the enclave's 1f32/n averaging (common.rs:14-19).  Scratch HBM is held per
+// device, grow-only, so steady-state calls do no hipMalloc (graph-capturable
+// once reserved).
+#include <sys/random.h>
+#include <time.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
+#include "common.h"
+#include "engine.h"
+
+namespace fltee {
+
+hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t d, float *mat,
+                                    uint32_t *status, hipStream_t s);
+hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
+                                  bool accumulate, hipStream_t s);
+
+static DeviceCtx g_ctx[kMaxDevices];
+static std::mutex g_ctx_mu;
+static std::atomic<uint64_t> g_debug_seed{0};
+static std::atomic<uint64_t> g_seed_calls{0};
+
+uint64_t next_seed() {
+    const uint64_t s = g_debug_seed.load();
+    if (s) return s + 0x9E3779B97F4A7C15ull * (++g_seed_calls);
+    uint64_t r = 0;
+    if (getrandom(&r, sizeof r, 0) != (ssize_t)sizeof r) r = (uint64_t)time(nullptr) * 0x2545F4914F6CDD1Dull;
+    return r ? r : 1;
+}
+
+void set_debug_seed(uint64_t seed) {
+    g_debug_seed.store(seed);
+    g_seed_calls.store(0);
+}
+
+DeviceCtx *device_ctx(int dev) {
+    if (dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    DeviceCtx &c = g_ctx[dev];
+    if (!c.ready) {
+        if (hipSetDevice(dev) != hipSuccess) return nullptr;
+        if (hipMalloc(&c.status, 256) != hipSuccess) return nullptr;
+        if (hipMemset(c.status, 0, 256) != hipSuccess) return nullptr;
+        c.device = dev;
+        c.ready = true;
+    }
+    return &c;
+}
+
+DeviceCtx *current_ctx() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    return device_ctx(dev);
+}
+
+bool Buffer::reserve(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    const size_t want = bytes + bytes / 8 + 256;
+    if (hipMalloc(&ptr, want) != hipSuccess) { ptr = nullptr; return false; }
+    cap = want;
+    return true;
+}
+
+float nips19_threshold(size_t d, size_t k, size_t n) {
+    const float epsilon = 100.0f, delta = 1.0f / (float)n;
+    const float l1 = 2.0f * (float)k;
+    return l1 / epsilon * logf((float)d / delta);
+}
+
+static size_t f32_to_usize_sat(float x) {
+    if (!(x > 0.0f)) return 0;
+    if (x >= 18446744073709551616.0f) return SIZE_MAX;
+    return (size_t)x;
+}
+
+// scratch plan per algorithm
+struct Plan {
+    size_t a_bytes = 0, b_bytes = 0, mat_bytes = 0, r_bytes = 0, coef_bytes = 0, rec_bytes = 0;
+};
+
+static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
+    Plan p;
+    const bool dense = (o.flags & FLTEE_OPT_DENSE) != 0;
+    const bool clip = (o.flags & FLTEE_OPT_CLIP) != 0;
+    if (clip) {
+        p.coef_bytes = n * 4;
+        if (!dense) p.rec_bytes = n * k * 8;
+    }
+    switch (alg) {
+    case FLTEE_ALG_BASELINE:
+    case FLTEE_ALG_PATH_ORAM:
+        if (!dense) p.mat_bytes = n * d * 4;
+        break;
+    case FLTEE_ALG_NON_OBLIVIOUS:
+        if (!dense) p.a_bytes = next_pow2_sz(n * k) * 8;
+        break;
+    case FLTEE_ALG_ADVANCED:
+        p.a_bytes = p.b_bytes = next_pow2_sz(n * k + d) * 8;
+        break;
+    case FLTEE_ALG_OPTIMIZED: {
+        size_t b = o.batch ? (o.batch < n ? o.batch : n) : n;
+        p.a_bytes = p.b_bytes = next_pow2_sz(b * k + d) * 8;
+        break;
+    }
+    case FLTEE_ALG_NIPS19: {
+        const float T = nips19_threshold(d, k, n);
+        p.a_bytes = next_pow2_sz(n * k + d * f32_to_usize_sat(T)) * 8;
+        p.r_bytes = d * 4;
+        break;
+    }
+    default: break;
+    }
+    return p;
+}
+
+static bool reserve_plan(DeviceCtx *c, const Plan &p) {
+    return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
+           c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
+           c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes);
+}
+
+// `advanced` over n clients' records into out (coef or accumulate).
+static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k, size_t d,
+                               size_t k_req, size_t halo, float coef, float *out, bool acc,
+                               uint32_t *status, hipStream_t s) {
+    const size_t L = n * k + d, M = next_pow2_sz(L);
+    const size_t fold_len = n * k_req + d;
+    uint64_t *A = (uint64_t *)c->ws_a.ptr, *B = (uint64_t *)c->ws_b.ptr;
+    hipError_t e = launch_advanced_init(rec, n * k, d, M, A, s);
+    if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
+    if (e == hipSuccess) e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
+    if (e == hipSuccess) e = bitonic_sort(B, M, 0, 0, s);
+    if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
+    return e;
+}
+
+fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,
+                         const fltee_device_opts &o, hipStream_t s, uint32_t *status) {
+    DeviceCtx *c = current_ctx();
+    if (!c) return FLTEE_ERROR_UNEXPECTED;
+    if (n == 0) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (n * k + d >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;  // 32-bit positions
+    const bool dense = (o.flags & FLTEE_OPT_DENSE) != 0;
+    if (dense && k != d) return FLTEE_ERROR_INVALID_PARAMETER;
+    const bool acc = (o.flags & FLTEE_OPT_ACCUMULATE) != 0;
+    const size_t n_avg = o.n_avg ? o.n_avg : n;
+    const float coef = (o.flags & FLTEE_OPT_NO_AVERAGE) ? 1.0f : 1.0f / (float)n_avg;
+    const Plan p = plan_for(alg, n, k, d, o);
+    if (!reserve_plan(c, p)) return FLTEE_ERROR_OUT_OF_MEMORY;
+
+    // per-client L2 clip (update.py:187-204), off by default
+    const float *ccoef = nullptr;
+    if (o.flags & FLTEE_OPT_CLIP) {
+        float *cf = (float *)c->ws_coef.ptr;
+        if (launch_client_clip_coef(rec, n, k, o.clipping, cf, s) != hipSuccess)
+            return FLTEE_ERROR_UNEXPECTED;
+        ccoef = cf;
+        if (!dense) {
+            if (hipMemcpyAsync(c->ws_rec.ptr, rec, n * k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                launch_apply_clip(c->ws_rec.ptr, n, k, cf, s) != hipSuccess)
+                return FLTEE_ERROR_UNEXPECTED;
+            rec = c->ws_rec.ptr;
+        }
+    }
+
+    hipError_t e = hipSuccess;
+    switch (alg) {
+    case FLTEE_ALG_BASELINE:
+    case FLTEE_ALG_PATH_ORAM:
+    case FLTEE_ALG_NON_OBLIVIOUS:
+        if (dense) {
+            e = launch_dense_accumulate(rec, n, d, coef, out, ccoef, acc, status, s);
+        } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
+            const size_t M = next_pow2_sz(n * k);
+            uint64_t *K = (uint64_t *)c->ws_a.ptr;
+            e = launch_composite_init(rec, n * k, d, M, K, status, s);
+            if (e == hipSuccess) e = bitonic_sort(K, M, 1, 0, s);
+            if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
+            if (e == hipSuccess) e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, s);
+        } else {
+            if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
+                e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
+            if (e == hipSuccess)
+                e = launch_sweep_materialize(rec, n, k, d, (float *)c->ws_mat.ptr, status, s);
+            if (e == hipSuccess)
+                e = launch_rows_accumulate((const float *)c->ws_mat.ptr, n, d, coef, out, acc, s);
+        }
+        break;
+    case FLTEE_ALG_ADVANCED: {
+        const size_t k_req = o.k_req ? o.k_req : k;
+        const size_t fold_len = n * k_req + d;
+        if (fold_len > n * k + d) return FLTEE_ERROR_INVALID_PARAMETER;  // advanced.rs:72 panic
+        e = run_advanced(c, rec, n, k, d, k_req, o.fold_halo, coef, out, acc, status, s);
+        break;
+    }
+    case FLTEE_ALG_OPTIMIZED: {
+        const size_t batch = o.batch ? o.batch : n;
+        if (!acc) e = hipMemsetAsync(out, 0, d * 4, s);
+        for (size_t c0 = 0; e == hipSuccess && c0 < n; c0 += batch) {
+            const size_t nb = (c0 + batch < n) ? batch : n - c0;
+            e = run_advanced(c, (const uint8_t *)rec + c0 * k * 8, nb, k, d, k, o.fold_halo, 1.0f,
+                             out, true, status, s);
+        }
+        if (e == hipSuccess && coef != 1.0f) e = launch_scale(out, d, coef, s);
+        break;
+    }
+    case FLTEE_ALG_NIPS19: {
+        const float T = nips19_threshold(d, k, n);
+        const size_t tf = f32_to_usize_sat(T);
+        const size_t L = n * k + d * tf, M = next_pow2_sz(L);
+        if (L >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+        const uint64_t seed = o.seed ? o.seed : next_seed();
+        uint32_t *r = (uint32_t *)c->ws_r.ptr;
+        uint64_t *A = (uint64_t *)c->ws_a.ptr;
+        e = launch_laplace_r(d, k, T, seed, r, s);
+        if (e == hipSuccess) e = launch_nips19_build(rec, n * k, r, d, tf, M, A, s);
+        if (e == hipSuccess) e = bitonic_sort(A, M, 2, (uint32_t)(seed ^ (seed >> 32)), s);
+        if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
+        if (e == hipSuccess) e = launch_safe_aggregate(A, M, d, out, s);
+        if (e == hipSuccess && !acc && coef != 1.0f) e = launch_scale(out, d, coef, s);
+        break;
+    }
+    default:
+        return FLTEE_ERROR_INVALID_PARAMETER;  // lib.rs:396 panics on unknown algs
+    }
+    if (e == hipSuccess && (o.flags & FLTEE_OPT_DP)) {
+        const uint64_t seed = o.seed ? o.seed : next_seed();
+        e = launch_dp_noise(out, d, o.sigma, o.clipping, n_avg, seed, s);
+    }
+    return e == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+}
+
+// Exact fallbacks, run by the ECALL layer after reading the status word.
+fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
+                                           float *out, bool acc, hipStream_t s) {
+    return launch_sweep_accumulate(rec, nrec, d, coef, out, acc, nullptr, s) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
+    const Plan p = plan_for(alg, n, k, d, o);
+    return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes;
+}
+
+bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
+    DeviceCtx *c = current_ctx();
+    return c && reserve_plan(c, plan_for(alg, n, k, d, o));
+}
+
+}  // namespace fltee
+
+// ============================================================ C ABI =========
+using namespace fltee;
+
+static fltee_device_opts default_opts() {
+    fltee_device_opts o;
+    std::memset(&o, 0, sizeof o);
+    return o;
+}
+
+extern "C" fltee_status_t fltee_aggregate_device(uint32_t alg, const void *d_records, size_t n,
+                                                 size_t k, size_t d, float *d_out,
+                                                 const fltee_device_opts *opts, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    const fltee_device_opts o = opts ? *opts : default_opts();
+    DeviceCtx *c = current_ctx();
+    if (!c) return FLTEE_ERROR_UNEXPECTED;
+    uint32_t *status = o.d_status ? o.d_status : c->status;
+    hipStream_t s = (hipStream_t)stream;
+    if (!o.d_status && hipMemsetAsync(c->status, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    return aggregate(alg, d_records, n, k, d, d_out, o, s, status);
+}
+
+extern "C" size_t fltee_workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d,
+                                        const fltee_device_opts *opts) {
+    const fltee_device_opts o = opts ? *opts : default_opts();
+    return workspace_bytes(alg, n, k, d, o);
+}
+
+extern "C" fltee_status_t fltee_reserve(uint32_t alg, size_t n, size_t k, size_t d,
+                                        const fltee_device_opts *opts) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    const fltee_device_opts o = opts ? *opts : default_opts();
+    return reserve(alg, n, k, d, o) ? FLTEE_SUCCESS : FLTEE_ERROR_OUT_OF_MEMORY;
+}
+
+extern "C" fltee_status_t fltee_device_status(void *stream, uint32_t *status) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c || !status) return FLTEE_ERROR_UNEXPECTED;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipStreamSynchronize(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (hipMemcpy(status, c->status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    if (hipMemset(c->status, 0, 4) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    return FLTEE_SUCCESS;
+}
+
+extern "C" fltee_status_t fltee_bitonic_device(void *d_records, size_t m, uint32_t mode,
+                                               uint32_t seed, void *stream) {
+    if (m & (m - 1)) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (m >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+    return bitonic_sort((uint64_t *)d_records, m, mode, seed, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_fold_device(const void *d_src, void *d_dst, size_t m,
+                                            size_t fold_len, size_t halo, uint32_t *d_status,
+                                            void *stream) {
+    if (fold_len == 0 || fold_len > m || !d_status) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_fold((const uint64_t *)d_src, (uint64_t *)d_dst, m, fold_len, halo, d_status,
+                       (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_INVALID_PARAMETER;
+}
+
+extern "C" fltee_status_t fltee_laplace_r_device(size_t d, size_t k, size_t n, uint64_t seed,
+                                                 uint32_t *d_r, float *T_out, void *stream) {
+    if (n == 0) return FLTEE_ERROR_INVALID_PARAMETER;
+    const float T = nips19_threshold(d, k, n);
+    if (T_out) *T_out = T;
+    return launch_laplace_r(d, k, T, seed, d_r, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }

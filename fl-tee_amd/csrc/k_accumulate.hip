@@ -1,0 +1,355 @@
+// k_accumulate.hip — element-wise accumulate across clients (gfx950).
+//
+// Reference semantics (non_oblivious.rs:6-15, baseline.rs:7-60, oram.rs:86-118):
+// out[idx] += val for every record in upload order (client order, then each
+// client's own order), starting from +0.0 (the SGX bridge zero-fills [out],
+// Enclave_t.c:626), then out *= 1f32/n (common.rs:14-19).  All kernels here
+// keep that exact per-index order, so results are bit-identical.
+//
+// dense_accumulate : records are dense (client c, slot j has idx j — the
+//   serialize_dense layout, utils.py:171-190).  One thread owns 2*V adjacent
+//   outputs, walks the n clients in order with 16-B non-temporal loads, U
+//   clients in flight.  HBM-read bound: n*d*8 + d*4 bytes per launch.  The
+//   access pattern does not depend on the data (every record is read once at
+//   a fixed address), so it is oblivious; idx != position is reported, not
+//   followed (FLTEE_DEV_ERR_DENSE_ORDER).
+// sweep_materialize + rows_accumulate : sparse records, oblivious.  GPU form of
+//   baseline.rs's o_update: every record of client c is compared against every
+//   output slot (LDS broadcast + branch-free select), producing the dense row
+//   mat[c][0..d) of client c; the rows are then summed in client order.  Exact
+//   while a client's indices are distinct (top-k, utils.py:327-354); a client
+//   with a repeated index sets FLTEE_DEV_ERR_FOLD_OVERFLOW and the host reruns
+//   sweep_sequential (one output per lane, all records in order).
+#include "common.h"
+
+namespace fltee {
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// streaming (non-temporal) loads: every byte is read exactly once
+static __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+static __device__ __forceinline__ uint2 ld_nt(const uint2 *p) {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t *>(p));
+    return make_uint2(v.x, v.y);
+}
+static __device__ __forceinline__ float4 ld_nt(const float4 *p) {
+    const f32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// ---------------------------------------------------------------- dense ----
+// rec viewed as uint4 = two records {idx0, val0, idx1, val1}; row stride d2 = d/2.
+template <int V, int U, bool CLIP, bool ACC>
+__global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
+                                                          uint32_t n, float coef,
+                                                          float *__restrict__ out,
+                                                          const float *__restrict__ ccoef,
+                                                          uint32_t *status) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t col0 = t * V;
+    if (col0 >= d2) return;
+    const int nv = (col0 + V <= d2) ? V : (int)(d2 - col0);
+    float acc[2 * V];
+#pragma unroll
+    for (int i = 0; i < 2 * V; ++i) acc[i] = 0.0f;
+    uint32_t bad = 0;
+    const uint32_t j0 = (uint32_t)(2 * col0);
+    const uint4 *p = rec + col0;
+    uint32_t c = 0;
+    if (nv == V) {
+        for (; c + U <= n; c += U) {
+            uint4 x[U][V];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[u][v] = ld_nt(p + (size_t)(c + u) * d2 + v);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float cc = CLIP ? ccoef[c + u] : 1.0f;
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    float a = __uint_as_float(x[u][v].y), b = __uint_as_float(x[u][v].w);
+                    if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
+                    acc[2 * v] = __fadd_rn(acc[2 * v], a);
+                    acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
+                    bad |= (x[u][v].x ^ (j0 + 2 * v)) | (x[u][v].z ^ (j0 + 2 * v + 1));
+                }
+            }
+        }
+    }
+    for (; c < n; ++c) {
+        float cc = CLIP ? ccoef[c] : 1.0f;
+        for (int v = 0; v < nv; ++v) {
+            uint4 x = ld_nt(p + (size_t)c * d2 + v);
+            float a = __uint_as_float(x.y), b = __uint_as_float(x.w);
+            if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
+            acc[2 * v] = __fadd_rn(acc[2 * v], a);
+            acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
+            bad |= (x.x ^ (j0 + 2 * v)) | (x.z ^ (j0 + 2 * v + 1));
+        }
+    }
+    float2 *o = reinterpret_cast<float2 *>(out) + col0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        if (v < nv) {
+            float2 r;
+            if (ACC) {
+                float2 prev = o[v];
+                r = make_float2(__fadd_rn(prev.x, acc[2 * v]), __fadd_rn(prev.y, acc[2 * v + 1]));
+            } else {
+                r = make_float2(__fmul_rn(acc[2 * v], coef), __fmul_rn(acc[2 * v + 1], coef));
+            }
+            o[v] = r;
+        }
+    }
+    if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
+// odd d or misaligned base: one record (8 B) per lane per client.
+template <bool CLIP, bool ACC>
+__global__ __launch_bounds__(256) void dense_accumulate_s(const uint2 *__restrict__ rec, size_t d,
+                                                          uint32_t n, float coef,
+                                                          float *__restrict__ out,
+                                                          const float *__restrict__ ccoef,
+                                                          uint32_t *status) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= d) return;
+    float acc = 0.0f;
+    uint32_t bad = 0;
+    for (uint32_t c = 0; c < n; ++c) {
+        uint2 x = ld_nt(rec + (size_t)c * d + j);
+        float a = __uint_as_float(x.y);
+        if (CLIP) a = __fmul_rn(a, ccoef[c]);
+        acc = __fadd_rn(acc, a);
+        bad |= x.x ^ (uint32_t)j;
+    }
+    out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+    if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
+template <bool CLIP, bool ACC>
+static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef, float *out,
+                                 const float *ccoef, uint32_t *status, hipStream_t s) {
+    const bool aligned = ((uintptr_t)rec % 16 == 0) && ((uintptr_t)out % 8 == 0) && (d % 2 == 0);
+    if (aligned) {
+        const size_t d2 = d / 2;
+        constexpr int V = 1, U = 16;
+        const size_t threads = (d2 + V - 1) / V;
+        const unsigned blocks = (unsigned)((threads + 255) / 256);
+        hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
+                           (const uint4 *)rec, d2, (uint32_t)n, coef, out, ccoef, status);
+    } else {
+        const unsigned blocks = (unsigned)((d + 255) / 256);
+        hipLaunchKernelGGL((dense_accumulate_s<CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
+                           (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,
+                                   const float *client_coef, bool accumulate, uint32_t *status,
+                                   hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    if (client_coef)
+        return accumulate ? dense_dispatch<true, true>(rec, n, d, coef, out, client_coef, status, s)
+                          : dense_dispatch<true, false>(rec, n, d, coef, out, client_coef, status, s);
+    return accumulate ? dense_dispatch<false, true>(rec, n, d, coef, out, nullptr, status, s)
+                      : dense_dispatch<false, false>(rec, n, d, coef, out, nullptr, status, s);
+}
+
+// ---------------------------------------------------------------- sparse ---
+// Oblivious sweep, one client per blockIdx.y: row[c][j] = sum of client c's
+// records with idx == j (in the client's order), matches counted.
+constexpr int SW_R = 4;          // outputs per lane
+constexpr int SW_CHUNK = 2048;   // records staged per LDS pass (16 KB)
+
+__global__ __launch_bounds__(256) void sweep_materialize(const uint2 *__restrict__ rec, size_t k,
+                                                         size_t d, float *__restrict__ mat,
+                                                         uint32_t *status) {
+    __shared__ uint2 tile[SW_CHUNK];
+    const uint32_t c = blockIdx.y;
+    const uint32_t base = (uint32_t)(((size_t)blockIdx.x * 256 + threadIdx.x) * SW_R);
+    const uint2 *src = rec + (size_t)c * k;
+    float acc[SW_R];
+    uint32_t cnt[SW_R];
+#pragma unroll
+    for (int i = 0; i < SW_R; ++i) { acc[i] = 0.0f; cnt[i] = 0; }
+    for (size_t c0 = 0; c0 < k; c0 += SW_CHUNK) {
+        const uint32_t m = (uint32_t)((k - c0) < SW_CHUNK ? (k - c0) : SW_CHUNK);
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < m; e += 256) tile[e] = src[c0 + e];
+        __syncthreads();
+        for (uint32_t q = 0; q < m; ++q) {
+            const uint2 r = tile[q];
+            const uint32_t delta = r.x - base;
+            const float v = __uint_as_float(r.y);
+#pragma unroll
+            for (int i = 0; i < SW_R; ++i) {
+                const bool hit = (delta == (uint32_t)i);
+                acc[i] = __fadd_rn(acc[i], hit ? v : 0.0f);
+                cnt[i] += hit;
+            }
+        }
+    }
+    uint32_t dup = 0;
+    float *row = mat + (size_t)c * d;
+#pragma unroll
+    for (int i = 0; i < SW_R; ++i) {
+        if ((size_t)base + i < d) row[base + i] = acc[i];
+        dup |= cnt[i] > 1;
+    }
+    if (dup) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+}
+
+// rows [n][d] f32 summed in row order: out[j] = sum_c mat[c][j] (* coef)
+template <int U, bool ACC>
+__global__ __launch_bounds__(256) void rows_accumulate(const float4 *__restrict__ mat, size_t d4,
+                                                       uint32_t n, float coef,
+                                                       float4 *__restrict__ out) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= d4) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t c = 0;
+    for (; c + U <= n; c += U) {
+        float4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld_nt(mat + (size_t)(c + u) * d4 + t);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc.x = __fadd_rn(acc.x, x[u].x); acc.y = __fadd_rn(acc.y, x[u].y);
+            acc.z = __fadd_rn(acc.z, x[u].z); acc.w = __fadd_rn(acc.w, x[u].w);
+        }
+    }
+    for (; c < n; ++c) {
+        float4 x = ld_nt(mat + (size_t)c * d4 + t);
+        acc.x = __fadd_rn(acc.x, x.x); acc.y = __fadd_rn(acc.y, x.y);
+        acc.z = __fadd_rn(acc.z, x.z); acc.w = __fadd_rn(acc.w, x.w);
+    }
+    if (ACC) {
+        float4 p = out[t];
+        out[t] = make_float4(__fadd_rn(p.x, acc.x), __fadd_rn(p.y, acc.y), __fadd_rn(p.z, acc.z),
+                             __fadd_rn(p.w, acc.w));
+    } else {
+        out[t] = make_float4(__fmul_rn(acc.x, coef), __fmul_rn(acc.y, coef),
+                             __fmul_rn(acc.z, coef), __fmul_rn(acc.w, coef));
+    }
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(256) void rows_accumulate_s(const float *__restrict__ mat, size_t d,
+                                                         uint32_t n, float coef,
+                                                         float *__restrict__ out) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= d) return;
+    float acc = 0.0f;
+    for (uint32_t c = 0; c < n; ++c) acc = __fadd_rn(acc, mat[(size_t)c * d + j]);
+    out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+}
+
+// Exact fallback for clients with repeated indices: one output per lane,
+// every record in upload order (the literal o_update loop, parallel over j).
+template <bool ACC>
+__global__ __launch_bounds__(256) void sweep_sequential(const uint2 *__restrict__ rec, size_t nrec,
+                                                        size_t d, float coef,
+                                                        float *__restrict__ out) {
+    __shared__ uint2 tile[SW_CHUNK];
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    float acc = 0.0f;
+    for (size_t c0 = 0; c0 < nrec; c0 += SW_CHUNK) {
+        const uint32_t m = (uint32_t)((nrec - c0) < SW_CHUNK ? (nrec - c0) : SW_CHUNK);
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < m; e += 256) tile[e] = rec[c0 + e];
+        __syncthreads();
+        for (uint32_t q = 0; q < m; ++q) {
+            const uint2 r = tile[q];
+            acc = __fadd_rn(acc, (r.x == (uint32_t)j) ? __uint_as_float(r.y) : 0.0f);
+        }
+    }
+    if (j < d) out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+}
+
+hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t d, float *mat,
+                                    uint32_t *status, hipStream_t s) {
+    if (n == 0 || d == 0) return hipSuccess;
+    const unsigned bx = (unsigned)((d + 256 * SW_R - 1) / (256 * SW_R));
+    hipLaunchKernelGGL(sweep_materialize, dim3(bx, (unsigned)n), dim3(256), 0, s,
+                       (const uint2 *)rec, k, d, mat, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
+                                  bool accumulate, hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    if (d % 4 == 0 && (uintptr_t)out % 16 == 0) {
+        const size_t d4 = d / 4;
+        const unsigned blocks = (unsigned)((d4 + 255) / 256);
+        if (accumulate)
+            hipLaunchKernelGGL((rows_accumulate<8, true>), dim3(blocks), dim3(256), 0, s,
+                               (const float4 *)mat, d4, (uint32_t)n, coef, (float4 *)out);
+        else
+            hipLaunchKernelGGL((rows_accumulate<8, false>), dim3(blocks), dim3(256), 0, s,
+                               (const float4 *)mat, d4, (uint32_t)n, coef, (float4 *)out);
+    } else {
+        const unsigned blocks = (unsigned)((d + 255) / 256);
+        if (accumulate)
+            hipLaunchKernelGGL(rows_accumulate_s<true>, dim3(blocks), dim3(256), 0, s, mat, d,
+                               (uint32_t)n, coef, out);
+        else
+            hipLaunchKernelGGL(rows_accumulate_s<false>, dim3(blocks), dim3(256), 0, s, mat, d,
+                               (uint32_t)n, coef, out);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float coef, float *out,
+                                   bool accumulate, uint32_t *status, hipStream_t s) {
+    (void)status;
+    if (d == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((d + 255) / 256);
+    if (accumulate)
+        hipLaunchKernelGGL(sweep_sequential<true>, dim3(blocks), dim3(256), 0, s,
+                           (const uint2 *)rec, nrec, d, coef, out);
+    else
+        hipLaunchKernelGGL(sweep_sequential<false>, dim3(blocks), dim3(256), 0, s,
+                           (const uint2 *)rec, nrec, d, coef, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------- helpers -----
+__global__ void scale_kernel(float *out, size_t d, float coef) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < d) out[j] = __fmul_rn(out[j], coef);
+}
+
+hipError_t launch_scale(float *out, size_t d, float coef, hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, out, d,
+                       coef);
+    return hipGetLastError();
+}
+
+// status |= INDEX_RANGE if any record idx >= limit
+__global__ void check_range_kernel(const uint2 *rec, size_t nrec, uint32_t limit,
+                                   uint32_t *status) {
+    uint32_t bad = 0;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < nrec; e += (size_t)gridDim.x * 256)
+        bad |= rec[e].x >= limit;
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, FLTEE_DEV_ERR_INDEX_RANGE);
+}
+
+hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint32_t *status,
+                              hipStream_t s) {
+    if (nrec == 0) return hipSuccess;
+    size_t blocks = (nrec + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(check_range_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint2 *)rec, nrec, limit, status);
+    return hipGetLastError();
+}
+
+}  // namespace fltee

@@ -1,0 +1,118 @@
+// k_nips19.hip — alg 2 (nips19.rs:18-63, common.rs:25-35,77-98,151-197) on gfx950.
+//
+//   laplace_r      : r_i from one Laplace(b = 2k/eps) draw per parameter, cut at
+//                    T = (2k/eps) ln(d/delta), eps = 100, delta = 1/n (f32 math
+//                    as in the enclave; the uniform comes from Philox4x32-10
+//                    instead of RDRAND-seeded sgx_rand — see DESIGN.md)
+//   nips19_build   : records ++ d*floor(T) dummies, entry (i, j) =
+//                    ((r_i < j) ? i : u32::MAX, 0.0) (oblivious_pad, branch-free)
+//                    ++ (u32::MAX, 0.0) pads to 2^m
+//   [bitonic network, mode 2 = keyed shuffle]
+//   safe_aggregate : g[idx] += val for idx < d in shuffled order.  Every entry
+//                    with idx < d is added (dummies add +0.0), exactly the
+//                    access histogram the enclave reveals.  Sums go through
+//                    LDS float atomics per (chunk, d-segment) and one global
+//                    atomic per slot per chunk, so the per-index summation
+//                    order is not the enclave's: parity is within fp32
+//                    tolerance (the enclave's own order is random anyway).
+#include "common.h"
+
+namespace fltee {
+
+__device__ __forceinline__ uint32_t f32_to_u32_sat(float x) {
+    if (!(x > 0.0f)) return 0u;
+    if (x >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)x;
+}
+
+__global__ void laplace_r_kernel(size_t d, float b, float T, uint32_t k0, uint32_t k1,
+                                 uint32_t *__restrict__ r) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= d) return;
+    uint32_t c[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), 0u, FLTEE_STREAM_LAPLACE};
+    philox4x32_10(c, k0, k1);
+    const float p = (float)(c[0] >> 8) * (1.0f / 16777216.0f);
+    const float noise = p > 0.5f ? -b * logf(2.0f - 2.0f * p) : b * logf(2.0f * p);
+    r[i] = fabsf(noise) > T ? f32_to_u32_sat(ceilf(T)) : f32_to_u32_sat(T + ceilf(noise));
+}
+
+hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t *r,
+                            hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    const float b = 2.0f * (float)k / 100.0f;
+    hipLaunchKernelGGL(laplace_r_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, d, b,
+                       T, (uint32_t)seed, (uint32_t)(seed >> 32), r);
+    return hipGetLastError();
+}
+
+__global__ void nips19_build_kernel(const uint64_t *__restrict__ rec, size_t nrec,
+                                    const uint32_t *__restrict__ r, size_t d, size_t tf, size_t m,
+                                    uint64_t *__restrict__ dst) {
+    const size_t npad = d * tf;
+    for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (size_t)gridDim.x * 256) {
+        uint64_t v;
+        if (p < nrec) {
+            v = rec[p];
+        } else if (p < nrec + npad) {
+            const size_t e = p - nrec;
+            const size_t i = e / tf, j = e - i * tf;
+            const uint32_t ri = r[i];
+            v = ((size_t)ri < j) ? (uint64_t)(uint32_t)i : (uint64_t)0xFFFFFFFFu;  // o_setb/o_mov
+        } else {
+            v = (uint64_t)0xFFFFFFFFu;
+        }
+        dst[p] = v;
+    }
+}
+
+hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, size_t d,
+                               size_t tf, size_t m, uint64_t *dst, hipStream_t s) {
+    size_t blocks = (m + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(nips19_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint64_t *)rec, nrec, r, d, tf, m, dst);
+    return hipGetLastError();
+}
+
+constexpr uint32_t SA_SEG = 32768;  // floats per LDS segment (128 KB)
+constexpr uint32_t SA_CHUNKS = 256;
+
+__global__ __launch_bounds__(1024) void safe_aggregate_kernel(const uint2 *__restrict__ src,
+                                                              size_t m, size_t d,
+                                                              float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float acc[];
+    const size_t seg_lo = (size_t)blockIdx.y * SA_SEG;
+    const uint32_t seg_n = (uint32_t)((d - seg_lo) < SA_SEG ? (d - seg_lo) : SA_SEG);
+    for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) acc[e] = 0.0f;
+    __syncthreads();
+    const size_t per = (m + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * per;
+    const size_t hi = lo + per < m ? lo + per : m;
+    for (size_t p = lo + threadIdx.x; p < hi; p += 1024) {
+        const uint2 w = src[p];
+        const uint32_t rel = w.x - (uint32_t)seg_lo;
+        if (w.x < d && rel < seg_n) atomicAdd(&acc[rel], __uint_as_float(w.y));
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) atomicAdd(&out[seg_lo + e], acc[e]);
+}
+
+hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float *out,
+                                 hipStream_t s) {
+    if (d == 0 || m == 0) return hipSuccess;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)safe_aggregate_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SA_SEG * 4);
+        attr = true;
+    }
+    const unsigned segs = (unsigned)((d + SA_SEG - 1) / SA_SEG);
+    size_t chunks = (m + 8191) / 8192;
+    if (chunks > SA_CHUNKS) chunks = SA_CHUNKS;
+    const size_t lds = (d < SA_SEG ? d : SA_SEG) * 4;
+    hipLaunchKernelGGL(safe_aggregate_kernel, dim3((unsigned)chunks, segs), dim3(1024), lds, s,
+                       (const uint2 *)src, m, d, out);
+    return hipGetLastError();
+}
+
+}  // namespace fltee

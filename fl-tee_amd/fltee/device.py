@@ -1,0 +1,110 @@
+"""Device-resident entry points of libfltee_agg.so on torch tensors.
+
+PyTorch only supplies HBM allocations, the stream and torch.distributed; all
+arithmetic runs in the library's HIP kernels.  Records are int64 tensors whose
+bytes are the enclave's Weight layout (parameters.rs:9): low 32 bits u32 idx,
+high 32 bits f32 val (little-endian), client-major in upload order.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def pack_records(idx, val):
+    """(u32 idx, f32 val) arrays -> int64 numpy array of Weight records."""
+    idx = np.ascontiguousarray(idx, dtype=np.uint32)
+    val = np.ascontiguousarray(val, dtype=np.float32)
+    rec = np.empty(len(idx), dtype=np.uint64)
+    rec[:] = idx.astype(np.uint64) | (val.view(np.uint32).astype(np.uint64) << np.uint64(32))
+    return rec.view(np.int64)
+
+
+def unpack_records(rec):
+    r = np.ascontiguousarray(rec).view(np.uint64)
+    return (r & np.uint64(0xFFFFFFFF)).astype(np.uint32), (r >> np.uint64(32)).astype(np.uint32).view(np.float32)
+
+
+def opts(*, dense=False, dp=False, clip=False, accumulate=False, no_average=False, sigma=1.12,
+         clipping=1.0, seed=0, k_req=0, batch=0, n_avg=0, fold_halo=0, status=None):
+    o = L.DeviceOpts()
+    o.flags = ((L.OPT_DENSE if dense else 0) | (L.OPT_DP if dp else 0) | (L.OPT_CLIP if clip else 0)
+               | (L.OPT_ACCUMULATE if accumulate else 0) | (L.OPT_NO_AVERAGE if no_average else 0))
+    o.sigma, o.clipping, o.seed = sigma, clipping, seed
+    o.k_req, o.batch, o.n_avg, o.fold_halo = k_req, batch, n_avg, fold_halo
+    o.d_status = status.data_ptr() if status is not None else None
+    return o
+
+
+def _check(st, what):
+    if st != L.SUCCESS:
+        raise RuntimeError(f"{what} failed with status {st:#x}")
+
+
+def aggregate(alg, records, n, k, d, out=None, stream=None, **kw):
+    """fltee_aggregate_device: aggregate n x k records (int64 cuda tensor) into out[d] (f32)."""
+    assert records.is_cuda and records.dtype == torch.int64 and records.numel() >= n * k
+    if out is None:
+        out = torch.empty(d, dtype=torch.float32, device=records.device)
+    o = opts(**kw)
+    st = L.lib().fltee_aggregate_device(alg, _ptr(records), n, k, d, _ptr(out), ctypes.byref(o),
+                                        _stream(stream))
+    _check(st, "fltee_aggregate_device")
+    return out
+
+
+def reserve(alg, n, k, d, **kw):
+    o = opts(**kw)
+    _check(L.lib().fltee_reserve(alg, n, k, d, ctypes.byref(o)), "fltee_reserve")
+
+
+def workspace_bytes(alg, n, k, d, **kw):
+    o = opts(**kw)
+    return L.lib().fltee_workspace_bytes(alg, n, k, d, ctypes.byref(o))
+
+
+def status(stream=None):
+    """Synchronise and return (and clear) the library-owned device status word."""
+    v = ctypes.c_uint32(0)
+    _check(L.lib().fltee_device_status(_stream(stream), ctypes.byref(v)), "fltee_device_status")
+    return v.value
+
+
+def bitonic(records, mode, seed=0, stream=None):
+    m = records.numel()
+    _check(L.lib().fltee_bitonic_device(_ptr(records), m, mode, seed, _stream(stream)),
+           "fltee_bitonic_device")
+    return records
+
+
+def fold(src, dst, fold_len, halo, status_word, stream=None):
+    _check(L.lib().fltee_fold_device(_ptr(src), _ptr(dst), src.numel(), fold_len, halo,
+                                     _ptr(status_word), _stream(stream)), "fltee_fold_device")
+    return dst
+
+
+def decrypt(client_ids, cipher, bytes_per_client, records, stream=None):
+    ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
+    _check(L.lib().fltee_decrypt_device(ids.ctypes.data_as(ctypes.c_void_p), len(ids),
+                                        _ptr(cipher), bytes_per_client, _ptr(records),
+                                        _stream(stream)), "fltee_decrypt_device")
+    return records
+
+
+def laplace_r(d, k, n, seed, device="cuda", stream=None):
+    r = torch.empty(d, dtype=torch.int32, device=device)
+    T = ctypes.c_float(0)
+    _check(L.lib().fltee_laplace_r_device(d, k, n, seed, _ptr(r), ctypes.byref(T),
+                                          _stream(stream)), "fltee_laplace_r_device")
+    return r, T.value

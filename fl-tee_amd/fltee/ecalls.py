@@ -1,0 +1,90 @@
+"""Host-side mirror of secure_aggregation/app/src/ecalls.rs over the C ABI.
+
+`Enclave` replaces `init_enclave()` / `SgxEnclave` (ecalls.rs:66-83) and
+exposes the four ECALLs with the argument meaning of ecalls.rs:6-64.  Each
+method returns `(bridge_status, retval, ...)` exactly like the Rust host sees
+them (`result`, `retval`): the server panics unless both are SUCCESS
+(server.rs:80-82,96-98,159-161,180-182,202-204).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Enclave:
+    def __init__(self, device=0):
+        self.lib = L.lib()
+        eid = ctypes.c_uint64(0)
+        st = self.lib.fltee_device_init(device, ctypes.byref(eid))
+        if st != L.SUCCESS:
+            raise RuntimeError(f"fltee_device_init({device}) failed: {st:#x}")
+        self.eid = eid.value
+
+    def geteid(self):
+        return self.eid
+
+    def destroy(self):
+        if self.eid:
+            self.lib.fltee_device_fini(self.eid)
+            self.eid = 0
+
+    # lib.rs:113-180
+    def ecall_fl_init(self, fl_id, client_ids, num_of_parameters, num_of_sparse_parameters,
+                      sigma, clipping, alpha, sampling_ratio, aggregation_alg, verbose, dp):
+        ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
+        rv = ctypes.c_uint32(0xFFFFFFFF)
+        st = self.lib.ecall_fl_init(self.eid, ctypes.byref(rv), fl_id, _p(ids), len(ids),
+                                    num_of_parameters, num_of_sparse_parameters, sigma, clipping,
+                                    alpha, sampling_ratio, aggregation_alg, int(verbose), int(dp))
+        return st, rv.value
+
+    # lib.rs:182-219
+    def ecall_start_round(self, fl_id, round_, sample_size):
+        out = np.zeros(max(sample_size, 1), dtype=np.uint32)
+        rv = ctypes.c_uint32(0xFFFFFFFF)
+        st = self.lib.ecall_start_round(self.eid, ctypes.byref(rv), fl_id, round_, sample_size,
+                                        _p(out))
+        return st, rv.value, out[:sample_size]
+
+    # lib.rs:221-423
+    def ecall_secure_aggregation(self, fl_id, round_, client_ids, encrypted_parameters,
+                                 num_of_parameters, num_of_sparse_parameters, aggregation_alg):
+        ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
+        enc = np.frombuffer(bytes(encrypted_parameters), dtype=np.uint8)
+        out = np.full(num_of_parameters, np.nan, dtype=np.float32)
+        times = np.full(3, np.nan, dtype=np.float32)
+        rv = ctypes.c_uint32(0xFFFFFFFF)
+        st = self.lib.ecall_secure_aggregation(
+            self.eid, ctypes.byref(rv), fl_id, round_, _p(ids), len(ids), _p(enc), enc.nbytes,
+            num_of_parameters, num_of_sparse_parameters, aggregation_alg, _p(out), _p(times))
+        return st, rv.value, out, times
+
+    # lib.rs:425-592
+    def ecall_client_size_optimized_secure_aggregation(self, fl_id, round_, optimal_num_of_clients,
+                                                       client_ids, encrypted_parameters,
+                                                       num_of_parameters, num_of_sparse_parameters,
+                                                       aggregation_alg):
+        ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
+        enc = np.frombuffer(bytes(encrypted_parameters), dtype=np.uint8)
+        need = len(ids) * num_of_sparse_parameters * 8
+        if enc.nbytes < need:  # [user_check]: the enclave would read past the buffer
+            raise ValueError(f"payload has {enc.nbytes} bytes, alg 6 reads {need}")
+        out = np.full(num_of_parameters, np.nan, dtype=np.float32)
+        times = np.full(3, np.nan, dtype=np.float32)
+        rv = ctypes.c_uint32(0xFFFFFFFF)
+        st = self.lib.ecall_client_size_optimized_secure_aggregation(
+            self.eid, ctypes.byref(rv), fl_id, round_, optimal_num_of_clients, _p(ids), len(ids),
+            _p(enc), num_of_parameters, num_of_sparse_parameters, aggregation_alg, _p(out),
+            _p(times))
+        return st, rv.value, out, times
+
+
+def set_debug_seed(seed):
+    """Deterministic RNG for sampling / nips19 / DP (tests only; 0 restores RDRAND-like)."""
+    L.lib().fltee_debug_set_seed(seed)

@@ -1,0 +1,192 @@
+/*
+ * fltee_agg.h — C ABI of libfltee_agg.so, the MI355X-native replacement for
+ * FL-TEE's SGX aggregation enclave (secure_aggregation/enclave).
+ *
+ * Drop-in boundary.  The four ECALLs below keep the exact symbol names and
+ * argument lists that the Rust host binds in
+ *     secure_aggregation/app/src/ecalls.rs:6-64
+ * (EDL contract: secure_aggregation/enclave/Enclave.edl:23-84), including the
+ * leading (eid, *retval) pair that sgx_edger8r's untrusted bridge adds.  A host
+ * that linked the edger8r bridge (app/Enclave_u.c) links this library instead;
+ * see INTEGRATION.md for the ecalls.rs / build.rs diff.
+ *
+ * Conventions:
+ *   - return value  = "bridge" status: always FLTEE_SUCCESS for an in-process
+ *                     call (the SGX bridge could fail; this one cannot), except
+ *                     FLTEE_ERROR_INVALID_ENCLAVE_ID for an unknown eid.
+ *   - *retval       = the enclave's status: 0 success, 0x1 unexpected
+ *                     (unknown fl_id / missing session key / device failure),
+ *                     0x2 invalid parameter (round / alg / id-set / size
+ *                     mismatch, and every case where the reference enclave
+ *                     would panic: unknown alg (lib.rs:396), out-of-range
+ *                     index in non_oblivious (non_oblivious.rs:12), fold
+ *                     longer than the payload (advanced.rs:70-72)).
+ *   - ownership     : the caller owns every buffer; nothing is retained.
+ *   - [out] buffers : zero-filled by the callee before anything else (the SGX
+ *                     bridge did this, Enclave_t.c:626); execution_time_results
+ *                     is always fully written.
+ *   - threading     : calls may arrive from any thread (tokio workers,
+ *                     server.rs:241-245); the library serialises them with one
+ *                     process-wide mutex (the enclave had one TCS,
+ *                     Enclave.config.xml:6) and binds the eid's device per call.
+ */
+#ifndef FLTEE_AGG_H
+#define FLTEE_AGG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* sgx_status_t subset (sgx_error.h values) */
+typedef uint32_t fltee_status_t;
+#define FLTEE_SUCCESS 0x0000u
+#define FLTEE_ERROR_UNEXPECTED 0x0001u
+#define FLTEE_ERROR_INVALID_PARAMETER 0x0002u
+#define FLTEE_ERROR_OUT_OF_MEMORY 0x0003u
+#define FLTEE_ERROR_INVALID_ENCLAVE_ID 0x2002u
+
+/* sgx_enclave_id_t */
+typedef uint64_t fltee_eid_t;
+
+/* aggregation_alg codes, src/option.py:131-145 */
+#define FLTEE_ALG_ADVANCED 1u
+#define FLTEE_ALG_NIPS19 2u
+#define FLTEE_ALG_BASELINE 3u
+#define FLTEE_ALG_NON_OBLIVIOUS 4u
+#define FLTEE_ALG_PATH_ORAM 5u
+#define FLTEE_ALG_OPTIMIZED 6u
+
+/* ------------------------------------------------------------------------ */
+/* Device lifetime — replaces init_enclave() / SgxEnclave::destroy()         */
+/* (app/src/ecalls.rs:66-83, server.rs:224-235,257).                          */
+/* ------------------------------------------------------------------------ */
+fltee_status_t fltee_device_init(int hip_device, fltee_eid_t *eid);
+fltee_status_t fltee_device_fini(fltee_eid_t eid);
+
+/* ------------------------------------------------------------------------ */
+/* The four ECALLs (ecalls.rs:6-64 / Enclave.edl:26-73)                      */
+/* ------------------------------------------------------------------------ */
+
+/* lib.rs:113-180 — (re)create the config of fl_id, mock session keys. */
+fltee_status_t ecall_fl_init(fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id,
+                             const uint32_t *client_ids, size_t client_size,
+                             size_t num_of_parameters, size_t num_of_sparse_parameters,
+                             float sigma, float clipping, float alpha, float sampling_ratio,
+                             uint32_t aggregation_alg, uint8_t verbose, uint8_t dp);
+
+/* lib.rs:182-219 — sample (|ids| * ratio) clients for `round`.  The EDL types
+ * sample_size as uint32_t (Enclave.edl:72) but Rust passes usize
+ * (ecalls.rs:29): size_t is accepted. */
+fltee_status_t ecall_start_round(fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id,
+                                 uint32_t round, size_t sample_size,
+                                 uint32_t *sampled_client_ids);
+
+/* lib.rs:221-423 — load (H2D), decrypt (AES-128-CTR on the GPU), aggregate
+ * with `aggregation_alg`, optional DP noise; writes the averaged f32[d] and
+ * execution_time_results[3] = {load, decrypt, aggregate} seconds. */
+fltee_status_t ecall_secure_aggregation(fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id,
+                                        uint32_t round, const uint32_t *client_ids,
+                                        size_t client_size,
+                                        const uint8_t *encrypted_parameters_data,
+                                        size_t encrypted_parameters_size,
+                                        size_t num_of_parameters,
+                                        size_t num_of_sparse_parameters,
+                                        uint32_t aggregation_alg,
+                                        float *updated_parameters_data,
+                                        float *execution_time_results);
+
+/* lib.rs:425-592 — alg 6: `advanced` over batches of optimal_num_of_clients
+ * clients; the payload pointer is [user_check]: client_size * k * 8 bytes are
+ * read. execution_time_results = {load, decrypt+aggregate, 0}. */
+fltee_status_t ecall_client_size_optimized_secure_aggregation(
+    fltee_eid_t eid, fltee_status_t *retval, uint32_t fl_id, uint32_t round,
+    size_t optimal_num_of_clients, const uint32_t *client_ids, size_t client_size,
+    const uint8_t *encrypted_parameters_data_ptr, size_t num_of_parameters,
+    size_t num_of_sparse_parameters, uint32_t aggregation_alg, float *updated_parameters_data,
+    float *execution_time_results);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident entry points: the aggregation below the ECALL, on records */
+/* already decrypted into HBM.  Used by the bench (device-resident metric),  */
+/* the multi-GPU driver and the parity tests.  All pointers are device       */
+/* pointers; `stream` is a hipStream_t (NULL = legacy default stream).       */
+/* Calls are asynchronous: errors found on the device are OR-ed into the     */
+/* 32-bit status word (opts.d_status, or the library's own word read back by */
+/* fltee_device_status()).                                                    */
+/* ------------------------------------------------------------------------ */
+
+/* device status bits */
+#define FLTEE_DEV_ERR_DENSE_ORDER 0x1u   /* dense input with idx != position */
+#define FLTEE_DEV_ERR_INDEX_RANGE 0x2u   /* idx >= d where the reference panics */
+#define FLTEE_DEV_ERR_FOLD_OVERFLOW 0x4u /* a run longer than the fold halo */
+#define FLTEE_DEV_ERR_LAUNCH 0x80000000u
+
+/* option flags */
+#define FLTEE_OPT_DENSE 0x1u      /* records are dense: client c, slot j has idx j */
+#define FLTEE_OPT_DP 0x2u         /* add N(0, clipping*sigma)/n noise (common.rs:56-72) */
+#define FLTEE_OPT_CLIP 0x4u       /* server-side per-client L2 clip (update.py:187-204) */
+#define FLTEE_OPT_ACCUMULATE 0x8u /* out += sum (no averaging): alg-6 batches, shards */
+#define FLTEE_OPT_NO_AVERAGE 0x10u /* skip the 1/n scaling (partial sums for RCCL) */
+
+typedef struct fltee_device_opts {
+    uint32_t flags;     /* FLTEE_OPT_* */
+    float sigma;        /* DP noise multiplier */
+    float clipping;     /* DP / clip norm bound C */
+    uint64_t seed;      /* RNG seed for nips19 / DP; 0 = draw from getrandom() */
+    size_t k_req;       /* advanced: request num_of_sparse_parameters (fold length n*k_req+d) */
+    size_t batch;       /* alg 6: optimal_num_of_clients */
+    size_t n_avg;       /* divisor for averaging (0 = n) */
+    size_t fold_halo;   /* advanced fold halo H (0 = n, exact when each client's indices are distinct) */
+    uint32_t *d_status; /* optional device status word (never cleared by the library) */
+} fltee_device_opts;
+
+/* Aggregate n clients x k records (8 B each: u32 LE idx, f32 LE val),
+ * client-major, into d_out[d] (overwritten, or accumulated with
+ * FLTEE_OPT_ACCUMULATE).  Returns FLTEE_ERROR_INVALID_PARAMETER for
+ * host-detectable argument errors. */
+fltee_status_t fltee_aggregate_device(uint32_t alg, const void *d_records, size_t n, size_t k,
+                                      size_t d, float *d_out, const fltee_device_opts *opts,
+                                      void *stream);
+
+/* Bytes of scratch HBM the library will hold for this shape (grow-only). */
+size_t fltee_workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d,
+                             const fltee_device_opts *opts);
+/* Pre-size the scratch so the first timed call does no hipMalloc. */
+fltee_status_t fltee_reserve(uint32_t alg, size_t n, size_t k, size_t d,
+                             const fltee_device_opts *opts);
+
+/* AES-128-CTR decrypt of n client slices (bytes_per_client each, zero counter
+ * block per client, key = session key of client_ids[i]) into compact records
+ * (n * (bytes_per_client/8) * 8 bytes).  lib.rs:312-343. */
+fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n, const void *d_cipher,
+                                    size_t bytes_per_client, void *d_records, void *stream);
+
+/* Synchronise `stream` and return (and clear) the library's status word. */
+fltee_status_t fltee_device_status(void *stream, uint32_t *status);
+
+/* ---- intermediate stages, exposed for the permutation-parity tests ------ */
+/* In-place oblivious bitonic network on M = 2^m 8-byte records.
+ * mode 0: sort by u32 idx with the reference comparator (advanced.rs:147-176)
+ * mode 1: sort by the whole u64 (stable-by-construction composite keys)
+ * mode 2: keyed shuffle network (nips19.rs:66-105 structure, seed)          */
+fltee_status_t fltee_bitonic_device(void *d_records, size_t m, uint32_t mode, uint32_t seed,
+                                    void *stream);
+/* advanced.rs:66-101 fold over [0, fold_len) of src (length m) into dst. */
+fltee_status_t fltee_fold_device(const void *d_src, void *d_dst, size_t m, size_t fold_len,
+                                 size_t halo, uint32_t *d_status, void *stream);
+/* common.rs:77-98,151-161 — nips19 Laplace counts r[d] and threshold T. */
+fltee_status_t fltee_laplace_r_device(size_t d, size_t k, size_t n, uint64_t seed, uint32_t *d_r,
+                                      float *T_out, void *stream);
+
+/* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
+void fltee_debug_set_seed(uint64_t seed);
+/* Library build/version string. */
+const char *fltee_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLTEE_AGG_H */

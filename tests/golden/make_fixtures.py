@@ -1,0 +1,144 @@
+"""Generate the committed golden fixtures from the REFERENCE's own client code.
+
+Run in the build container only (it needs /root/reference):
+    python tests/golden/make_fixtures.py
+
+What it imports from the reference (read-only, never copied):
+  src/utils.py  : zero_except_top_k_weights, serialize_sparse, serialize_dense,
+                  encrypt_parameters, flatten_params, get_learnable_parameters
+  src/update.py : l2clipping, diff_weights
+  src/models.py : MLP (MLP-MNIST, d = 50,890)
+utils.py loads 'src/libsgx_enc.so' relative to the cwd at import time.  The
+prebuilt binary shipped in the reference is NEVER loaded: we run from a scratch
+cwd whose src/libsgx_enc.so is oracle/_ref/libsgx_enc.so, compiled by
+oracle/Makefile from the reference's own src/cpp/encryption.cpp.
+torchvision is absent here, so a stub module is injected (utils.py only uses it
+for dataset loaders, which are out of scope).
+
+Outputs (tests/golden/*.npz) hold inputs and the reference-produced bytes
+(plaintext records, ciphertext), plus the oracle's aggregates at generation
+time for regression.  Expected aggregates are from the oracle (the Rust enclave
+cannot run here): the aggregation arithmetic is parity-unpinned beyond the
+invariants in tests/test_oracle.py.
+"""
+import os
+import shutil
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF_SRC = "/root/reference/src"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle as O  # noqa: E402
+
+
+def import_reference():
+    O.build()
+    assert os.path.exists(O.REF_AES_PATH), "oracle/_ref/libsgx_enc.so missing"
+    scratch = tempfile.mkdtemp(prefix="fltee_fix_")
+    os.makedirs(os.path.join(scratch, "src"))
+    shutil.copy(O.REF_AES_PATH, os.path.join(scratch, "src", "libsgx_enc.so"))
+    tv = types.ModuleType("torchvision")
+    tv.datasets = types.SimpleNamespace()
+    tv.transforms = types.SimpleNamespace()
+    sys.modules["torchvision"] = tv
+    sys.path.insert(0, REF_SRC)
+    cwd = os.getcwd()
+    os.chdir(scratch)
+    try:
+        import models
+        import update
+        import utils
+    finally:
+        os.chdir(cwd)
+    return utils, update, models
+
+
+def perturbed_diff(model, seed, scale=0.01):
+    g = torch.Generator().manual_seed(seed)
+    diff = {}
+    for key, val in model.state_dict().items():
+        diff[key] = torch.randn(val.shape, generator=g) * scale
+    from collections import OrderedDict
+    return OrderedDict(diff)
+
+
+def main():
+    utils, update, models = import_reference()
+    torch.manual_seed(1)
+
+    # ---------------- MLP-MNIST sparse (alpha = 0.1), fl_main.py:221-238 ----------
+    model = models.MLP(dim_in=784, dim_hidden=64, dim_out=10)
+    buffer_names = utils.get_buffer_names(model)
+    d = utils.count_parameters(model)
+    alpha = 0.1
+    k = int(alpha * d)
+    client_ids = np.array([3, 17, 42, 99], dtype=np.uint32)
+    for clip in (False, True):
+        plain, enc, topk = [], [], []
+        for cid in client_ids:
+            diff = perturbed_diff(model, seed=1000 + int(cid))
+            top, idxs = utils.zero_except_top_k_weights(diff, buffer_names, k)
+            if clip:
+                top = update.l2clipping(top, buffer_names, 1.0)
+            b = utils.serialize_sparse(top, buffer_names, idxs)
+            e = bytes(utils.encrypt_parameters(b, int(cid)))
+            plain.append(np.frombuffer(b, dtype=np.uint8))
+            enc.append(np.frombuffer(e, dtype=np.uint8))
+            topk.append(np.asarray(idxs, dtype=np.uint32))
+        plain = np.concatenate(plain)
+        enc = np.concatenate(enc)
+        w = O.decrypt_and_parse(client_ids, enc)
+        n = len(client_ids)
+        g_non, _ = O.non_oblivious(w, d, n)
+        g_adv, _ = O.advanced(k, w, d, n)
+        name = "mnist_sparse_clip" if clip else "mnist_sparse"
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), client_ids=client_ids,
+                            plaintext=plain, ciphertext=enc, topk=np.stack(topk), d=d, k=k,
+                            alpha=alpha, oracle_non_oblivious=g_non, oracle_advanced=g_adv)
+        print(name, "d", d, "k", k, "bytes", enc.nbytes)
+
+    # ---------------- dense uploads (no --alpha): serialize_dense ---------------
+    small = torch.nn.Sequential(torch.nn.Linear(20, 10), torch.nn.ReLU(), torch.nn.Linear(10, 5))
+    bn = utils.get_buffer_names(small)
+    d2 = utils.count_parameters(small)
+    ids2 = np.array([0, 1, 7], dtype=np.uint32)
+    plain, enc = [], []
+    for cid in ids2:
+        diff = perturbed_diff(small, seed=2000 + int(cid))
+        b = utils.serialize_dense(diff, bn, d2)
+        e = bytes(utils.encrypt_parameters(b, int(cid)))
+        plain.append(np.frombuffer(b, dtype=np.uint8))
+        enc.append(np.frombuffer(e, dtype=np.uint8))
+    plain = np.concatenate(plain)
+    enc = np.concatenate(enc)
+    w = O.decrypt_and_parse(ids2, enc)
+    g_base = O.baseline(w, d2, len(ids2))
+    np.savez_compressed(os.path.join(OUT, "dense_small.npz"), client_ids=ids2, plaintext=plain,
+                        ciphertext=enc, d=d2, oracle_baseline=g_base)
+    print("dense_small d", d2)
+
+    # ---------------- l2clipping (update.py:187-204) on a full state dict -------
+    diff = perturbed_diff(model, seed=77, scale=0.05)
+    clipped = update.l2clipping(diff, buffer_names, 1.0)
+    flat_in = utils.flatten_params(utils.get_learnable_parameters(diff, buffer_names)).numpy()
+    flat_out = utils.flatten_params(utils.get_learnable_parameters(clipped, buffer_names)).numpy()
+    np.savez_compressed(os.path.join(OUT, "l2clip.npz"), flat_in=flat_in.astype(np.float32),
+                        flat_out=flat_out.astype(np.float32), clipping=1.0)
+    print("l2clip d", flat_in.size)
+
+    # ---------------- src/ffi_test.py known answer (100 x 0x01, key 0, IV 0) ----
+    src = bytes([1] * 100)
+    ct = O.ref_aes_ctr_encrypt(bytes(16), src)
+    np.savez_compressed(os.path.join(OUT, "ffi_test_kat.npz"), plaintext=np.frombuffer(src, np.uint8),
+                        ciphertext=np.frombuffer(ct, np.uint8))
+    print("ffi kat ok")
+
+
+if __name__ == "__main__":
+    main()

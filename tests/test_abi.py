@@ -1,0 +1,94 @@
+"""The C-ABI library loads and exports every symbol include/fltee_agg.h declares.
+
+CPU-only: no compute entry point is called (no GPU here), except the host-side
+AES block self-test which uses the same tables the device kernel stages in LDS.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "fltee_agg.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", text)) -
+                  {"defined", "sizeof"})
+
+
+def test_header_declares_the_four_ecalls():
+    names = declared_functions()
+    for ecall in ("ecall_fl_init", "ecall_start_round", "ecall_secure_aggregation",
+                  "ecall_client_size_optimized_secure_aggregation"):
+        assert ecall in names
+
+
+def test_library_exports_every_declared_symbol():
+    from fltee import _lib as L
+    lib = L.lib()
+    names = declared_functions()
+    assert names, "no declarations parsed"
+    for name in names:
+        assert hasattr(lib, name), f"{name} declared in fltee_agg.h but not exported"
+        assert name in L.SIGNATURES, f"{name} has no ctypes signature in fltee/_lib.py"
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (\S+)", out))
+    assert set(names) <= exported
+
+
+def test_version_string():
+    from fltee import _lib as L
+    assert b"gfx950" in L.lib().fltee_version()
+
+
+def test_device_aes_tables_fips197():
+    # FIPS-197 Appendix C.1 (AES-128)
+    from fltee import _lib as L
+    key = (ctypes.c_uint8 * 16)(*range(16))
+    pt = (ctypes.c_uint8 * 16)(*bytes.fromhex("00112233445566778899aabbccddeeff"))
+    out = (ctypes.c_uint8 * 16)()
+    L.lib().fltee_debug_aes_block(key, pt, out)
+    assert bytes(out).hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"
+
+
+def test_device_aes_tables_match_ctr_keystream(oracle):
+    # keystream block b of AES-128-CTR (zero IV) = AES_k(BE128(b))
+    from fltee import _lib as L
+    key = oracle.session_key(4242)
+    ks = oracle.aes128_ctr(key, bytes(48))
+    for b in range(3):
+        ctr = (ctypes.c_uint8 * 16)(*([0] * 15 + [b]))
+        out = (ctypes.c_uint8 * 16)()
+        L.lib().fltee_debug_aes_block((ctypes.c_uint8 * 16)(*key.tolist()), ctr, out)
+        assert bytes(out) == ks[16 * b:16 * b + 16]
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path, monkeypatch):
+    from fltee import _lib as L
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    try:
+        L.lib()
+    except RuntimeError as e:
+        assert "no CPU fallback" in str(e)
+    else:
+        raise AssertionError("loading a missing library must fail loudly")
+
+
+def test_pack_records_roundtrip():
+    from fltee.device import pack_records, unpack_records
+    idx = np.array([0, 7, 0xFFFFFFFF], np.uint32)
+    val = np.array([1.5, -0.0, np.inf], np.float32)
+    r = pack_records(idx, val)
+    i2, v2 = unpack_records(r)
+    assert np.array_equal(i2, idx) and np.array_equal(v2.view(np.uint32), val.view(np.uint32))
+    # byte layout == Weight (parameters.rs:9): [u32 LE idx][f32 LE val]
+    w = np.frombuffer(r.tobytes(), dtype=[("idx", "<u4"), ("val", "<f4")])
+    assert np.array_equal(w["idx"], idx)

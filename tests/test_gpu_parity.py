@@ -1,0 +1,285 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact for indices / permutations and for every aggregation whose
+reference order we reproduce (dense + sparse flat algorithms, advanced, alg 6);
+nips19's atomics-based scatter and the DP noise are within the stated fp32
+tolerance / statistically (the enclave's own order and noise are random).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+U32MAX = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    from fltee import device as D
+    torch.cuda.init()
+    return D
+
+
+def cuda_records(D, idx, val):
+    import torch
+    return torch.from_numpy(D.pack_records(idx, val)).cuda()
+
+
+def rand_sparse(rng, n, d, k, scale=0.01):
+    idx = np.concatenate([rng.choice(d, k, replace=False) for _ in range(n)]).astype(np.uint32)
+    val = rng.normal(0, scale, n * k).astype(np.float32)
+    return idx, val
+
+
+def bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# ------------------------------------------------------- flat algorithms ----
+@pytest.mark.parametrize("n,d", [(1, 2), (3, 7), (5, 1000), (30, 50890), (2, 65537), (17, 4099)])
+@pytest.mark.parametrize("alg", [3, 4, 5])
+def test_dense_bit_exact(dev, oracle, n, d, alg):
+    rng = np.random.default_rng(n * 1000 + d)
+    idx = np.tile(np.arange(d, dtype=np.uint32), n)
+    val = rng.normal(0, 0.01, n * d).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(alg, rec, n, d, d, dense=True).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
+def test_dense_order_violation_is_reported(dev):
+    n, d = 2, 64
+    idx = np.tile(np.arange(d, dtype=np.uint32), n)
+    idx[70] = 3
+    rec = cuda_records(dev, idx, np.ones(n * d, np.float32))
+    dev.aggregate(3, rec, n, d, d, dense=True)
+    assert dev.status() & 0x1
+
+
+@pytest.mark.parametrize("n,d,k", [(1, 10, 3), (4, 1000, 100), (30, 50890, 5089), (7, 3001, 2999)])
+@pytest.mark.parametrize("alg", [3, 4, 5])
+def test_sparse_bit_exact(dev, oracle, n, d, k, alg):
+    rng = np.random.default_rng(n + d + k)
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(alg, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
+def test_sparse_repeated_index_flagged(dev):
+    idx = np.array([1, 1, 2, 3], np.uint32)
+    rec = cuda_records(dev, idx, np.ones(4, np.float32))
+    dev.aggregate(3, rec, 2, 2, 8)
+    assert dev.status() & 0x4                      # baseline sweep: needs the sequential rerun
+    out = dev.aggregate(4, rec, 2, 2, 8).cpu().numpy()  # non_oblivious handles it exactly
+    assert dev.status() == 0
+    assert out.tolist() == [0, 1.0, 0.5, 0.5, 0, 0, 0, 0]
+
+
+def test_non_oblivious_index_out_of_range(dev):
+    rec = cuda_records(dev, np.array([0, 9], np.uint32), np.ones(2, np.float32))
+    dev.aggregate(4, rec, 1, 2, 5)
+    assert dev.status() & 0x2
+
+
+# ---------------------------------------------------------- bitonic ---------
+@pytest.mark.parametrize("m", [2, 4, 64, 1024, 8192, 1 << 15, 1 << 18])
+def test_bitonic_idx_network_bit_exact(dev, oracle, m):
+    import torch
+    rng = np.random.default_rng(m)
+    idx = rng.integers(0, max(2, m // 8), m).astype(np.uint32)   # heavy ties
+    val = np.arange(m, dtype=np.float32)                          # identity tracking
+    rec = cuda_records(dev, idx, val)
+    dev.bitonic(rec, 0)
+    torch.cuda.synchronize()
+    gi, gv = dev.unpack_records(rec.cpu().numpy())
+    ref = oracle.bitonic_sort(oracle.as_weights(idx, val))
+    assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
+
+
+@pytest.mark.parametrize("m", [2, 256, 8192, 1 << 16])
+def test_keyed_shuffle_bit_exact(dev, oracle, m):
+    import torch
+    rng = np.random.default_rng(m + 1)
+    idx = rng.integers(0, 50, m).astype(np.uint32)
+    val = np.arange(m, dtype=np.float32)
+    rec = cuda_records(dev, idx, val)
+    dev.bitonic(rec, 2, seed=0xC0FFEE)
+    torch.cuda.synchronize()
+    gi, gv = dev.unpack_records(rec.cpu().numpy())
+    ref = oracle.shuffle_keyed(oracle.as_weights(idx, val), 0xC0FFEE)
+    assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
+
+
+def test_composite_key_sort(dev):
+    import torch
+    rng = np.random.default_rng(9)
+    keys = rng.permutation(1 << 14).astype(np.int64) * 7919 + 3
+    t = torch.from_numpy(keys).cuda()
+    dev.bitonic(t, 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(t.cpu().numpy(), np.sort(keys))
+
+
+# -------------------------------------------------------------- fold -------
+@pytest.mark.parametrize("n,d,k", [(3, 200, 50), (100, 5000, 500), (40, 70000, 7000)])
+def test_fold_bit_exact(dev, oracle, n, d, k):
+    import torch
+    rng = np.random.default_rng(d)
+    idx, val = rand_sparse(rng, n, d, k)
+    w = np.concatenate([oracle.as_weights(idx, val),
+                        oracle.as_weights(np.arange(d, dtype=np.uint32), np.zeros(d, np.float32))])
+    L = len(w)
+    M = oracle.next_pow2(L)
+    w = np.concatenate([w, oracle.as_weights(np.full(M - L, U32MAX, np.uint32), np.zeros(M - L, np.float32))])
+    s = oracle.bitonic_sort(w)
+    for fold_len in (L, n * (k // 2) + d):
+        src = cuda_records(dev, s["idx"], s["val"])
+        dst = torch.empty_like(src)
+        st = torch.zeros(1, dtype=torch.int32, device="cuda")
+        dev.fold(src, dst, fold_len, n, st)
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0
+        gi, gv = dev.unpack_records(dst.cpu().numpy())
+        ref = oracle.fold(s, fold_len)
+        assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
+
+
+def test_fold_overflow_detected(dev):
+    import torch
+    m = 4096
+    idx = np.zeros(m, np.uint32)                     # one run of m records
+    src = cuda_records(dev, idx, np.ones(m, np.float32))
+    dst = torch.empty_like(src)
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dev.fold(src, dst, m, 8, st)
+    torch.cuda.synchronize()
+    assert int(st.item()) & 0x4
+
+
+# ---------------------------------------------------------- advanced -------
+@pytest.mark.parametrize("n,d,k", [(1, 16, 4), (10, 1000, 100), (100, 50890, 5089), (7, 3333, 1)])
+def test_advanced_bit_exact(dev, oracle, n, d, k):
+    rng = np.random.default_rng(n * 7 + d)
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
+def test_advanced_k0_quirk_bit_exact(dev, oracle):
+    rng = np.random.default_rng(5)
+    n, d = 5, 300
+    idx = np.tile(np.arange(d, dtype=np.uint32), n)
+    val = rng.normal(0, 1, n * d).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(1, rec, n, d, d, k_req=0, fold_halo=n * d + d).cpu().numpy()
+    ref, st = oracle.advanced(0, oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 4, 10])
+def test_optimized_alg6_bit_exact(dev, oracle, batch):
+    rng = np.random.default_rng(batch)
+    n, d, k = 10, 2000, 150
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(6, rec, n, k, d, batch=batch).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.client_size_optimized(batch, k, oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
+# ------------------------------------------------------------ nips19 -------
+def test_laplace_counts_match_oracle(dev, oracle):
+    d, k, n = 44964, 4496, 300
+    r, T = dev.laplace_r(d, k, n, seed=77)
+    rr, TT = oracle.laplace_r(d, k, n, seed=77)
+    assert T == TT
+    diff = r.cpu().numpy().astype(np.int64) - rr.astype(np.int64)
+    # device logf may differ from glibc by an ulp: r can move by 1 when T + ceil(x)
+    # sits on an integer boundary — allow a handful, never more than +-1
+    assert np.abs(diff).max() <= 1 and np.count_nonzero(diff) <= 5
+
+
+def test_nips19_close_to_oracle(dev, oracle):
+    rng = np.random.default_rng(19)
+    n, d, k = 12, 3000, 300
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(2, rec, n, k, d, seed=1234).cpu().numpy()
+    assert dev.status() == 0
+    ref, _ = oracle.nips19(k, oracle.as_weights(idx, val), d, n, seed=1234)
+    inorder, _ = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    tol = 1e-6 * np.abs(val).max() * (n + 1)
+    assert np.abs(out - ref).max() <= tol and np.abs(out - inorder).max() <= tol
+
+
+# --------------------------------------------------------------- DP --------
+def test_dp_noise_statistics(dev):
+    import torch
+    n, d = 100, 1 << 20
+    rec = torch.from_numpy(dev.pack_records(np.tile(np.arange(d, dtype=np.uint32), 1),
+                                            np.zeros(d, np.float32))).cuda()
+    out = dev.aggregate(4, rec, 1, d, d, dense=True, dp=True, sigma=1.12, clipping=1.0, seed=5,
+                        n_avg=n).cpu().numpy().astype(np.float64)
+    sd = 1.12 * 1.0 / n
+    assert abs(out.mean()) < 5 * sd / np.sqrt(d)
+    assert abs(out.std() / sd - 1) < 0.01
+    # 4th moment of a Gaussian: E[z^4] = 3
+    assert abs(np.mean((out / sd) ** 4) - 3) < 0.05
+
+
+# ------------------------------------------------------------- clip --------
+def test_server_side_clip_matches_reference_torch(dev):
+    fx = np.load(os.path.join(GOLDEN, "l2clip.npz"))
+    d = fx["flat_in"].size
+    rec = cuda_records(dev, np.arange(d, dtype=np.uint32), fx["flat_in"])
+    out = dev.aggregate(3, rec, 1, d, d, dense=True, clip=True, clipping=float(fx["clipping"]))
+    assert np.allclose(out.cpu().numpy(), fx["flat_out"], rtol=1e-6, atol=0)
+
+
+# -------------------------------------------------------------- AES --------
+@pytest.mark.parametrize("name", ["mnist_sparse", "mnist_sparse_clip", "dense_small"])
+def test_gpu_decrypt_reference_client_payloads(dev, name):
+    import torch
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"))
+    ids = fx["client_ids"]
+    ct = torch.from_numpy(fx["ciphertext"].copy()).cuda()
+    bpc = fx["ciphertext"].size // len(ids)
+    out = torch.empty(fx["plaintext"].size // 8, dtype=torch.int64, device="cuda")
+    dev.decrypt(ids, ct, bpc, out)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == fx["plaintext"].tobytes()
+
+
+# ------------------------------------------------------- full size NS ------
+def test_headline_shape_100x1M_bit_exact(dev):
+    import torch
+    n, d = 100, 1_000_000
+    g = torch.Generator(device="cuda").manual_seed(13)
+    vals = torch.randn(n, d, generator=g, device="cuda") * 0.01
+    idx = torch.arange(d, device="cuda", dtype=torch.int64).repeat(n, 1)
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
+    out = dev.aggregate(3, rec, n, d, d, dense=True).cpu().numpy()
+    assert dev.status() == 0
+    v = vals.cpu().numpy()
+    ref = np.sum(v, axis=0, dtype=np.float32) * np.float32(np.float32(1) / np.float32(n))
+    assert bits_equal(out, ref)
+    # bench checksum (benchmark.rs:226-239)
+    assert abs(float(out.astype(np.float64).sum()) - float(v.astype(np.float64).sum()) / n) < 1e-3
