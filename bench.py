@@ -1,0 +1,262 @@
+"""bench.py — device-resident aggregation throughput of the FL-TEE enclave path on MI355X.
+
+Metric (BASELINE.json): aggregated params/sec (device-resident) = client-parameter
+contributions folded into the aggregate per second, i.e. n*k records / step time,
+summed over all GPUs.
+
+Headline workload (`ns`, SURVEY §8 row NS / the north-star target): aggregation_alg
+= baseline over 100 clients x 1,000,000 dense fp32 updates per GPU (records of
+8 B = u32 idx + f32 val, 800 MB), averaged with 1f32/n.  Multi-GPU: one process
+per GPU, the parameter range is sharded (each rank owns 1M parameters of every
+client: weak scaling) and each step ends with an RCCL gather of the averaged
+shards to rank 0 over xGMI (the response vector is assembled on the root).
+
+Also reported on the same line (rank 0, N=1): the roofline of the dominant kernel,
+a bounded CPU-baseline sample of the oracle (the C restatement of the enclave's
+`baseline`, 1 thread), and the other BASELINE.json configs as `extra`.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ns] [--no-extra]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fl-tee_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+WORKLOADS = {
+    # name: alg, n clients, d params, k records/client (None = dense, k = d)
+    "ns": dict(alg=3, n=100, d=1_000_000, k=None,
+               desc="NS: baseline dense fp32 reduce, 100 clients x 1M params"),
+    "mnist30": dict(alg=3, n=30, d=50890, k=None,
+                    desc="configs[1]: MLP-MNIST num_users=100 frac=0.3 (n=30), baseline, dense"),
+    "mnist100": dict(alg=3, n=100, d=50890, k=None,
+                     desc="100 clients x MLP-MNIST dense (metric text), baseline"),
+    "c1": dict(alg=4, n=30, d=50890, k=5089,
+               desc="configs[0] shape on GPU: MLP-MNIST n=30 alpha=0.1, non_oblivious"),
+    "c3": dict(alg=1, n=100, d=50890, k=5089,
+               desc="configs[2]: MLP-MNIST num_users=1000 frac=0.1 alpha=0.1 (n=100), advanced"),
+    "c4": dict(alg=2, n=300, d=44964, k=4496, dp=True,
+               desc="configs[3]: Purchase100 num_users=1000 frac=0.3 (n=300) alpha=0.1, nips19 + DP"),
+    "c5": dict(alg=1, n=1000, d=10_000_000, k=100_000,
+               desc="configs[4]: synthetic 10M x 1000 clients (k=1%), advanced"),
+}
+ALG_NAMES = {1: "advanced", 2: "nips19", 3: "baseline", 4: "non_oblivious", 5: "path_oram", 6: "optimized"}
+
+
+def make_records(torch, n, d, k, seed, device):
+    """Synthetic client records in HBM (int64 = Weight bytes), client-major."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    if k is None:
+        vals = torch.randn(n, d, generator=g, device=device) * 0.01
+        idx = torch.arange(d, device=device, dtype=torch.int64).expand(n, d)
+    else:
+        vals = torch.randn(n, k, generator=g, device=device) * 0.01
+        # k distinct indices per client (a run from a random offset, mod d); the
+        # oblivious networks' cost does not depend on which indices these are
+        j = torch.arange(k, device=device, dtype=torch.int64)
+        off = torch.randint(0, d, (n, 1), generator=g, device=device)
+        idx = (off + j.unsqueeze(0)) % d
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
+    return rec
+
+
+def time_steps(torch, fn, steps, warmup, stream):
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        fn(warmup + i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = sum(a.elapsed_time(b) for a, b in ev) / steps / 1e3
+    return wall, kern
+
+
+def bench_workload(torch, D, name, steps, warmup, device, nbuf=3):
+    w = WORKLOADS[name]
+    n, d, k = w["n"], w["d"], w["k"]
+    kk = d if k is None else k
+    bytes_per_step = n * kk * 8
+    nbuf = max(1, min(nbuf, int(2.4e9 // max(bytes_per_step, 1))))  # rotate >=3 when it fits
+    recs = [make_records(torch, n, d, k, 1000 + b, device) for b in range(nbuf)]
+    out = torch.empty(d, dtype=torch.float32, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    kw = dict(dense=k is None, status=status)
+    if w.get("dp"):
+        kw.update(dp=True, sigma=1.12, clipping=1.0, seed=7)
+    D.reserve(w["alg"], n, kk, d, **{x: y for x, y in kw.items() if x != "status"})
+    stream = torch.cuda.current_stream()
+
+    def step(i):
+        D.aggregate(w["alg"], recs[i % nbuf], n, kk, d, out=out, **kw)
+
+    wall, kern = time_steps(torch, step, steps, warmup, stream)
+    assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
+    del recs
+    return dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
+                rate=n * kk / kern, bytes=n * kk * 8 + d * 4)
+
+
+def cpu_baseline_sample(d, n, seconds):
+    """The oracle's `baseline` (baseline.rs o_update: one cmov RMW per 64-B line of the
+    d-float output per record) on a bounded prefix of client 0's dense records,
+    single thread.  Rate in client-params/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    rng = np.random.default_rng(0)
+    m = 256
+    spent, done = 0.0, 0
+    while spent < seconds:
+        w = O.as_weights(np.arange(done, done + m, dtype=np.uint32) % d,
+                         rng.normal(0, 0.01, m).astype(np.float32))
+        t0 = time.perf_counter()
+        O.baseline(w, d, n)
+        spent += time.perf_counter() - t0
+        done += m
+        m = min(m * 2, 1 << 16)
+    # context: the enclave's non_oblivious scatter over the FULL workload
+    idx = np.tile(np.arange(d, dtype=np.uint32), 1)
+    w = O.as_weights(idx, rng.normal(0, 0.01, d).astype(np.float32))
+    t0 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - t0 < 1.0:
+        O.non_oblivious(w, d, n)
+        reps += 1
+    non_obl = reps * d / (time.perf_counter() - t0)
+    return dict(value=done / spent, unit="client-params/s", cores=1, kind="port",
+                sample=f"oracle baseline (cmov sweep) over {done} records of client 0 into d={d}, "
+                       f"{spent:.1f}s, 1 thread",
+                non_oblivious_rate=non_obl)
+
+
+def traffic_from_profiles(name):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="ns", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-extra", action="store_true", help="skip the other configs")
+    ap.add_argument("--extra", default="mnist30,mnist100,c1,c3,c4")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from fltee import device as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    w = WORKLOADS[args.workload]
+    n, d, k = w["n"], w["d"], w["k"]
+    kk = d if k is None else k
+
+    recs = [make_records(torch, n, d, k, 17 + 101 * rank + b, device) for b in range(3)]
+    out = torch.empty(d, dtype=torch.float32, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    gathered = ([torch.empty(d, dtype=torch.float32, device=device) for _ in range(world)]
+                if (world > 1 and rank == 0) else None)
+    kw = dict(dense=k is None, status=status)
+    D.reserve(w["alg"], n, kk, d, dense=k is None)
+    stream = torch.cuda.current_stream()
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+
+    def step(i, ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        D.aggregate(w["alg"], recs[i % 3], n, kk, d, out=out, **kw)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:  # final RCCL step: averaged shards -> root over xGMI
+            dist.gather(out, gathered, dst=0)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, kev[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern = sum(a.elapsed_time(b) for a, b in kev) / args.steps / 1e3
+    if world > 1:
+        t = torch.tensor([elapsed, kern], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern = float(t[0]), float(t[1])
+    assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
+    ms = elapsed / args.steps * 1e3
+    value = world * n * kk / (elapsed / args.steps)
+    algo_bytes = n * kk * 8 + d * 4  # records read + averaged output written, per launch
+    del recs
+
+    if rank == 0:
+        line = {
+            "metric": "aggregated params/sec (device-resident), 100 clients x MLP-MNIST updates",
+            "value": value, "unit": "client-params/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": w["desc"], "alg": ALG_NAMES[w["alg"]], "n_clients": n,
+                       "d_per_gpu": d, "k": kk, "record_bytes": 8,
+                       "parallelism": f"param-range shard x{world}" +
+                                      (", RCCL gather to rank 0" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": algo_bytes / kern / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": algo_bytes / kern / 1e9 / HBM_PEAK_GBS,
+                         "traffic": traffic_from_profiles(args.workload),
+                         "kernel": "dense_accumulate_v", "algorithmic_bytes": algo_bytes,
+                         "kernel_ms": kern * 1e3},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_sample(d, n, args.cpu_seconds)
+        if world == 1 and not args.no_extra:
+            extra = {}
+            for name in [x for x in args.extra.split(",") if x]:
+                r = bench_workload(torch, D, name, steps=max(5, args.steps // 5), warmup=2,
+                                   device=device)
+                extra[name] = dict(desc=WORKLOADS[name]["desc"], alg=r["alg"], n=r["n"], d=r["d"],
+                                   k=r["k"], ms_per_step=r["wall_s"] * 1e3 / max(5, args.steps // 5),
+                                   kernel_ms=r["kernel_s"] * 1e3, value=r["rate"],
+                                   unit="client-params/s")
+            line["extra"] = extra
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -147,6 +147,7 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     fltee_device_opts o;
     std::memset(&o, 0, sizeof o);
     o.k_req = k_req;
+    o.flags |= FLTEE_OPT_K_REQ;
     o.batch = batch;
     const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
                       alg == FLTEE_ALG_NON_OBLIVIOUS;

@@ -199,7 +199,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         }
         break;
     case FLTEE_ALG_ADVANCED: {
-        const size_t k_req = o.k_req ? o.k_req : k;
+        const size_t k_req = (o.flags & FLTEE_OPT_K_REQ) ? o.k_req : k;
         const size_t fold_len = n * k_req + d;
         if (fold_len > n * k + d) return FLTEE_ERROR_INVALID_PARAMETER;  // advanced.rs:72 panic
         e = run_advanced(c, rec, n, k, d, k_req, o.fold_halo, coef, out, acc, status, s);
@@ -339,3 +339,22 @@ extern "C" fltee_status_t fltee_laplace_r_device(size_t d, size_t k, size_t n, u
 }
 
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
+
+extern "C" fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d,
+                                                float coef, float *d_out, void *stream) {
+    if (nrows == 0) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_rows_accumulate(d_rows, nrows, d, coef, d_out, false, (hipStream_t)stream) ==
+                   hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float sigma,
+                                                float clipping, size_t n, uint64_t seed,
+                                                void *stream) {
+    if (n == 0) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_dp_noise(d_out, d, sigma, clipping, n, seed ? seed : next_seed(),
+                           (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}

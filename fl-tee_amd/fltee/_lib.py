@@ -32,6 +32,7 @@ OPT_DP = 0x2
 OPT_CLIP = 0x4
 OPT_ACCUMULATE = 0x8
 OPT_NO_AVERAGE = 0x10
+OPT_K_REQ = 0x20
 
 
 class DeviceOpts(ctypes.Structure):
@@ -65,6 +66,8 @@ SIGNATURES = {
     "fltee_reserve": (_U32, [_U32, _S, _S, _S, ctypes.POINTER(DeviceOpts)]),
     "fltee_decrypt_device": (_U32, [_P, _S, _P, _S, _P, _P]),
     "fltee_device_status": (_U32, [_P, _P]),
+    "fltee_sum_rows_device": (_U32, [_P, _S, _S, _F, _P, _P]),
+    "fltee_dp_noise_device": (_U32, [_P, _S, _F, _F, _S, _U64, _P]),
     "fltee_bitonic_device": (_U32, [_P, _S, _U32, _U32, _P]),
     "fltee_fold_device": (_U32, [_P, _P, _S, _S, _S, _P, _P]),
     "fltee_laplace_r_device": (_U32, [_S, _S, _S, _U64, _P, _P, _P]),

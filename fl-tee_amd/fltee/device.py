@@ -37,12 +37,15 @@ def unpack_records(rec):
 
 
 def opts(*, dense=False, dp=False, clip=False, accumulate=False, no_average=False, sigma=1.12,
-         clipping=1.0, seed=0, k_req=0, batch=0, n_avg=0, fold_halo=0, status=None):
+         clipping=1.0, seed=0, k_req=None, batch=0, n_avg=0, fold_halo=0, status=None):
     o = L.DeviceOpts()
     o.flags = ((L.OPT_DENSE if dense else 0) | (L.OPT_DP if dp else 0) | (L.OPT_CLIP if clip else 0)
                | (L.OPT_ACCUMULATE if accumulate else 0) | (L.OPT_NO_AVERAGE if no_average else 0))
     o.sigma, o.clipping, o.seed = sigma, clipping, seed
-    o.k_req, o.batch, o.n_avg, o.fold_halo = k_req, batch, n_avg, fold_halo
+    if k_req is not None:
+        o.flags |= L.OPT_K_REQ
+        o.k_req = k_req
+    o.batch, o.n_avg, o.fold_halo = batch, n_avg, fold_halo
     o.d_status = status.data_ptr() if status is not None else None
     return o
 
@@ -108,3 +111,22 @@ def laplace_r(d, k, n, seed, device="cuda", stream=None):
     _check(L.lib().fltee_laplace_r_device(d, k, n, seed, _ptr(r), ctypes.byref(T),
                                           _stream(stream)), "fltee_laplace_r_device")
     return r, T.value
+
+
+def sum_rows(rows, coef=1.0, out=None, stream=None):
+    """fltee_sum_rows_device: out = coef * (rows[0] + rows[1] + ...), added in row order."""
+    assert rows.is_cuda and rows.dtype == torch.float32 and rows.dim() == 2
+    nrows, d = rows.shape
+    rows = rows.contiguous()
+    if out is None:
+        out = torch.empty(d, dtype=torch.float32, device=rows.device)
+    _check(L.lib().fltee_sum_rows_device(_ptr(rows), nrows, d, coef, _ptr(out), _stream(stream)),
+           "fltee_sum_rows_device")
+    return out
+
+
+def dp_noise(out, sigma, clipping, n, seed=0, stream=None):
+    """fltee_dp_noise_device: out += (N(0, clipping*sigma) / n) as f32 (common.rs:56-72)."""
+    _check(L.lib().fltee_dp_noise_device(_ptr(out), out.numel(), sigma, clipping, n, seed,
+                                         _stream(stream)), "fltee_dp_noise_device")
+    return out

@@ -130,13 +130,16 @@ fltee_status_t ecall_client_size_optimized_secure_aggregation(
 #define FLTEE_OPT_CLIP 0x4u       /* server-side per-client L2 clip (update.py:187-204) */
 #define FLTEE_OPT_ACCUMULATE 0x8u /* out += sum (no averaging): alg-6 batches, shards */
 #define FLTEE_OPT_NO_AVERAGE 0x10u /* skip the 1/n scaling (partial sums for RCCL) */
+#define FLTEE_OPT_K_REQ 0x20u      /* advanced: fold over n*k_req+d even if k_req != k
+                                      (advanced.rs:70 uses the REQUEST's k; 0 when
+                                      fl_main.py sends dense uploads without --alpha) */
 
 typedef struct fltee_device_opts {
     uint32_t flags;     /* FLTEE_OPT_* */
     float sigma;        /* DP noise multiplier */
     float clipping;     /* DP / clip norm bound C */
     uint64_t seed;      /* RNG seed for nips19 / DP; 0 = draw from getrandom() */
-    size_t k_req;       /* advanced: request num_of_sparse_parameters (fold length n*k_req+d) */
+    size_t k_req;       /* advanced: request num_of_sparse_parameters (with FLTEE_OPT_K_REQ) */
     size_t batch;       /* alg 6: optimal_num_of_clients */
     size_t n_avg;       /* divisor for averaging (0 = n) */
     size_t fold_halo;   /* advanced fold halo H (0 = n, exact when each client's indices are distinct) */
@@ -163,6 +166,16 @@ fltee_status_t fltee_reserve(uint32_t alg, size_t n, size_t k, size_t d,
  * (n * (bytes_per_client/8) * 8 bytes).  lib.rs:312-343. */
 fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n, const void *d_cipher,
                                     size_t bytes_per_client, void *d_records, void *stream);
+
+/* out[j] = coef * sum_r rows[r*d + j], rows added in order (exact fp32): the
+ * root-side combine of per-GPU partial sums, in the batch order of alg 6
+ * (lib.rs:564-573: global[i] += batch_sum[i], then average). */
+fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d, float coef,
+                                     float *d_out, void *stream);
+
+/* common.rs:56-72 on a device vector: out[i] += (N(0, clipping*sigma) / n) as f32. */
+fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float sigma, float clipping,
+                                     size_t n, uint64_t seed, void *stream);
 
 /* Synchronise `stream` and return (and clear) the library's status word. */
 fltee_status_t fltee_device_status(void *stream, uint32_t *status);
