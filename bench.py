@@ -148,8 +148,8 @@ def traffic_from_profiles(name):
     try:
         with open(path) as f:
             t = json.load(f)
-        return t.get(name)
-    except (OSError, ValueError):
+        return t[name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
         return None
 
 
