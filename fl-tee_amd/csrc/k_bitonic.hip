@@ -12,14 +12,21 @@
 //           keyed mixer replaces the running FxHash of heap addresses)
 // Every compare-exchange is branch-free (v_cndmask) and every address depends
 // only on (i, j, k): the memory trace is data-independent, like the cmov
-// network it replaces.
+// network it replaces.  Compare-exchanges of one step are disjoint, so any
+// grouping of consecutive steps that keeps their order is the same network.
 //
-// Schedule for M = 2^m records, LDS tile T = 2^t:
-//   tile_sort            all stages i <= T inside LDS (one launch)
-//   per stage i > T:     steps j >= T in global passes, R <= 4 levels per pass
-//                        held in registers (2^R records / lane);
-//                        steps j < T in one LDS merge launch.
-// HBM traffic per launch = 2 * M * 8 bytes.
+// Grouping.  R consecutive steps j = 2^jtop .. 2^(jtop-R+1) of one stage only
+// pair records whose positions differ in bits [jtop-R+1, jtop]: the 2^R records
+// {b + q * 2^(jtop-R+1)} form a closed group that one lane can run through all
+// R steps in registers.
+//   tile_sort   : stages 2..T in LDS (T = 2^t <= 8192 records = 64 KB); each lane
+//                 holds 16 records per round, i.e. 4 steps per barrier.
+//   per stage i > T:
+//     global    : steps j >= T in passes of up to 6 steps (64 records / lane in
+//                 registers), HBM traffic 2*M*8 bytes per pass;
+//     merge     : steps j < T in one LDS launch (4 steps per barrier).
+// LDS layout pads one slot per 16 records so that the 64 lanes of a wave hit
+// distinct banks when each walks a 16-record group.
 #include "common.h"
 
 namespace fltee {
@@ -35,76 +42,18 @@ __device__ __forceinline__ bool swap_rule(uint64_t a, uint64_t b, uint32_t l, ui
     return asc ^ lt;
 }
 
-constexpr int BT_THREADS = 512;
-
-template <int MODE>
-__device__ __forceinline__ void lds_step(uint64_t *sm, uint32_t T, uint32_t base, uint32_t ilog,
-                                         uint32_t jlog, uint32_t key) {
-    const uint32_t j = 1u << jlog, imask = 1u << ilog;
-    for (uint32_t k = threadIdx.x; k < (T >> 1); k += BT_THREADS) {
-        const uint32_t l = ((k >> jlog) << (jlog + 1)) | (k & (j - 1));
-        const uint32_t m = l + j;
-        const uint64_t a = sm[l], b = sm[m];
-        const bool sw = swap_rule<MODE>(a, b, base + l, imask, key);
-        sm[l] = sw ? b : a;
-        sm[m] = sw ? a : b;
-    }
+// insert r zero bits at bit position d of g
+__device__ __forceinline__ uint32_t spread(uint32_t g, uint32_t d, uint32_t r) {
+    const uint32_t lo = g & ((1u << d) - 1u);
+    return ((g >> d) << (d + r)) | lo;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(BT_THREADS) void bitonic_tile_sort(uint64_t *__restrict__ data,
-                                                                uint32_t tlog, uint32_t seed) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const uint32_t T = 1u << tlog;
-    const uint32_t base = blockIdx.x << tlog;
-    uint4 *g4 = reinterpret_cast<uint4 *>(data + base);
-    uint4 *s4 = reinterpret_cast<uint4 *>(sm);
-    for (uint32_t e = threadIdx.x; e < T / 2; e += BT_THREADS) s4[e] = g4[e];
-    __syncthreads();
-    for (uint32_t ilog = 1; ilog <= tlog; ++ilog) {
-        for (int jlog = (int)ilog - 1; jlog >= 0; --jlog) {
-            const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, (uint32_t)jlog) : 0u;
-            lds_step<MODE>(sm, T, base, ilog, (uint32_t)jlog, key);
-            __syncthreads();
-        }
-    }
-    for (uint32_t e = threadIdx.x; e < T / 2; e += BT_THREADS) g4[e] = s4[e];
-}
-
-template <int MODE>
-__global__ __launch_bounds__(BT_THREADS) void bitonic_tile_merge(uint64_t *__restrict__ data,
-                                                                 uint32_t tlog, uint32_t ilog,
-                                                                 uint32_t seed) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const uint32_t T = 1u << tlog;
-    const uint32_t base = blockIdx.x << tlog;
-    uint4 *g4 = reinterpret_cast<uint4 *>(data + base);
-    uint4 *s4 = reinterpret_cast<uint4 *>(sm);
-    for (uint32_t e = threadIdx.x; e < T / 2; e += BT_THREADS) s4[e] = g4[e];
-    __syncthreads();
-    for (int jlog = (int)tlog - 1; jlog >= 0; --jlog) {
-        const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, (uint32_t)jlog) : 0u;
-        lds_step<MODE>(sm, T, base, ilog, (uint32_t)jlog, key);
-        __syncthreads();
-    }
-    for (uint32_t e = threadIdx.x; e < T / 2; e += BT_THREADS) g4[e] = s4[e];
-}
-
-// R consecutive steps jlog, jlog-1, ..., jlog-R+1 of stage ilog in registers.
-// Lane t owns the group {b + q*delta : q < 2^R}, delta = 2^(jlog-R+1).
+// Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
+// records held in v[], whose first record sits at global position p0.
 template <int MODE, int R>
-__global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
-                                                      uint32_t jlog, uint32_t seed,
-                                                      uint32_t ngroups) {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= ngroups) return;
-    const uint32_t dlog = jlog - R + 1;
-    const uint32_t delta = 1u << dlog;
-    const uint32_t b = ((t >> dlog) << (dlog + R)) | (t & (delta - 1));
+__device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, uint32_t dlog,
+                                            uint32_t ilog, uint32_t seed) {
     const uint32_t imask = 1u << ilog;
-    uint64_t v[1 << R];
-#pragma unroll
-    for (int q = 0; q < (1 << R); ++q) v[q] = data[b + (uint32_t)q * delta];
 #pragma unroll
     for (int lv = R - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
@@ -113,51 +62,162 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
             const uint64_t a = v[q], c = v[qm];
-            const bool sw = swap_rule<MODE>(a, c, b + (uint32_t)q * delta, imask, key);
+            const bool sw = swap_rule<MODE>(a, c, p0 + ((uint32_t)q << dlog), imask, key);
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
         }
     }
+}
+
+// ------------------------------------------------------------- LDS tile ----
+__device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
+
+// One LDS round: steps jtop..jtop-R+1 of stage ilog over the whole tile.
+// Every lane handles 16 records = 16 >> R groups of 2^R records.
+template <int MODE, int R>
+__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t tlog, uint32_t base,
+                                          uint32_t ilog, uint32_t jtop, uint32_t seed) {
+    constexpr int G = 16 >> R;  // groups per lane
+    const uint32_t dlog = jtop - R + 1;
+    const uint32_t ngroups = 1u << (tlog - R);
+    for (uint32_t g0 = threadIdx.x; g0 < ngroups; g0 += blockDim.x * G) {
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) data[b + (uint32_t)q * delta] = v[q];
+        for (int h = 0; h < G; ++h) {
+            const uint32_t g = g0 + (uint32_t)h * blockDim.x;
+            if (g >= ngroups) break;
+            const uint32_t b = spread(g, dlog, R);
+            uint64_t v[1 << R];
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << dlog))];
+            group_steps<MODE, R>(v, base + b, dlog, ilog, seed);
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << dlog))] = v[q];
+        }
+    }
 }
 
 template <int MODE>
-static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jlog,
+__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t tlog, uint32_t base,
+                                          uint32_t ilog, int jtop, uint32_t seed) {
+    while (jtop >= 0) {
+        const int r = jtop + 1 < 4 ? jtop + 1 : 4;
+        switch (r) {
+        case 1: lds_round<MODE, 1>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
+        case 2: lds_round<MODE, 2>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
+        case 3: lds_round<MODE, 3>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
+        default: lds_round<MODE, 4>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
+        }
+        __syncthreads();
+        jtop -= r;
+    }
+}
+
+__device__ __forceinline__ void tile_load(uint64_t *sm, const uint64_t *g, uint32_t T) {
+    for (uint32_t e = threadIdx.x; e < T; e += blockDim.x) sm[lpad(e)] = g[e];
+}
+__device__ __forceinline__ void tile_store(const uint64_t *sm, uint64_t *g, uint32_t T) {
+    for (uint32_t e = threadIdx.x; e < T; e += blockDim.x) g[e] = sm[lpad(e)];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void bitonic_tile_sort(uint64_t *__restrict__ data,
+                                                         uint32_t tlog, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+    const uint32_t T = 1u << tlog;
+    const uint32_t base = blockIdx.x << tlog;
+    tile_load(sm, data + base, T);
+    __syncthreads();
+    for (uint32_t ilog = 1; ilog <= tlog; ++ilog) lds_steps<MODE>(sm, tlog, base, ilog, (int)ilog - 1, seed);
+    tile_store(sm, data + base, T);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void bitonic_tile_merge(uint64_t *__restrict__ data,
+                                                          uint32_t tlog, uint32_t ilog,
+                                                          uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+    const uint32_t T = 1u << tlog;
+    const uint32_t base = blockIdx.x << tlog;
+    tile_load(sm, data + base, T);
+    __syncthreads();
+    lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, seed);
+    tile_store(sm, data + base, T);
+}
+
+// --------------------------------------------------------- global pass -----
+// Steps jtop..jtop-R+1 of stage ilog straight from HBM: lane t owns group t.
+template <int MODE, int R>
+__global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
+                                                      uint32_t jtop, uint32_t seed,
+                                                      uint32_t ngroups) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= ngroups) return;
+    const uint32_t dlog = jtop - R + 1;
+    const uint32_t b = spread(t, dlog, R);
+    uint64_t v[1 << R];
+#pragma unroll
+    for (int q = 0; q < (1 << R); ++q) v[q] = __builtin_nontemporal_load(data + b + ((uint32_t)q << dlog));
+    group_steps<MODE, R>(v, b, dlog, ilog, seed);
+#pragma unroll
+    for (int q = 0; q < (1 << R); ++q) __builtin_nontemporal_store(v[q], data + b + ((uint32_t)q << dlog));
+}
+
+template <int MODE>
+static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jtop,
                                 int R, uint32_t seed, hipStream_t s) {
     const uint32_t ngroups = 1u << (mlog - R);
     const unsigned blocks = (ngroups + 255) / 256;
     switch (R) {
-    case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jlog, seed, ngroups); break;
-    case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jlog, seed, ngroups); break;
-    case 3: hipLaunchKernelGGL((bitonic_global<MODE, 3>), dim3(blocks), dim3(256), 0, s, data, ilog, jlog, seed, ngroups); break;
-    default: hipLaunchKernelGGL((bitonic_global<MODE, 4>), dim3(blocks), dim3(256), 0, s, data, ilog, jlog, seed, ngroups); break;
+    case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    case 3: hipLaunchKernelGGL((bitonic_global<MODE, 3>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    case 4: hipLaunchKernelGGL((bitonic_global<MODE, 4>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    case 5: hipLaunchKernelGGL((bitonic_global<MODE, 5>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    default: hipLaunchKernelGGL((bitonic_global<MODE, 6>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
     }
     return hipGetLastError();
 }
 
+constexpr uint32_t kMaxTileLog = 13;  // 8192 records = 64 KB (+1/16 padding) of LDS
+
+// Steps per global pass: 5 (32 records/lane, 2 waves/SIMD) by default; the
+// FLTEE_BITONIC_MAXR knob (1..6) exists for tuning runs only.
+static int max_global_r() {
+    static int r = [] {
+        const char *e = getenv("FLTEE_BITONIC_MAXR");
+        int v = e ? atoi(e) : 5;
+        return v < 1 ? 1 : (v > 6 ? 6 : v);
+    }();
+    return r;
+}
+
 template <int MODE>
 static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s) {
+    const int kMaxGlobalR = max_global_r();
     const uint32_t mlog = log2_pow2(m);
-    uint32_t tlog = mlog < 13 ? mlog : 13;
-    while (tlog > 10 && (mlog - tlog) < 8) --tlog;  // keep >= 256 tiles when possible
+    uint32_t tlog = mlog < kMaxTileLog ? mlog : kMaxTileLog;
+    while (tlog > 11 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles to fill the CUs
     if (tlog < 1) tlog = 1;
     const unsigned tiles = 1u << (mlog - tlog);
-    const size_t lds = ((size_t)1 << tlog) * 8;
-    hipLaunchKernelGGL((bitonic_tile_sort<MODE>), dim3(tiles), dim3(BT_THREADS), lds, s, data, tlog,
+    const uint32_t T = 1u << tlog;
+    const unsigned threads = T / 16 < 64 ? 64 : (T / 16 > 512 ? 512 : T / 16);
+    const size_t lds = (size_t)(T + T / 16 + 1) * 8;
+    hipLaunchKernelGGL((bitonic_tile_sort<MODE>), dim3(tiles), dim3(threads), lds, s, data, tlog,
                        seed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     for (uint32_t ilog = tlog + 1; ilog <= mlog; ++ilog) {
-        int jlog = (int)ilog - 1;
-        while (jlog >= (int)tlog) {
-            int R = jlog - (int)tlog + 1;
-            if (R > 4) R = 4;
-            e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jlog, R, seed, s);
+        int jtop = (int)ilog - 1;
+        const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
+        const int passes = (nglobal + kMaxGlobalR - 1) / kMaxGlobalR;
+        for (int p = 0; p < passes; ++p) {
+            const int left = jtop - (int)tlog + 1;
+            const int R = (left + (passes - p) - 1) / (passes - p);  // balanced split
+            e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s);
             if (e != hipSuccess) return e;
-            jlog -= R;
+            jtop -= R;
         }
-        hipLaunchKernelGGL((bitonic_tile_merge<MODE>), dim3(tiles), dim3(BT_THREADS), lds, s, data,
+        hipLaunchKernelGGL((bitonic_tile_merge<MODE>), dim3(tiles), dim3(threads), lds, s, data,
                            tlog, ilog, seed);
         e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -17,6 +17,15 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _as_u8(buf):
+    """bytes / bytearray / numpy array -> flat uint8 view (no copy of large payloads)."""
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    if isinstance(buf, (bytes, bytearray, memoryview)):
+        return np.frombuffer(buf, dtype=np.uint8)
+    return np.frombuffer(bytes(buf), dtype=np.uint8)  # e.g. fl_main.py's list of ints
+
+
 class Enclave:
     def __init__(self, device=0):
         self.lib = L.lib()
@@ -56,7 +65,7 @@ class Enclave:
     def ecall_secure_aggregation(self, fl_id, round_, client_ids, encrypted_parameters,
                                  num_of_parameters, num_of_sparse_parameters, aggregation_alg):
         ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
-        enc = np.frombuffer(bytes(encrypted_parameters), dtype=np.uint8)
+        enc = _as_u8(encrypted_parameters)
         out = np.full(num_of_parameters, np.nan, dtype=np.float32)
         times = np.full(3, np.nan, dtype=np.float32)
         rv = ctypes.c_uint32(0xFFFFFFFF)
@@ -71,7 +80,7 @@ class Enclave:
                                                        num_of_parameters, num_of_sparse_parameters,
                                                        aggregation_alg):
         ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
-        enc = np.frombuffer(bytes(encrypted_parameters), dtype=np.uint8)
+        enc = _as_u8(encrypted_parameters)
         need = len(ids) * num_of_sparse_parameters * 8
         if enc.nbytes < need:  # [user_check]: the enclave would read past the buffer
             raise ValueError(f"payload has {enc.nbytes} bytes, alg 6 reads {need}")
