@@ -196,7 +196,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="ns", choices=sorted(WORKLOADS))
     ap.add_argument("--no-extra", action="store_true", help="skip the other configs")
-    ap.add_argument("--extra", default="mnist30,mnist100,c1,c3,c4")
+    ap.add_argument("--extra", default="mnist30,mnist100,c1,c3,c4,c5")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-inclusive ECALL leg")

@@ -73,7 +73,8 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 __device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
 
 // One LDS round: steps jtop..jtop-R+1 of stage ilog over the whole tile.
-// Every lane handles 16 records = 16 >> R groups of 2^R records.
+// A lane handles up to 16 >> R groups of 2^R records (E = T / blockDim records
+// per lane; the host keeps R <= log2(E) so every lane is busy).
 template <int MODE, int R>
 __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t tlog, uint32_t base,
                                           uint32_t ilog, uint32_t jtop, uint32_t seed) {
@@ -98,9 +99,9 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t tlog, uint32_t 
 
 template <int MODE>
 __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t tlog, uint32_t base,
-                                          uint32_t ilog, int jtop, uint32_t seed) {
+                                          uint32_t ilog, int jtop, int rmax, uint32_t seed) {
     while (jtop >= 0) {
-        const int r = jtop + 1 < 4 ? jtop + 1 : 4;
+        const int r = jtop + 1 < rmax ? jtop + 1 : rmax;
         switch (r) {
         case 1: lds_round<MODE, 1>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
         case 2: lds_round<MODE, 2>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
@@ -121,26 +122,27 @@ __device__ __forceinline__ void tile_store(const uint64_t *sm, uint64_t *g, uint
 
 template <int MODE>
 __global__ __launch_bounds__(512) void bitonic_tile_sort(uint64_t *__restrict__ data,
-                                                         uint32_t tlog, uint32_t seed) {
+                                                         uint32_t tlog, int rmax,
+                                                         uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     const uint32_t T = 1u << tlog;
     const uint32_t base = blockIdx.x << tlog;
     tile_load(sm, data + base, T);
     __syncthreads();
-    for (uint32_t ilog = 1; ilog <= tlog; ++ilog) lds_steps<MODE>(sm, tlog, base, ilog, (int)ilog - 1, seed);
+    for (uint32_t ilog = 1; ilog <= tlog; ++ilog) lds_steps<MODE>(sm, tlog, base, ilog, (int)ilog - 1, rmax, seed);
     tile_store(sm, data + base, T);
 }
 
 template <int MODE>
 __global__ __launch_bounds__(512) void bitonic_tile_merge(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t ilog,
-                                                          uint32_t seed) {
+                                                          int rmax, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     const uint32_t T = 1u << tlog;
     const uint32_t base = blockIdx.x << tlog;
     tile_load(sm, data + base, T);
     __syncthreads();
-    lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, seed);
+    lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, rmax, seed);
     tile_store(sm, data + base, T);
 }
 
@@ -180,12 +182,12 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
 
 constexpr uint32_t kMaxTileLog = 13;  // 8192 records = 64 KB (+1/16 padding) of LDS
 
-// Steps per global pass: 5 (32 records/lane, 2 waves/SIMD) by default; the
+// Steps per global pass: 6 (64 records/lane; measured fastest at M = 2^24, 2^27); the
 // FLTEE_BITONIC_MAXR knob (1..6) exists for tuning runs only.
 static int max_global_r() {
     static int r = [] {
         const char *e = getenv("FLTEE_BITONIC_MAXR");
-        int v = e ? atoi(e) : 5;
+        int v = e ? atoi(e) : 6;
         return v < 1 ? 1 : (v > 6 ? 6 : v);
     }();
     return r;
@@ -200,10 +202,13 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     if (tlog < 1) tlog = 1;
     const unsigned tiles = 1u << (mlog - tlog);
     const uint32_t T = 1u << tlog;
-    const unsigned threads = T / 16 < 64 ? 64 : (T / 16 > 512 ? 512 : T / 16);
+    // records per lane E = T/512 clamped to [2, 16]: 512 lanes per tile whenever T >= 1024
+    const uint32_t E = T / 512 < 2 ? 2 : (T / 512 > 16 ? 16 : T / 512);
+    const unsigned threads = T / E ? T / E : 1;
+    const int rmax = (int)log2_pow2(E);
     const size_t lds = (size_t)(T + T / 16 + 1) * 8;
     hipLaunchKernelGGL((bitonic_tile_sort<MODE>), dim3(tiles), dim3(threads), lds, s, data, tlog,
-                       seed);
+                       rmax, seed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     for (uint32_t ilog = tlog + 1; ilog <= mlog; ++ilog) {
@@ -218,7 +223,7 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
             jtop -= R;
         }
         hipLaunchKernelGGL((bitonic_tile_merge<MODE>), dim3(tiles), dim3(threads), lds, s, data,
-                           tlog, ilog, seed);
+                           tlog, ilog, rmax, seed);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

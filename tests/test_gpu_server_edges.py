@@ -1,0 +1,135 @@
+"""Host logic of server.rs over the C ABI, and the edge cases of the ECALL path
+(empty / ragged payloads, k = 0, single client), each against the oracle enclave."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+
+@pytest.fixture(scope="module")
+def enclave():
+    import torch
+    torch.cuda.init()
+    from fltee.ecalls import Enclave
+    e = Enclave(0)
+    yield e
+    e.destroy()
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32),
+                          np.asarray(b, np.float32).view(np.uint32))
+
+
+def both(enclave, oracle, fl, ids, d, k, alg, enc, seed=3):
+    from fltee.ecalls import set_debug_seed
+    set_debug_seed(seed)
+    O = oracle.OracleEnclave(seed=seed)
+    assert enclave.ecall_fl_init(fl, ids, d, k, 1.0, 1.0, 0.1, 1.0, alg, 0, 0) == (0, 0)
+    assert O.fl_init(fl, ids, d, k, 1.0, 1.0, 0.1, 1.0, alg) == 0
+    enclave.ecall_start_round(fl, 0, len(ids))
+    O.start_round(fl, 0, len(ids))
+    got = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k, alg)
+    ref = O.secure_aggregation(fl, 0, ids, enc, d, k, alg)
+    set_debug_seed(0)
+    return got, ref
+
+
+def test_server_round_trip(oracle):
+    from fltee.server import Aggregator, ServerPanic
+    fx = np.load(os.path.join(GOLDEN, "mnist_sparse.npz"))
+    ids, d, k = [int(x) for x in fx["client_ids"]], int(fx["d"]), int(fx["k"])
+    srv = Aggregator(device=0)
+    rep = srv.start(11, ids, 1.12, 1.0, 0.1, 1.0, 4, d, k)
+    assert rep["round"] == 0 and sorted(rep["client_ids"]) == sorted(ids)
+    # fl_main.py's defaults: optimal_num_of_clients = 100 > n = 4 — the reference
+    # server panics here for every alg (server.rs:126-128); we only check alg 6
+    out = srv.aggregate(11, 0, fx["ciphertext"].tobytes(), d, k, 100, 4, ids)
+    assert out["round"] == 1 and len(out["client_ids"]) == len(ids)
+    assert bits_equal(out["updated_parameters"], fx["oracle_non_oblivious"])
+    assert out["execution_time"] > 0
+    strict = Aggregator(enclave=srv.enclave, strict_reference=True)
+    with pytest.raises(ServerPanic):
+        strict.aggregate(11, 1, fx["ciphertext"].tobytes(), d, k, 100, 4, ids)
+    with pytest.raises(ServerPanic):  # wrong round -> retval 0x2 -> panic
+        srv.aggregate(11, 5, fx["ciphertext"].tobytes(), d, k, 1, 4, ids)
+    srv.start(12, ids, 1.12, 1.0, 0.1, 1.0, 6, d, k)
+    with pytest.raises(ServerPanic):  # alg 6 keeps the check
+        srv.aggregate(12, 0, fx["ciphertext"].tobytes(), d, k, 100, 6, ids)
+
+
+@pytest.mark.parametrize("alg", [1, 2, 3, 4, 5])
+def test_empty_payload_k0(enclave, oracle, alg):
+    ids = np.array([1, 2, 3], np.uint32)
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 20 + alg, ids, 64, 0, alg, b"")
+    assert (st, rv) == (0, ost) == (0, 0)
+    assert bits_equal(out, ref) and not out.any()
+
+
+@pytest.mark.parametrize("alg", [1, 3, 4, 5])
+def test_ragged_payload_tail_ignored(enclave, oracle, alg):
+    # enc_len not a multiple of n: lib.rs:305 floors bytes-per-client, the tail is ignored
+    rng = np.random.default_rng(alg)
+    ids = np.array([5, 9], np.uint32)
+    d, k = 100, 10
+    plain = []
+    for _ in ids:
+        idx = rng.choice(d, k, replace=False).astype(np.uint32)
+        val = rng.normal(0, 1, k).astype(np.float32)
+        plain.append(oracle.as_weights(idx, val).tobytes())
+    enc = oracle.encrypt_clients(ids, plain) + b"\x07" * 5
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 40 + alg, ids, d, k, alg, enc)
+    assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
+
+
+@pytest.mark.parametrize("alg", [1, 3, 4, 5])
+def test_single_client_dense(enclave, oracle, alg):
+    rng = np.random.default_rng(10 + alg)
+    d = 777
+    ids = np.array([42], np.uint32)
+    w = oracle.as_weights(np.arange(d, dtype=np.uint32), rng.normal(0, 1, d).astype(np.float32))
+    enc = oracle.encrypt_clients(ids, [w.tobytes()])
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 60 + alg, ids, d, d, alg, enc)
+    assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
+
+
+def test_dense_out_of_order_falls_back_to_scatter(enclave, oracle):
+    # k == d but the records are permuted: the dense kernel reports it and the
+    # ECALL layer reruns the scatter semantics (still bit-exact)
+    rng = np.random.default_rng(4)
+    d = 500
+    ids = np.array([1, 2, 3], np.uint32)
+    plain = []
+    for _ in ids:
+        idx = rng.permutation(d).astype(np.uint32)
+        plain.append(oracle.as_weights(idx, rng.normal(0, 1, d).astype(np.float32)).tobytes())
+    enc = oracle.encrypt_clients(ids, plain)
+    for alg in (3, 4, 5):
+        (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 80 + alg, ids, d, d, alg, enc)
+        assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
+
+
+def test_repeated_index_within_client(enclave, oracle):
+    # a client repeats an index: baseline's oblivious sweep reruns sequentially (exact)
+    ids = np.array([1, 2], np.uint32)
+    w1 = oracle.as_weights(np.array([3, 3, 5], np.uint32), np.array([0.1, 0.2, 0.3], np.float32))
+    w2 = oracle.as_weights(np.array([3, 4, 5], np.uint32), np.array([1e-8, 0.5, 0.7], np.float32))
+    enc = oracle.encrypt_clients(ids, [w1.tobytes(), w2.tobytes()])
+    for alg in (1, 3, 4, 5):
+        (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 90 + alg, ids, 8, 3, alg, enc)
+        assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref), alg
+
+
+def test_non_oblivious_out_of_range_rejected(enclave, oracle):
+    ids = np.array([1], np.uint32)
+    w = oracle.as_weights(np.array([0, 8], np.uint32), np.array([1, 1], np.float32))
+    enc = oracle.encrypt_clients(ids, [w.tobytes()])
+    (st, rv, out, _), (ost, _, _) = both(enclave, oracle, 99, ids, 8, 2, 4, enc)
+    assert rv == 0x2 and ost == 0x2 and not out.any()     # the enclave would panic
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 98, ids, 8, 2, 3, enc)
+    assert (rv, ost) == (0, 0) and bits_equal(out, ref)  # baseline ignores it (o_update)
