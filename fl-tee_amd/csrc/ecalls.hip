@@ -296,8 +296,9 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     case FLTEE_ALG_NON_OBLIVIOUS: case FLTEE_ALG_PATH_ORAM: break;
     default: return fail(FLTEE_ERROR_INVALID_PARAMETER);
     }
-    const size_t bpc = encrypted_parameters_size / n;  // lib.rs:305-306
-    if (bpc % 8) return fail(FLTEE_ERROR_INVALID_PARAMETER);  // (records must stay 8-B aligned)
+    // lib.rs:305-306: bytes per client floored, records per client floored; slice i
+    // starts at i*bpc even when that is not a record boundary (ragged payloads)
+    const size_t bpc = encrypted_parameters_size / n;
     const size_t rpc = bpc / 8;
     if (aggregation_alg == FLTEE_ALG_ADVANCED && n * num_of_sparse_parameters > n * rpc)
         return fail(FLTEE_ERROR_INVALID_PARAMETER);  // advanced.rs:72 out-of-bounds panic
@@ -386,7 +387,7 @@ extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_
                                                void *d_records, void *stream) {
     std::lock_guard<std::recursive_mutex> lk(api_mutex());
     DeviceCtx *c = current_ctx();
-    if (!c || bytes_per_client % 8) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (!c) return FLTEE_ERROR_INVALID_PARAMETER;
     if (!c->round_keys.reserve(n * 44 * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
     std::vector<uint32_t> rk(n * 44);
     for (size_t i = 0; i < n; ++i) {

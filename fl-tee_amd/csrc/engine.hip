@@ -358,3 +358,7 @@ extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float si
                ? FLTEE_SUCCESS
                : FLTEE_ERROR_UNEXPECTED;
 }
+
+namespace fltee { void set_dense_variant(int v); }
+// tuning hook (not part of the public header)
+extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(v); }

@@ -44,68 +44,80 @@ static __device__ __forceinline__ float4 ld_nt(const float4 *p) {
 
 // ---------------------------------------------------------------- dense ----
 // rec viewed as uint4 = two records {idx0, val0, idx1, val1}; row stride d2 = d/2.
-template <int V, int U, bool CLIP, bool ACC>
+// A block covers V*256 consecutive uint4 columns; lane t owns columns
+// base + t + v*256 (v < V), so every load instruction of a wave is 1 KB contiguous.
+template <typename T4>
+static __device__ __forceinline__ uint4 ld4(const uint4 *p, bool nt) {
+    return nt ? ld_nt(p) : *p;
+}
+
+template <int V, int U, bool CLIP, bool ACC, bool NT>
 __global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
                                                           uint32_t n, float coef,
                                                           float *__restrict__ out,
                                                           const float *__restrict__ ccoef,
                                                           uint32_t *status) {
-    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const size_t col0 = t * V;
-    if (col0 >= d2) return;
-    const int nv = (col0 + V <= d2) ? V : (int)(d2 - col0);
+    const size_t base = (size_t)blockIdx.x * (256 * V) + threadIdx.x;
     float acc[2 * V];
+    bool live[V];
 #pragma unroll
-    for (int i = 0; i < 2 * V; ++i) acc[i] = 0.0f;
+    for (int v = 0; v < V; ++v) {
+        acc[2 * v] = acc[2 * v + 1] = 0.0f;
+        live[v] = base + (size_t)v * 256 < d2;
+    }
+    if (!live[0]) return;
     uint32_t bad = 0;
-    const uint32_t j0 = (uint32_t)(2 * col0);
-    const uint4 *p = rec + col0;
+    const uint4 *p = rec + base;
     uint32_t c = 0;
-    if (nv == V) {
+    const bool full = live[V - 1];
+    if (full) {
         for (; c + U <= n; c += U) {
             uint4 x[U][V];
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[u][v] = ld_nt(p + (size_t)(c + u) * d2 + v);
+                for (int v = 0; v < V; ++v) x[u][v] = ld4<uint4>(p + (size_t)(c + u) * d2 + v * 256, NT);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                float cc = CLIP ? ccoef[c + u] : 1.0f;
+                const float cc = CLIP ? ccoef[c + u] : 1.0f;
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     float a = __uint_as_float(x[u][v].y), b = __uint_as_float(x[u][v].w);
                     if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
                     acc[2 * v] = __fadd_rn(acc[2 * v], a);
                     acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
-                    bad |= (x[u][v].x ^ (j0 + 2 * v)) | (x[u][v].z ^ (j0 + 2 * v + 1));
+                    const uint32_t j = (uint32_t)(2 * (base + (size_t)v * 256));
+                    bad |= (x[u][v].x ^ j) | (x[u][v].z ^ (j + 1));
                 }
             }
         }
     }
     for (; c < n; ++c) {
-        float cc = CLIP ? ccoef[c] : 1.0f;
-        for (int v = 0; v < nv; ++v) {
-            uint4 x = ld_nt(p + (size_t)c * d2 + v);
+        const float cc = CLIP ? ccoef[c] : 1.0f;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            if (!live[v]) continue;
+            const uint4 x = ld4<uint4>(p + (size_t)c * d2 + v * 256, NT);
             float a = __uint_as_float(x.y), b = __uint_as_float(x.w);
             if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
             acc[2 * v] = __fadd_rn(acc[2 * v], a);
             acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
-            bad |= (x.x ^ (j0 + 2 * v)) | (x.z ^ (j0 + 2 * v + 1));
+            const uint32_t j = (uint32_t)(2 * (base + (size_t)v * 256));
+            bad |= (x.x ^ j) | (x.z ^ (j + 1));
         }
     }
-    float2 *o = reinterpret_cast<float2 *>(out) + col0;
+    float2 *o = reinterpret_cast<float2 *>(out) + base;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-        if (v < nv) {
-            float2 r;
-            if (ACC) {
-                float2 prev = o[v];
-                r = make_float2(__fadd_rn(prev.x, acc[2 * v]), __fadd_rn(prev.y, acc[2 * v + 1]));
-            } else {
-                r = make_float2(__fmul_rn(acc[2 * v], coef), __fmul_rn(acc[2 * v + 1], coef));
-            }
-            o[v] = r;
+        if (!live[v]) continue;
+        float2 r;
+        if (ACC) {
+            const float2 prev = o[v * 256];
+            r = make_float2(__fadd_rn(prev.x, acc[2 * v]), __fadd_rn(prev.y, acc[2 * v + 1]));
+        } else {
+            r = make_float2(__fmul_rn(acc[2 * v], coef), __fmul_rn(acc[2 * v + 1], coef));
         }
+        o[v * 256] = r;
     }
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
@@ -132,17 +144,33 @@ __global__ __launch_bounds__(256) void dense_accumulate_s(const uint2 *__restric
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
 
+// Tuning hook (fltee_debug_set_dense_variant): 0 is the shipped configuration.
+static int g_dense_variant = 0;
+
+template <int V, int U, bool CLIP, bool ACC, bool NT>
+static void launch_v(const void *rec, size_t n, size_t d2, float coef, float *out,
+                     const float *ccoef, uint32_t *status, hipStream_t s) {
+    const unsigned blocks = (unsigned)((d2 + 256 * V - 1) / (256 * V));
+    hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC, NT>), dim3(blocks), dim3(256), 0, s,
+                       (const uint4 *)rec, d2, (uint32_t)n, coef, out, ccoef, status);
+}
+
 template <bool CLIP, bool ACC>
 static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef, float *out,
                                  const float *ccoef, uint32_t *status, hipStream_t s) {
     const bool aligned = ((uintptr_t)rec % 16 == 0) && ((uintptr_t)out % 8 == 0) && (d % 2 == 0);
     if (aligned) {
         const size_t d2 = d / 2;
-        constexpr int V = 1, U = 16;
-        const size_t threads = (d2 + V - 1) / V;
-        const unsigned blocks = (unsigned)((threads + 255) / 256);
-        hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
-                           (const uint4 *)rec, d2, (uint32_t)n, coef, out, ccoef, status);
+        switch (g_dense_variant) {
+        case 1: launch_v<1, 8, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 2: launch_v<1, 32, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 3: launch_v<2, 8, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 4: launch_v<2, 16, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 5: launch_v<1, 16, CLIP, ACC, false>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 6: launch_v<4, 4, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 7: launch_v<4, 8, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        default: launch_v<1, 16, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        }
     } else {
         const unsigned blocks = (unsigned)((d + 255) / 256);
         hipLaunchKernelGGL((dense_accumulate_s<CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
@@ -150,6 +178,8 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
     }
     return hipGetLastError();
 }
+
+void set_dense_variant(int v) { g_dense_variant = v; }
 
 hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,
                                    const float *client_coef, bool accumulate, uint32_t *status,

@@ -105,7 +105,15 @@ __host__ __device__ __forceinline__ void aes128_block(const uint32_t *T0, const 
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// lane -> (client c, block b); blocks_per_client = ceil(rec_per_client * 8 / 16)
+// lane -> (client c, block b); blocks_per_client = ceil(rec_per_client * 8 / 16).
+// ALIGNED: every slice starts on an 8-byte boundary (bpc % 8 == 0, the unchanged
+// client).  Otherwise (enc_len % n != 0: lib.rs:305 floors bpc, so slice i starts
+// at i*bpc) the ciphertext is read byte by byte; the output stays compact records.
+__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+template <bool ALIGNED>
 __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict__ cipher,
                                                       size_t n, size_t bpc, size_t rpc,
                                                       const uint32_t *__restrict__ rks,
@@ -122,14 +130,20 @@ __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict_
         uint32_t ks[4];
         aes128_block(T, T + 256, T + 512, T + 768, T + 1024, rks + c * 44, 0u, 0u,
                      (uint32_t)((uint64_t)b >> 32), (uint32_t)b, ks);
-        const uint2 *src = reinterpret_cast<const uint2 *>(cipher + c * bpc) + 2 * b;
         uint2 *dst = reinterpret_cast<uint2 *>(plain + c * rpc * 8) + 2 * b;
-        uint2 x = src[0];
-        dst[0] = make_uint2(x.x ^ bswap32(ks[0]), x.y ^ bswap32(ks[1]));
-        if (2 * b + 1 < rpc) {
-            uint2 y = src[1];
-            dst[1] = make_uint2(y.x ^ bswap32(ks[2]), y.y ^ bswap32(ks[3]));
+        const bool two = 2 * b + 1 < rpc;
+        uint2 x, y = make_uint2(0, 0);
+        if (ALIGNED) {
+            const uint2 *src = reinterpret_cast<const uint2 *>(cipher + c * bpc) + 2 * b;
+            x = src[0];
+            if (two) y = src[1];
+        } else {
+            const uint8_t *src = cipher + c * bpc + 16 * b;
+            x = make_uint2(ld_u32_bytes(src), ld_u32_bytes(src + 4));
+            if (two) y = make_uint2(ld_u32_bytes(src + 8), ld_u32_bytes(src + 12));
         }
+        dst[0] = make_uint2(x.x ^ bswap32(ks[0]), x.y ^ bswap32(ks[1]));
+        if (two) dst[1] = make_uint2(y.x ^ bswap32(ks[2]), y.y ^ bswap32(ks[3]));
     }
 }
 
@@ -153,13 +167,16 @@ hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_clie
                           hipStream_t s) {
     const size_t total = n * ((rec_per_client + 1) / 2);
     if (total == 0) return hipSuccess;
-    if (bytes_per_client % 8) return hipErrorInvalidValue;  // slices must stay 8-B aligned
     uint32_t *tables = device_tables(s);
     if (!tables) return hipErrorOutOfMemory;
     size_t blocks = (total + 255) / 256;
     if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(aes_ctr_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cipher, n,
-                       bytes_per_client, rec_per_client, round_keys, tables, plain);
+    if (bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0)
+        hipLaunchKernelGGL(aes_ctr_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, cipher, n,
+                           bytes_per_client, rec_per_client, round_keys, tables, plain);
+    else
+        hipLaunchKernelGGL(aes_ctr_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, cipher,
+                           n, bytes_per_client, rec_per_client, round_keys, tables, plain);
     return hipGetLastError();
 }
 

@@ -8,7 +8,7 @@
 // records (and hence the fold order) is bit-identical to the enclave's.
 //   mode 0: cond2 = (u32)idx[l] < (u32)idx[m]            (advanced.rs:166)
 //   mode 1: cond2 = u64[l] < u64[m]                      (stable composite keys)
-//   mode 2: cond2 = mix32(l ^ stepkey(seed,i,j)) & 1     (nips19.rs:66-105 shape;
+//   mode 2: cond2 = top bit of (l ^ stepkey(seed,i,j)) * 0x9E3779B1  (nips19.rs:66-105;
 //           keyed mixer replaces the running FxHash of heap addresses)
 // Every compare-exchange is branch-free (v_cndmask) and every address depends
 // only on (i, j, k): the memory trace is data-independent, like the cmov
@@ -38,7 +38,7 @@ __device__ __forceinline__ bool swap_rule(uint64_t a, uint64_t b, uint32_t l, ui
     bool lt;
     if (MODE == 0) lt = (uint32_t)a < (uint32_t)b;
     else if (MODE == 1) lt = a < b;
-    else lt = (mix32(l ^ key) & 1u) != 0;
+    else lt = ((l ^ key) * 0x9E3779B1u) >> 31;  // multiplicative hash, top bit
     return asc ^ lt;
 }
 

@@ -76,6 +76,7 @@ SIGNATURES = {
 }
 EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_aes_block": (None, [_P, _P, _P]),
+    "fltee_debug_set_dense_variant": (None, [ctypes.c_int]),
 }
 
 _lib = None

@@ -1,6 +1,6 @@
 /*
  * fltee_oracle.c — CPU restatement of FL-TEE's SGX enclave aggregation path
- * (secure_aggregation/enclave/src/*.rs).  TEST INFRASTRUCTURE ONLY: see the
+ * (secure_aggregation/enclave/src/ Rust files).  TEST INFRASTRUCTURE ONLY: see the
  * header for what may load it and for its parity status.
  *
  * Restated line-for-line, keeping the reference's loop structure and its x86
@@ -387,7 +387,7 @@ void fo_shuffle_keyed(fo_weight *s, size_t size, uint32_t seed) {
                 size_t l = ((k & mh) << 1) | (k & ml);
                 size_t m = l + j;
                 int cond1 = o_equal(l & i, 0);
-                int cond2 = (int)(fo_mix32((uint32_t)l ^ key) & 1u);
+                int cond2 = (int)((((uint32_t)l ^ key) * 0x9E3779B1u) >> 31);
                 o_swap((int64_t)(cond1 ^ cond2), (uint64_t *)&s[l], (uint64_t *)&s[m]);
             }
         }

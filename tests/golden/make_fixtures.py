@@ -132,6 +132,20 @@ def main():
                         flat_out=flat_out.astype(np.float32), clipping=1.0)
     print("l2clip d", flat_in.size)
 
+    # ---------------- client_level_dp_update_global_weights (update.py:207-224) --
+    # zero diffs: global += (0 + N(0, C*sigma)) / n, numpy RandomState(seed + 5)
+    # (fl_main.py:49) — the reference's seeded DP noise, for distribution checks
+    import numpy.random as npr
+    n_dp, sigma, clipping = 30, 1.12, 1.0
+    zeros = {key: torch.zeros_like(v) for key, v in model.state_dict().items()}
+    glob = {key: torch.zeros_like(v) for key, v in model.state_dict().items()}
+    update.client_level_dp_update_global_weights(glob, [zeros] * n_dp, sigma, clipping, 0.1,
+                                                 npr.RandomState(0 + 5))
+    dp_flat = utils.flatten_params(utils.get_learnable_parameters(glob, buffer_names)).numpy()
+    np.savez_compressed(os.path.join(OUT, "dp_reference.npz"), noise=dp_flat.astype(np.float32),
+                        n=n_dp, sigma=sigma, clipping=clipping)
+    print("dp_reference d", dp_flat.size, "std", dp_flat.std())
+
     # ---------------- src/ffi_test.py known answer (100 x 0x01, key 0, IV 0) ----
     src = bytes([1] * 100)
     ct = O.ref_aes_ctr_encrypt(bytes(16), src)

@@ -245,6 +245,31 @@ def test_dp_noise_statistics(dev):
     assert abs(np.mean((out / sd) ** 4) - 3) < 0.05
 
 
+def test_dp_noise_matches_reference_distribution(dev):
+    # the reference's seeded DP aggregate (update.py:207-224, RandomState(seed+5)) on zero
+    # updates, vs the device mechanism (common.rs:56-72): two-sample KS + std
+    import torch
+    from scipy import stats
+    fx = np.load(os.path.join(GOLDEN, "dp_reference.npz"))
+    ref = fx["noise"]
+    out = torch.zeros(ref.size, dtype=torch.float32, device="cuda")
+    dev.dp_noise(out, float(fx["sigma"]), float(fx["clipping"]), int(fx["n"]), seed=99)
+    got = out.cpu().numpy()
+    assert stats.ks_2samp(got, ref).pvalue > 1e-3
+    assert abs(got.std() / ref.std() - 1) < 0.02
+
+
+def test_dp_noise_matches_oracle_draws(dev, oracle):
+    # same Philox stream: device and oracle draw the same noise (f64 log/cos may differ
+    # in the last ulp before the f32 rounding)
+    import torch
+    d, n = 4096, 30
+    out = torch.zeros(d, dtype=torch.float32, device="cuda")
+    dev.dp_noise(out, 1.12, 1.0, n, seed=4242)
+    ref = oracle.dp_noise(np.zeros(d, np.float32), 1.12, 1.0, n, seed=4242)
+    assert np.allclose(out.cpu().numpy(), ref, rtol=1e-6, atol=1e-9)
+
+
 # ------------------------------------------------------------- clip --------
 def test_server_side_clip_matches_reference_torch(dev):
     fx = np.load(os.path.join(GOLDEN, "l2clip.npz"))

@@ -72,19 +72,26 @@ def test_empty_payload_k0(enclave, oracle, alg):
 
 
 @pytest.mark.parametrize("alg", [1, 3, 4, 5])
-def test_ragged_payload_tail_ignored(enclave, oracle, alg):
-    # enc_len not a multiple of n: lib.rs:305 floors bytes-per-client, the tail is ignored
+def test_ragged_payload(enclave, oracle, alg):
+    # enc_len not a multiple of n: lib.rs:305 floors bytes-per-client and slice i starts
+    # at i*bpc.  With one client the tail is simply ignored; with two, client 1's slice
+    # is shifted by 2 bytes and decrypts to garbage (idx >= d almost surely): the
+    # reference aggregates client 0 only — or panics in non_oblivious.  Same here.
     rng = np.random.default_rng(alg)
-    ids = np.array([5, 9], np.uint32)
     d, k = 100, 10
-    plain = []
-    for _ in ids:
-        idx = rng.choice(d, k, replace=False).astype(np.uint32)
-        val = rng.normal(0, 1, k).astype(np.float32)
-        plain.append(oracle.as_weights(idx, val).tobytes())
-    enc = oracle.encrypt_clients(ids, plain) + b"\x07" * 5
-    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 40 + alg, ids, d, k, alg, enc)
-    assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
+    for ids in (np.array([5], np.uint32), np.array([5, 9], np.uint32)):
+        plain = []
+        for _ in ids:
+            idx = rng.choice(d, k, replace=False).astype(np.uint32)
+            val = rng.normal(0, 1, k).astype(np.float32)
+            plain.append(oracle.as_weights(idx, val).tobytes())
+        enc = oracle.encrypt_clients(ids, plain) + b"\x07" * 5
+        fl = 40 + alg + 10 * len(ids)
+        (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, fl, ids, d, k, alg, enc)
+        assert st == 0 and rv == ost
+        if len(ids) == 1:
+            assert rv == 0
+        assert bits_equal(out, ref)
 
 
 @pytest.mark.parametrize("alg", [1, 3, 4, 5])

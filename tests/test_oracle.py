@@ -326,3 +326,15 @@ def test_numpy_axis0_sum_is_in_order(oracle):
     ref, _ = oracle.non_oblivious(oracle.as_weights(idx, v.reshape(-1)), d, n)
     got = np.sum(v, axis=0, dtype=np.float32) * np.float32(np.float32(1) / np.float32(n))
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_dp_noise_distribution_matches_reference(oracle):
+    # update.py:207-224 with zero diffs (numpy RandomState(seed+5), fl_main.py:49) vs the
+    # restated common.rs:56-72 mechanism: same N(0, C*sigma)/n law (two-sample KS)
+    from scipy import stats
+    fx = load("dp_reference")
+    ref = fx["noise"]
+    n, sigma, clipping = int(fx["n"]), float(fx["sigma"]), float(fx["clipping"])
+    got = oracle.dp_noise(np.zeros(ref.size, np.float32), sigma, clipping, n, seed=123)
+    assert stats.ks_2samp(got, ref).pvalue > 1e-3
+    assert abs(got.std() / ref.std() - 1) < 0.02
