@@ -680,7 +680,10 @@ uint32_t fo_ecall_secure_aggregation(uint32_t fl_id, uint32_t round, const uint3
     }
     free(scratch);
     free(w);
-    if (st) return st == FO_ERROR_ENCLAVE_CRASHED ? FO_ERROR_INVALID_PARAMETER : st;
+    if (st) { /* a panic aborts the ECALL: the bridge never copies [out] back */
+        memset(out, 0, d * sizeof(float));
+        return st == FO_ERROR_ENCLAVE_CRASHED ? FO_ERROR_INVALID_PARAMETER : st;
+    }
     if (c->dp) fo_dp_noise(out, d, c->sigma, c->clipping, n, next_seed());
     times[2] = (float)(now_s() - t2);
     c->round += 1; /* lib.rs:421 */
@@ -715,7 +718,10 @@ uint32_t fo_ecall_client_size_optimized_secure_aggregation(
     st = fo_client_size_optimized(batch, k, out, d, w, client_size, scratch, cap);
     free(scratch);
     free(w);
-    if (st) return st == FO_ERROR_ENCLAVE_CRASHED ? FO_ERROR_INVALID_PARAMETER : st;
+    if (st) { /* a panic aborts the ECALL: the bridge never copies [out] back */
+        memset(out, 0, d * sizeof(float));
+        return st == FO_ERROR_ENCLAVE_CRASHED ? FO_ERROR_INVALID_PARAMETER : st;
+    }
     times[1] = (float)(now_s() - t1);
     if (c->dp) fo_dp_noise(out, d, c->sigma, c->clipping, client_size, next_seed());
     c->round += 1;
