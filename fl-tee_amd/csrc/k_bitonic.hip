@@ -31,15 +31,12 @@
 
 namespace fltee {
 
+// cond2 of the compare-exchange at position l (see the header comment)
 template <int MODE>
-__device__ __forceinline__ bool swap_rule(uint64_t a, uint64_t b, uint32_t l, uint32_t imask,
-                                          uint32_t key) {
-    const bool asc = (l & imask) == 0;
-    bool lt;
-    if (MODE == 0) lt = (uint32_t)a < (uint32_t)b;
-    else if (MODE == 1) lt = a < b;
-    else lt = ((l ^ key) * 0x9E3779B1u) >> 31;  // multiplicative hash, top bit
-    return asc ^ lt;
+__device__ __forceinline__ bool cond2(uint64_t a, uint64_t b, uint32_t l, uint32_t key) {
+    if (MODE == 0) return (uint32_t)a < (uint32_t)b;
+    if (MODE == 1) return a < b;
+    return (((l ^ key) * 0x9E3779B1u) >> 31) != 0;  // multiplicative hash, top bit
 }
 
 // insert r zero bits at bit position d of g
@@ -49,11 +46,13 @@ __device__ __forceinline__ uint32_t spread(uint32_t g, uint32_t d, uint32_t r) {
 }
 
 // Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
-// records held in v[], whose first record sits at global position p0.
+// records held in v[], whose first record sits at global position p0.  The group
+// spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
+// is the same for every compare-exchange of the group: computed once.
 template <int MODE, int R>
 __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, uint32_t dlog,
                                             uint32_t ilog, uint32_t seed) {
-    const uint32_t imask = 1u << ilog;
+    const bool asc = (p0 & (1u << ilog)) == 0;
 #pragma unroll
     for (int lv = R - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
@@ -62,7 +61,7 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
             const uint64_t a = v[q], c = v[qm];
-            const bool sw = swap_rule<MODE>(a, c, p0 + ((uint32_t)q << dlog), imask, key);
+            const bool sw = asc ^ cond2<MODE>(a, c, p0 + ((uint32_t)q << dlog), key);
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
         }
@@ -113,37 +112,50 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t tlog, uint32_t 
     }
 }
 
-__device__ __forceinline__ void tile_load(uint64_t *sm, const uint64_t *g, uint32_t T) {
-    for (uint32_t e = threadIdx.x; e < T; e += blockDim.x) sm[lpad(e)] = g[e];
-}
-__device__ __forceinline__ void tile_store(const uint64_t *sm, uint64_t *g, uint32_t T) {
-    for (uint32_t e = threadIdx.x; e < T; e += blockDim.x) g[e] = sm[lpad(e)];
-}
-
-template <int MODE>
-__global__ __launch_bounds__(512) void bitonic_tile_sort(uint64_t *__restrict__ data,
-                                                         uint32_t tlog, int rmax,
-                                                         uint32_t seed) {
+// Persistent tile kernels: a block walks tiles blockIdx.x, +gridDim.x, ...; the
+// next tile's records are prefetched into registers (E <= 16 per lane, coalesced)
+// while the current tile runs its LDS rounds, so HBM and LDS work overlap
+// (T14-style issue-early / write-late staging).
+//   SORT  : all stages 2..T of each tile (first launch of a sort)
+//   !SORT : the steps j < T of stage ilog (merge after the global passes)
+template <int MODE, bool SORT>
+__global__ __launch_bounds__(512) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
+                                                     uint32_t ilog, int rmax, uint32_t seed,
+                                                     uint32_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     const uint32_t T = 1u << tlog;
-    const uint32_t base = blockIdx.x << tlog;
-    tile_load(sm, data + base, T);
-    __syncthreads();
-    for (uint32_t ilog = 1; ilog <= tlog; ++ilog) lds_steps<MODE>(sm, tlog, base, ilog, (int)ilog - 1, rmax, seed);
-    tile_store(sm, data + base, T);
-}
-
-template <int MODE>
-__global__ __launch_bounds__(512) void bitonic_tile_merge(uint64_t *__restrict__ data,
-                                                          uint32_t tlog, uint32_t ilog,
-                                                          int rmax, uint32_t seed) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const uint32_t T = 1u << tlog;
-    const uint32_t base = blockIdx.x << tlog;
-    tile_load(sm, data + base, T);
-    __syncthreads();
-    lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, rmax, seed);
-    tile_store(sm, data + base, T);
+    const uint32_t E = T / blockDim.x;  // records per lane, <= 16
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    uint64_t pf[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if ((uint32_t)r < E) pf[r] = data[((size_t)tile << tlog) + threadIdx.x + r * blockDim.x];
+    for (;;) {
+        const uint32_t base = tile << tlog;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if ((uint32_t)r < E) sm[lpad(threadIdx.x + r * blockDim.x)] = pf[r];
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        if (next < ntiles) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if ((uint32_t)r < E) pf[r] = data[((size_t)next << tlog) + threadIdx.x + r * blockDim.x];
+        }
+        if (SORT) {
+            for (uint32_t il = 1; il <= tlog; ++il)
+                lds_steps<MODE>(sm, tlog, base, il, (int)il - 1, rmax, seed);
+        } else {
+            lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, rmax, seed);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if ((uint32_t)r < E) data[(size_t)base + threadIdx.x + r * blockDim.x] = sm[lpad(threadIdx.x + r * blockDim.x)];
+        if (next >= ntiles) break;
+        __syncthreads();  // this tile's LDS reads retire before the next tile lands
+        tile = next;
+    }
 }
 
 // --------------------------------------------------------- global pass -----
@@ -207,8 +219,18 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     const unsigned threads = T / E ? T / E : 1;
     const int rmax = (int)log2_pow2(E);
     const size_t lds = (size_t)(T + T / 16 + 1) * 8;
-    hipLaunchKernelGGL((bitonic_tile_sort<MODE>), dim3(tiles), dim3(threads), lds, s, data, tlog,
-                       rmax, seed);
+    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    // persistent: two resident tiles per CU, each prefetching its next tile
+    const unsigned grid = tiles < 512 ? tiles : 512;
+    hipLaunchKernelGGL((bitonic_tiles<MODE, true>), dim3(grid), dim3(threads), lds, s, data, tlog,
+                       0u, rmax, seed, tiles);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     for (uint32_t ilog = tlog + 1; ilog <= mlog; ++ilog) {
@@ -222,8 +244,8 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
             if (e != hipSuccess) return e;
             jtop -= R;
         }
-        hipLaunchKernelGGL((bitonic_tile_merge<MODE>), dim3(tiles), dim3(threads), lds, s, data,
-                           tlog, ilog, rmax, seed);
+        hipLaunchKernelGGL((bitonic_tiles<MODE, false>), dim3(grid), dim3(threads), lds, s, data,
+                           tlog, ilog, rmax, seed, tiles);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
