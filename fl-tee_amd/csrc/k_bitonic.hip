@@ -71,42 +71,39 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 // ------------------------------------------------------------- LDS tile ----
 __device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
 
-// One LDS round: steps jtop..jtop-R+1 of stage ilog over the whole tile.
-// A lane handles up to 16 >> R groups of 2^R records (E = T / blockDim records
-// per lane; the host keeps R <= log2(E) so every lane is busy).
-template <int MODE, int R>
-__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t tlog, uint32_t base,
+// One LDS round: steps jtop..jtop-R+1 of stage ilog over the whole tile of
+// T = E * nt records.  Lane t handles the G = E >> R groups t + h*nt (R <= log2 E,
+// so every lane is busy).  nt is passed in, never read from blockDim inside the
+// rounds: hipcc reloads it with a vector load + vmcnt(0), which would drain the
+// tile prefetch in flight.
+template <int MODE, int R, int E>
+__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t nt, uint32_t base,
                                           uint32_t ilog, uint32_t jtop, uint32_t seed) {
-    constexpr int G = 16 >> R;  // groups per lane
+    constexpr int G = E >> R;
     const uint32_t dlog = jtop - R + 1;
-    const uint32_t ngroups = 1u << (tlog - R);
-    for (uint32_t g0 = threadIdx.x; g0 < ngroups; g0 += blockDim.x * G) {
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const uint32_t g = g0 + (uint32_t)h * blockDim.x;
-            if (g >= ngroups) break;
-            const uint32_t b = spread(g, dlog, R);
-            uint64_t v[1 << R];
+    for (int h = 0; h < G; ++h) {
+        const uint32_t g = threadIdx.x + (uint32_t)h * nt;
+        const uint32_t b = spread(g, dlog, R);
+        uint64_t v[1 << R];
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << dlog))];
-            group_steps<MODE, R>(v, base + b, dlog, ilog, seed);
+        for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << dlog))];
+        group_steps<MODE, R>(v, base + b, dlog, ilog, seed);
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << dlog))] = v[q];
-        }
+        for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << dlog))] = v[q];
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t tlog, uint32_t base,
-                                          uint32_t ilog, int jtop, int rmax, uint32_t seed) {
+template <int MODE, int E>
+__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t nt, uint32_t base, uint32_t ilog,
+                                          int jtop, uint32_t seed) {
+    constexpr int rmax = E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1));
     while (jtop >= 0) {
         const int r = jtop + 1 < rmax ? jtop + 1 : rmax;
-        switch (r) {
-        case 1: lds_round<MODE, 1>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
-        case 2: lds_round<MODE, 2>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
-        case 3: lds_round<MODE, 3>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
-        default: lds_round<MODE, 4>(sm, tlog, base, ilog, (uint32_t)jtop, seed); break;
-        }
+        if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
+        else lds_round<MODE, 1, E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
         __syncthreads();
         jtop -= r;
     }
@@ -118,40 +115,37 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t tlog, uint32_t 
 // (T14-style issue-early / write-late staging).
 //   SORT  : all stages 2..T of each tile (first launch of a sort)
 //   !SORT : the steps j < T of stage ilog (merge after the global passes)
-template <int MODE, bool SORT>
+// E = records per lane (T = E * blockDim) is a template parameter: a runtime
+// guard around each prefetch load makes hipcc branch and wait vmcnt(0) per load
+// (cdna_hip_programming.md §5 trap 4c), which serialises the prefetch.
+template <int MODE, bool SORT, int E>
 __global__ __launch_bounds__(512) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
-                                                     uint32_t ilog, int rmax, uint32_t seed,
+                                                     uint32_t ilog, uint32_t nt, uint32_t seed,
                                                      uint32_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const uint32_t T = 1u << tlog;
-    const uint32_t E = T / blockDim.x;  // records per lane, <= 16
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
-    uint64_t pf[16];
+    uint64_t pf[E];
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-        if ((uint32_t)r < E) pf[r] = data[((size_t)tile << tlog) + threadIdx.x + r * blockDim.x];
+    for (int r = 0; r < E; ++r) pf[r] = data[((size_t)tile << tlog) + threadIdx.x + r * nt];
     for (;;) {
         const uint32_t base = tile << tlog;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if ((uint32_t)r < E) sm[lpad(threadIdx.x + r * blockDim.x)] = pf[r];
+        for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * nt)] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        if (next < ntiles) {
+        // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
+        const uint32_t pft = next < ntiles ? next : tile;
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if ((uint32_t)r < E) pf[r] = data[((size_t)next << tlog) + threadIdx.x + r * blockDim.x];
-        }
+        for (int r = 0; r < E; ++r) pf[r] = data[((size_t)pft << tlog) + threadIdx.x + r * nt];
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE>(sm, tlog, base, il, (int)il - 1, rmax, seed);
+                lds_steps<MODE, E>(sm, nt, base, il, (int)il - 1, seed);
         } else {
-            lds_steps<MODE>(sm, tlog, base, ilog, (int)tlog - 1, rmax, seed);
+            lds_steps<MODE, E>(sm, nt, base, ilog, (int)tlog - 1, seed);
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            if ((uint32_t)r < E) data[(size_t)base + threadIdx.x + r * blockDim.x] = sm[lpad(threadIdx.x + r * blockDim.x)];
+        for (int r = 0; r < E; ++r) data[(size_t)base + threadIdx.x + r * nt] = sm[lpad(threadIdx.x + r * nt)];
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
         tile = next;
@@ -205,6 +199,34 @@ static int max_global_r() {
     return r;
 }
 
+template <int MODE, bool SORT, int E>
+static hipError_t launch_tiles_e(unsigned grid, unsigned threads, size_t lds, hipStream_t s,
+                                 uint64_t *data, uint32_t tlog, uint32_t ilog, int rmax,
+                                 uint32_t seed, uint32_t tiles) {
+    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    (void)rmax;  // implied by E
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E>), dim3(grid), dim3(threads), lds, s, data,
+                       tlog, ilog, (uint32_t)threads, seed, tiles);
+    return hipGetLastError();
+}
+
+template <int MODE, bool SORT>
+static hipError_t launch_tiles(uint32_t E, unsigned grid, unsigned threads, size_t lds,
+                               hipStream_t s, uint64_t *data, uint32_t tlog, uint32_t ilog,
+                               int rmax, uint32_t seed, uint32_t tiles) {
+    switch (E) {
+    case 2: return launch_tiles_e<MODE, SORT, 2>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+    case 4: return launch_tiles_e<MODE, SORT, 4>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+    case 8: return launch_tiles_e<MODE, SORT, 8>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+    default: return launch_tiles_e<MODE, SORT, 16>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+    }
+}
+
 template <int MODE>
 static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s) {
     const int kMaxGlobalR = max_global_r();
@@ -219,19 +241,10 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     const unsigned threads = T / E ? T / E : 1;
     const int rmax = (int)log2_pow2(E);
     const size_t lds = (size_t)(T + T / 16 + 1) * 8;
-    static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
     // persistent: two resident tiles per CU, each prefetching its next tile
     const unsigned grid = tiles < 512 ? tiles : 512;
-    hipLaunchKernelGGL((bitonic_tiles<MODE, true>), dim3(grid), dim3(threads), lds, s, data, tlog,
-                       0u, rmax, seed, tiles);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_tiles<MODE, true>(E, grid, threads, lds, s, data, tlog, 0u, rmax, seed,
+                                            tiles);
     if (e != hipSuccess) return e;
     for (uint32_t ilog = tlog + 1; ilog <= mlog; ++ilog) {
         int jtop = (int)ilog - 1;
@@ -244,9 +257,7 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
             if (e != hipSuccess) return e;
             jtop -= R;
         }
-        hipLaunchKernelGGL((bitonic_tiles<MODE, false>), dim3(grid), dim3(threads), lds, s, data,
-                           tlog, ilog, rmax, seed, tiles);
-        e = hipGetLastError();
+        e = launch_tiles<MODE, false>(E, grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -308,3 +308,32 @@ def test_headline_shape_100x1M_bit_exact(dev):
     assert bits_equal(out, ref)
     # bench checksum (benchmark.rs:226-239)
     assert abs(float(out.astype(np.float64).sum()) - float(v.astype(np.float64).sum()) / n) < 1e-3
+
+
+# ------------------------------------------------- multi-GPU building blocks ----
+def test_parallel_paths_single_rank(dev, oracle):
+    """fltee.parallel with the real kernels (world = 1): column split + dense kernel, and
+    client-range `advanced` partials combined by fltee_sum_rows_device (alg-6 order)."""
+    import torch
+
+    from fltee import parallel as P
+    rng = np.random.default_rng(77)
+    n, d = 6, 1001
+    dense = rng.normal(0, 0.01, (n, d)).astype(np.float32)
+    rec, lo, hi = P.split_dense_columns(torch.from_numpy(dense).cuda(), 1, 0)
+    full = P.param_sharded_dense(rec, n, hi - lo, d, 1, 0).cpu().numpy()
+    ref = oracle.baseline(oracle.as_weights(np.tile(np.arange(d, dtype=np.uint32), n),
+                                            dense.reshape(-1)), d, n)
+    assert bits_equal(full, ref)
+    nc, dk, k = 8, 700, 40
+    idx, val = rand_sparse(rng, nc, dk, k)
+    out = P.client_sharded_advanced(cuda_records(dev, idx, val), nc, k, dk, nc, 1, 0)
+    ref, st = oracle.client_size_optimized(nc, k, oracle.as_weights(idx, val), dk, nc)
+    assert st == 0 and bits_equal(out.cpu().numpy(), ref)
+    # two "ranks" emulated in one process: partials of clients [0,4) and [4,8) summed in order
+    parts = [dev.aggregate(1, cuda_records(dev, idx[c0 * k:c1 * k], val[c0 * k:c1 * k]),
+                           c1 - c0, k, dk, no_average=True) for c0, c1 in ((0, 4), (4, 8))]
+    coef = float(np.float32(1) / np.float32(nc))
+    got = dev.sum_rows(torch.stack(parts), coef).cpu().numpy()
+    ref, st = oracle.client_size_optimized(4, k, oracle.as_weights(idx, val), dk, nc)
+    assert st == 0 and bits_equal(got, ref)
