@@ -110,6 +110,48 @@ def bench_workload(torch, D, name, steps, warmup, device, nbuf=3):
                 rate=n * kk / kern, bytes=n * kk * 8 + d * 4)
 
 
+def bench_c5_sharded(torch, D, dist, world, rank, device, steps, warmup):
+    """configs[4] across the node (SURVEY §8e Option A, strong scaling): C5's 1000
+    clients x 100K records over d = 10M are split by client range; every rank runs
+    `advanced` on its clients (un-averaged partial), the partials are gathered to rank 0
+    over RCCL and summed there in rank order, x 1f32/n (fltee/parallel.py) — the
+    reference's alg 6 with batch = n / world.  Timed on every rank, max over ranks."""
+    from fltee import parallel as P
+    w = WORKLOADS["c5"]
+    n, d, k = w["n"], w["d"], w["k"]
+    lo, hi = P.shard_range(n, world, rank)
+    rec = make_records(torch, hi - lo, d, k, 5000 + rank, device)
+    part = torch.empty(d, dtype=torch.float32, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    D.reserve(1, hi - lo, k, d)
+
+    def partial(r, n_, k_, d_):
+        return D.aggregate(1, r, n_, k_, d_, out=part, no_average=True, status=status)
+
+    def step():
+        P.client_sharded_advanced(rec, hi - lo, k, d, n, world, rank, compute_partial=partial)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
+    del rec
+    wall = float(t[0]) / steps
+    return dict(desc=w["desc"] + f", client-range sharded x{world} + RCCL gather, rank-order sum",
+                alg="advanced", n=n, d=d, k=k, ms_per_step=wall * 1e3, value=n * k / wall,
+                unit="client-params/s", scaling="strong")
+
+
 def cpu_baseline_sample(d, n, seconds):
     """The oracle's `baseline` (baseline.rs o_update: one cmov RMW per 64-B line of the
     d-float output per record) on a bounded prefix of client 0's dense records,
@@ -209,10 +251,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FLTEE_BENCH_BACKEND=gloo + FLTEE_BENCH_ONE_DEVICE=1 rehearse the N>1 code path
+    # with every rank on cuda:0 (RCCL refuses two ranks on one GPU); the default is
+    # RCCL with one GPU per rank.
+    if os.environ.get("FLTEE_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("FLTEE_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     w = WORKLOADS[args.workload]
     n, d, k = w["n"], w["d"], w["k"]
     kk = d if k is None else k
@@ -223,7 +274,9 @@ def main():
     gathered = ([torch.empty(d, dtype=torch.float32, device=device) for _ in range(world)]
                 if (world > 1 and rank == 0) else None)
     kw = dict(dense=k is None, status=status)
-    D.reserve(w["alg"], n, kk, d, dense=k is None)
+    if w.get("dp"):
+        kw.update(dp=True, sigma=1.12, clipping=1.0, seed=7)
+    D.reserve(w["alg"], n, kk, d, **{x: y for x, y in kw.items() if x != "status"})
     stream = torch.cuda.current_stream()
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -260,7 +313,11 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = world * n * kk / (elapsed / args.steps)
     algo_bytes = n * kk * 8 + d * 4  # records read + averaged output written, per launch
-    del recs
+    del recs, gathered
+    sharded = None
+    if world > 1 and not args.no_extra:
+        sharded = bench_c5_sharded(torch, D, dist, world, rank, device,
+                                   steps=max(3, args.steps // 10), warmup=1)
 
     if rank == 0:
         line = {
@@ -292,6 +349,8 @@ def main():
                                    kernel_ms=r["kernel_s"] * 1e3, value=r["rate"],
                                    unit="client-params/s")
             line["extra"] = extra
+        if sharded is not None:
+            line["extra"] = {"c5_sharded": sharded}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -89,6 +89,9 @@ hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold
                        uint32_t *status, hipStream_t s);
 hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
                           hipStream_t s);
+// k_compact.hip
+hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
+                                  float *out, bool accumulate, hipStream_t s);
 hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,
                                  uint32_t *status, hipStream_t s);
 hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,

@@ -132,6 +132,8 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
 }
 
 // `advanced` over n clients' records into out (coef or accumulate).
+static bool g_advanced_compaction = true;  // fltee_debug_set_advanced_compaction
+
 static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k, size_t d,
                                size_t k_req, size_t halo, float coef, float *out, bool acc,
                                uint32_t *status, hipStream_t s) {
@@ -141,7 +143,14 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     hipError_t e = launch_advanced_init(rec, n * k, d, M, A, s);
     if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
     if (e == hipSuccess) e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
-    if (e == hipSuccess) e = bitonic_sort(B, M, 0, 0, s);
+    if (e != hipSuccess) return e;
+    // Second sort (advanced.rs:106-111): with fold_len == L its [0, d) prefix is the
+    // order-preserving compaction of the idx < d representatives (k_compact.hip);
+    // the k_req != k quirk leaves unfolded records competing for that prefix and
+    // keeps the full network.
+    if (fold_len == L && g_advanced_compaction)
+        return launch_compact_extract(B, A, L, d, coef, out, acc, s);
+    e = bitonic_sort(B, M, 0, 0, s);
     if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
     return e;
 }
@@ -362,3 +371,5 @@ extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float si
 namespace fltee { void set_dense_variant(int v); }
 // tuning hook (not part of the public header)
 extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(v); }
+// A/B hook: 0 runs advanced's second bitonic sort instead of the compaction network
+extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_compaction = on != 0; }

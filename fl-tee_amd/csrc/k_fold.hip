@@ -5,22 +5,29 @@
 //                    pads to M = next_pow2 (:133-142)
 //   [bitonic sort, mode 0]
 //   fold           : the oblivious fold (:66-101), EXACT and oblivious:
-//   [bitonic sort, mode 0]
+//   [second sort -> k_compact.hip, or bitonic sort mode 0 for the k quirk]
 //   extract        : global[i] = v[i].1 (:32-34) * 1f32/n (common.rs:14-19)
 //
 // The fold.  The enclave walks the sorted array once, carrying (pre_idx,
 // pre_val): position p-1 receives (u32::MAX - (p-1), 0.0) if p continues the
 // run of p-1, else the run's left-to-right sum.  A parallel scan would
 // re-associate that sum.  Instead every lane folds its own chunk of C
-// positions sequentially, after re-folding the H positions in front of it
-// (the halo): whenever no run is longer than H+1 the carry entering the chunk
-// is then bit-identical to the enclave's.  With each client's indices distinct
-// (top-k, utils.py:327-354) a run holds at most n+1 records, so H = n.  Every
-// lane performs the same H+C LDS reads whatever the data (oblivious); a run
-// longer than H+1 is detected (S[q].idx == S[q-H-1].idx) and reported as
-// FLTEE_DEV_ERR_FOLD_OVERFLOW so the host can re-run with a larger halo.
-// Tile: W = 256*C outputs + H+2 halo records in LDS, padded one slot per C
-// records so the 64 lanes' chunk walks hit distinct banks.
+// positions sequentially, after re-folding the Hr >= H positions in front of
+// it (the halo): whenever the run crossing the chunk start began inside the
+// halo, the carry entering the chunk is bit-identical to the enclave's.  With
+// each client's indices distinct (top-k, utils.py:327-354) a run holds at most
+// n+1 records, so H = n.  A lane whose carry could be wrong (key[a-Hr-1] ==
+// key[a-1] == key[a]) reports FLTEE_DEV_ERR_FOLD_OVERFLOW and the host re-runs
+// with a larger halo.  Every lane performs the same Hr+C+16 steps whatever the
+// data (oblivious).
+//
+// Layout: C >= Hr (halo work <= 2x), so a lane walks a long chunk; the 64
+// lanes of a wave walk 64 chunks in lockstep, 16 records per stage.  A stage's
+// 64 windows of 16 records (128 B each) are loaded coalesced (8 lanes per
+// window) one stage ahead into registers, transposed through LDS (row stride
+// 17 records: conflict-free 8-B reads), folded, and the outputs go back out
+// through the same LDS rows as coalesced 128-B stores.  No block barriers:
+// every wave works alone.
 #include "common.h"
 
 namespace fltee {
@@ -45,84 +52,122 @@ hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m
     return hipGetLastError();
 }
 
-constexpr int FOLD_C = 16;
-constexpr int FOLD_CLOG = 4;
-constexpr int FOLD_W = 256 * FOLD_C;
+constexpr uint32_t FS_W = 16;    // records per window (one 128-B line)
+constexpr uint32_t FS_ROW = 17;  // LDS row stride in records (conflict-free lane reads)
+typedef unsigned int fs_u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t padi(uint32_t e) { return e + (e >> FOLD_CLOG); }
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
-__global__ __launch_bounds__(256) void fold_kernel(const uint64_t *__restrict__ src,
-                                                   uint64_t *__restrict__ dst, size_t m,
-                                                   size_t fold_len, uint32_t H,
-                                                   uint32_t *status) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    const long long start = (long long)blockIdx.x * FOLD_W;
-    const long long lo = start - (long long)H - 1;  // global position of local 0
-    const uint32_t nload = FOLD_W + H + 2;
-    for (uint32_t e = threadIdx.x; e < nload; e += 256) {
-        const long long g = lo + e;
-        sm[padi(e)] = (g >= 0 && g < (long long)m) ? src[g] : 0ull;
+// One wave per block; lane l of wave w owns positions [a, a + C), a = (w*64 + l)*C.
+__global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restrict__ src,
+                                                         uint64_t *__restrict__ dst, long long m,
+                                                         long long fold_len, uint32_t Hr,
+                                                         uint32_t C, uint32_t *status) {
+    __shared__ uint64_t win[2][64 * FS_ROW];
+    const uint32_t l = threadIdx.x;
+    const long long wave0 = (long long)blockIdx.x * 64 * C;  // first position of lane 0
+    const long long a = wave0 + (long long)l * C;
+    const uint32_t nstage = (Hr + C + FS_W) / FS_W;
+    const uint32_t hw = Hr / FS_W;  // stage s holds window u = s - hw of the chunk
+
+    // carry check (see header): only the first owned position consumes the carry
+    if (a < fold_len && a - (long long)Hr - 1 >= 0 && a < m) {
+        const uint32_t k1 = rec_idx(src[a - 1]);
+        if (rec_idx(src[a - Hr - 1]) == k1 && rec_idx(src[a]) == k1)
+            atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
     }
-    __syncthreads();
 
-    const long long a = start + (long long)threadIdx.x * FOLD_C;  // first owned position
-    uint64_t res[FOLD_C];
-    uint32_t overflow = 0;
-    // halo re-fold: positions [a - H, a)
+    // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
+    const uint32_t part = (l & 7) * 2;
+    fs_u32x4 pf[8];
+    auto load_stage = [&](uint32_t s) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t w = (l >> 3) + 8 * i;
+            const long long g = wave0 + (long long)w * C - Hr + (long long)s * FS_W + part;
+            if (g >= 0 && g < m) {
+                pf[i] = __builtin_nontemporal_load((const fs_u32x4 *)(src + g));
+            } else {
+                pf[i] = fs_u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+    };
+    load_stage(0);
+
     uint32_t pre_idx = 0;
     float pre_val = 0.0f;
-    long long q = a - (long long)H;
     bool started = false;
-    for (uint32_t it = 0; it < H + FOLD_C; ++it, ++q) {
-        const uint32_t e = (uint32_t)(q - lo);
-        const uint64_t cur = sm[padi(e)];
-        const uint32_t ci = rec_idx(cur);
-        const float cv = rec_val(cur);
-        if (q >= 0) {
-            const bool eq = started && (ci == pre_idx);
-            pre_val = eq ? __fadd_rn(pre_val, cv) : cv;
-            pre_idx = ci;
-            started = true;
-        }
-        if (it >= H) {
-            const uint32_t r = it - H;
-            // output for position q (only meaningful for q < fold_len)
-            const uint64_t nxt = sm[padi(e + 1)];
-            const bool cont = (q + 1 < (long long)fold_len) && (rec_idx(nxt) == ci);
-            const uint64_t folded = cont ? (uint64_t)(0xFFFFFFFFu - (uint32_t)q)  // (MAX-q, +0.0)
-                                         : make_rec(ci, pre_val);
-            res[r] = (q < (long long)fold_len) ? folded : cur;
-            const uint64_t back = sm[padi(e - H - 1)];
-            overflow |= (q >= (long long)H + 1 && q < (long long)fold_len &&
-                         rec_idx(back) == ci);
-        }
-    }
-    __syncthreads();
+    uint64_t prev = 0;
+    for (uint32_t s = 0; s < nstage; ++s) {
+        uint64_t *cur = win[s & 1], *old = win[(s + 1) & 1];
 #pragma unroll
-    for (int r = 0; r < FOLD_C; ++r) sm[padi((uint32_t)(a + r - lo))] = res[r];
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < FOLD_W; e += 256) {
-        const long long g = start + e;
-        if (g < (long long)m) dst[g] = sm[padi((uint32_t)(g - lo))];
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t w = (l >> 3) + 8 * i;
+            cur[w * FS_ROW + part] = ((uint64_t)pf[i].y << 32) | pf[i].x;
+            cur[w * FS_ROW + part + 1] = ((uint64_t)pf[i].w << 32) | pf[i].z;
+        }
+        if (s + 1 < nstage) load_stage(s + 1);
+        wave_sync_lds();
+        uint64_t r[FS_W];
+#pragma unroll
+        for (uint32_t t = 0; t < FS_W; ++t) r[t] = cur[l * FS_ROW + t];
+        const long long q0 = a - (long long)Hr + (long long)s * FS_W;
+#pragma unroll
+        for (uint32_t t = 0; t < FS_W; ++t) {
+            const long long q = q0 + t;  // this step reads position q, emits position q - 1
+            const uint32_t ci = rec_idx(r[t]);
+            const bool eq = started && ci == pre_idx;
+            const uint64_t emit =
+                (q - 1 >= fold_len) ? prev
+                : (q < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(q - 1))  // (MAX-p, +0.0)
+                                       : make_rec(pre_idx, pre_val);
+            if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
+            else cur[l * FS_ROW + t - 1] = emit;
+            if (q >= 0) {
+                pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
+                pre_idx = ci;
+                started = true;
+            }
+            prev = r[t];
+        }
+        wave_sync_lds();
+        // window u = s - 1 - hw of every chunk is complete in `old`: store it
+        const long long u = (long long)s - 1 - hw;
+        if (u >= 0 && u < (long long)(C / FS_W)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t w = (l >> 3) + 8 * i;
+                const long long g = wave0 + (long long)w * C + u * FS_W + part;
+                if (g < m) {
+                    const uint64_t x0 = old[w * FS_ROW + part], x1 = old[w * FS_ROW + part + 1];
+                    const fs_u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
+                                        (uint32_t)(x1 >> 32)};
+                    __builtin_nontemporal_store(v, (fs_u32x4 *)(dst + g));
+                }
+            }
+        }
+        wave_sync_lds();
     }
-    if (overflow) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
 }
 
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
                        uint32_t *status, hipStream_t s) {
-    const uint32_t H = (uint32_t)halo;
-    const size_t nload = FOLD_W + (size_t)H + 2;
-    const size_t lds = (nload + nload / FOLD_C + 2) * 8;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
-        attr = true;
-    }
-    const unsigned blocks = (unsigned)((m + FOLD_W - 1) / FOLD_W);
-    hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), lds, s, src, dst, m, fold_len, H,
-                       status);
+    if (m == 1)  // nothing to fold: position 0 receives itself (:102-103)
+        return hipMemcpyAsync(dst, src, 8, hipMemcpyDeviceToDevice, s);
+    if (m == 0 || (m & 1)) return hipErrorInvalidValue;  // m = next_pow2: 16-B windows
+    const size_t Hr = (halo + FS_W - 1) / FS_W * FS_W;
+    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
+    size_t C = 64;
+    while (C < Hr) C <<= 1;
+    while (C > 64 && m / (64 * C) < 1024) C >>= 1;  // keep >= ~1024 waves when halo allows
+    const size_t lanes = (m + C - 1) / C;
+    const size_t blocks = (lanes + 63) / 64;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fold_stream_kernel, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
+                       (long long)m, (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
     return hipGetLastError();
 }
 

@@ -182,6 +182,72 @@ def test_advanced_bit_exact(dev, oracle, n, d, k):
     assert st == 0 and bits_equal(out, ref)
 
 
+def _advanced_both_ways(dev, rec, n, k, d):
+    """advanced with the compaction network (default) and with the enclave's second
+    bitonic sort (advanced.rs:106-111)."""
+    from fltee import _lib as L
+    try:
+        a = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+        assert dev.status() == 0
+        L.lib().fltee_debug_set_advanced_compaction(0)
+        b = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+        assert dev.status() == 0
+    finally:
+        L.lib().fltee_debug_set_advanced_compaction(1)
+    return a, b
+
+
+# (n, d, k): compaction levels log2(L - d) = 3 / 14 / 19 / 23 -> 1 / 2 / 3 / 4 passes
+@pytest.mark.parametrize("n,d,k", [(2, 1_000_000, 3), (1000, 16, 16), (100, 50890, 5089),
+                                   (300, 2_000_000, 20_000)])
+def test_advanced_compaction_equals_second_sort(dev, oracle, n, d, k):
+    rng = np.random.default_rng(n + d + k)
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    a, b = _advanced_both_ways(dev, rec, n, k, d)
+    assert bits_equal(a, b)
+    if n * k + d <= 600_000:
+        ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+        assert st == 0 and bits_equal(a, ref)
+
+
+def test_advanced_compaction_out_of_range_and_repeated_indices(dev, oracle):
+    # indices >= d fold into their own runs and never reach [0, d); a client's
+    # repeated index makes runs longer than n+1 (halo re-run by the ECALL layer,
+    # here given directly)
+    rng = np.random.default_rng(11)
+    n, d, k = 20, 3000, 400
+    idx = rng.integers(0, d + 64, n * k).astype(np.uint32)
+    val = rng.normal(0, 1, n * k).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    from fltee import _lib as L
+    try:
+        a = dev.aggregate(1, rec, n, k, d, fold_halo=n * k + d).cpu().numpy()
+        L.lib().fltee_debug_set_advanced_compaction(0)
+        b = dev.aggregate(1, rec, n, k, d, fold_halo=n * k + d).cpu().numpy()
+    finally:
+        L.lib().fltee_debug_set_advanced_compaction(1)
+    assert dev.status() == 0
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(a, ref) and bits_equal(b, ref)
+
+
+def test_advanced_compaction_c5_scale(dev):
+    """configs[4] at full size (M = 2^27): compaction network == second bitonic sort,
+    bit for bit, and the checksum of the average equals the sum of all values / n."""
+    import torch
+    n, d, k = 1000, 10_000_000, 100_000
+    g = torch.Generator(device="cuda").manual_seed(3)
+    vals = torch.randn(n, k, generator=g, device="cuda") * 0.01
+    off = torch.randint(0, d, (n, 1), generator=g, device="cuda")
+    idx = (off + torch.arange(k, device="cuda").unsqueeze(0)) % d
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
+    a, b = _advanced_both_ways(dev, rec, n, k, d)
+    assert bits_equal(a, b)
+    tot = float(vals.double().sum()) / n
+    assert abs(float(np.sum(a, dtype=np.float64)) - tot) < 1e-4 * max(1.0, abs(tot))
+
+
 def test_advanced_k0_quirk_bit_exact(dev, oracle):
     rng = np.random.default_rng(5)
     n, d = 5, 300
