@@ -368,8 +368,9 @@ extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float si
                : FLTEE_ERROR_UNEXPECTED;
 }
 
-namespace fltee { void set_dense_variant(int v); }
+namespace fltee { void set_dense_variant(int v); void set_compact_variant(int v); }
 // tuning hook (not part of the public header)
 extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(v); }
 // A/B hook: 0 runs advanced's second bitonic sort instead of the compaction network
 extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_compaction = on != 0; }
+extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_variant(v); }

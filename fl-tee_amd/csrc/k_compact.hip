@@ -32,72 +32,77 @@
 
 namespace fltee {
 
-constexpr uint32_t CP_CAP = 8192;  // records per LDS tile (64 KiB) -> 2 blocks per CU
-constexpr uint32_t CP_NT = 512;
-constexpr uint32_t CP_PER = CP_CAP / CP_NT;
-constexpr uint64_t CP_DUMMY = 0xFFFFFFFFull;  // (u32::MAX, +0.0): never selected
+constexpr uint64_t CP_DUMMY = 0xFFFFFFFFull;  // c = u32::MAX (never selected), +0.0
 
-__device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint32_t ps, uint64_t right, uint32_t pr,
-                                            uint32_t j, uint32_t d) {
-    const uint32_t is = (uint32_t)self, ir = (uint32_t)right;
-    const bool mv = ir < d && (((pr - ir) >> j) & 1u);
-    const bool st = is < d && !(((ps - is) >> j) & 1u);
+// In flight the key is not idx but c = p0 - idx, the record's total left shift
+// (p0 = its position after the fold), u32::MAX for records that are not selected
+// (idx >= d).  Level j moves a record iff bit j of c is set (c < 2^31 <= the top
+// bit of a dummy, which therefore never moves and never stays).
+__device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint32_t j) {
+    const uint32_t cs = (uint32_t)self, cr = (uint32_t)right;
+    const bool mv = ((cr >> j) & ~(cr >> 31)) & 1u;
+    const bool st = !((cs >> j) & 1u);
     return mv ? right : (st ? self : CP_DUMMY);
 }
 
-// FINAL: 0 = write records, 1 = out[i] = val*coef, 2 = out[i] += val
-template <int FINAL>
-__global__ __launch_bounds__(CP_NT) void compact_pass(const uint64_t *__restrict__ src,
-                                                      uint64_t *__restrict__ dst, uint32_t L,
-                                                      uint32_t d, uint32_t j0, uint32_t G,
-                                                      uint32_t logW, uint32_t S, uint32_t rows,
-                                                      uint32_t ngroups, float coef,
-                                                      float *__restrict__ out) {
-    __shared__ uint64_t sm[CP_CAP];
+// FIRST: src holds folded records (idx, val); else (c, val).
+// FINAL: 0 = write (c, val) records, 1 = out[i] = val*coef, 2 = out[i] += val.
+template <int CAP, int NT, bool FIRST, int FINAL>
+__global__ __launch_bounds__(NT) void compact_pass(const uint64_t *__restrict__ src,
+                                                   uint64_t *__restrict__ dst, uint32_t L,
+                                                   uint32_t d, uint32_t j0, uint32_t G,
+                                                   uint32_t logW, uint32_t S, uint32_t rows,
+                                                   uint32_t ngroups, float coef,
+                                                   float *__restrict__ out) {
+    constexpr uint32_t PER = CAP / NT;
+    __shared__ uint64_t sm[CAP];
     const uint32_t W = 1u << logW, H = (1u << G) - 1;
     const uint32_t band = blockIdx.x / ngroups, grp = blockIdx.x - band * ngroups;
     const uint32_t s0 = band * S, b0 = grp << logW;
-    const uint32_t nrows = min(S + H, rows - s0);  // rows of this tile that exist
     const uint32_t t = threadIdx.x;
+    const uint32_t nld = min(S + H, rows - s0) << logW;  // tile slots that map below L's rows
     auto pos_of = [&](uint32_t f) -> uint32_t {
         return ((s0 + (f >> logW)) << j0) + b0 + (f & (W - 1));
     };
 #pragma unroll
-    for (uint32_t i = 0; i < CP_PER; ++i) {
-        const uint32_t f = t + i * CP_NT;
-        if (f < nrows * W) {
+    for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t f = t + i * NT;
+        uint64_t v = CP_DUMMY;
+        if (f < nld) {
             const uint32_t p = pos_of(f);
-            sm[f] = p < L ? src[p] : CP_DUMMY;
+            if (p < L) {
+                v = src[p];
+                if (FIRST) {
+                    const uint32_t idx = (uint32_t)v;
+                    v = (v & 0xFFFFFFFF00000000ull) | (idx < d ? (uint64_t)(p - idx) : CP_DUMMY);
+                }
+            }
         }
+        sm[f] = v;
     }
     __syncthreads();
-    uint64_t nv[CP_PER];
+    uint64_t nv[PER];
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t stepf = W << g;
-        const uint32_t lim = min(S + H - ((2u << g) - 1), nrows) * W;
-        const uint32_t have = nrows * W;
+        const uint32_t lim = (S + H - ((2u << g) - 1)) << logW;  // rows still needed after g
         const uint32_t j = j0 + g;
 #pragma unroll
-        for (uint32_t i = 0; i < CP_PER; ++i) {
-            const uint32_t f = t + i * CP_NT;
-            if (f < lim) {
-                const uint32_t ps = pos_of(f);
-                const uint64_t right = (f + stepf < have) ? sm[f + stepf] : CP_DUMMY;
-                nv[i] = cp_pick(sm[f], ps, right, ps + (1u << j), j, d);
-            }
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t f = t + i * NT;
+            if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], j);
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t i = 0; i < CP_PER; ++i) {
-            const uint32_t f = t + i * CP_NT;
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t f = t + i * NT;
             if (f < lim) sm[f] = nv[i];
         }
         __syncthreads();
     }
-    const uint32_t nout = min(S, nrows) * W;
+    const uint32_t nout = min(S << logW, nld);
 #pragma unroll
-    for (uint32_t i = 0; i < CP_PER; ++i) {
-        const uint32_t f = t + i * CP_NT;
+    for (uint32_t i = 0; i < PER; ++i) {
+        const uint32_t f = t + i * NT;
         if (f < nout) {
             const uint32_t p = pos_of(f);
             if (FINAL == 0) {
@@ -108,6 +113,26 @@ __global__ __launch_bounds__(CP_NT) void compact_pass(const uint64_t *__restrict
             }
         }
     }
+}
+
+static int g_compact_variant = 0;  // fltee_debug_set_compact_variant (A/B): 0 = 64 KiB tiles
+void set_compact_variant(int v) { g_compact_variant = v; }
+
+template <int CAP, int NT>
+static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
+                              uint64_t *dst, uint32_t L, uint32_t d, uint32_t j0, uint32_t G,
+                              uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
+                              float coef, float *out) {
+#define CP_GO(F, X)                                                                           \
+    hipLaunchKernelGGL((compact_pass<CAP, NT, F, X>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
+                       d, j0, G, logW, S, rows, ngroups, coef, out)
+    if (first) {
+        if (fin == 0) CP_GO(true, 0); else if (fin == 1) CP_GO(true, 1); else CP_GO(true, 2);
+    } else {
+        if (fin == 0) CP_GO(false, 0); else if (fin == 1) CP_GO(false, 1); else CP_GO(false, 2);
+    }
+#undef CP_GO
+    return hipGetLastError();
 }
 
 static uint32_t bitlen(uint64_t x) {
@@ -123,23 +148,25 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
     if (d == 0) return hipSuccess;
     const uint32_t nlev = L > d ? bitlen(L - d) : 0;
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
+    const bool small = g_compact_variant == 1;
+    const uint32_t CAP = small ? 4096 : 8192;
     uint64_t *cur = src, *oth = tmp;
     for (uint32_t j0 = 0; j0 < nlev;) {
-        const uint32_t gmax = j0 == 0 ? 10 : 6;
+        const uint32_t gmax = j0 == 0 ? (small ? 9 : 10) : (small ? 5 : 6);
         const uint32_t G = min(gmax, nlev - j0), H = (1u << G) - 1;
         const uint64_t rows64 = (L + ((uint64_t)1 << j0) - 1) >> j0;
         const uint32_t rows = (uint32_t)rows64;
         uint32_t logW, S;
         if (j0 == 0) {
             logW = 0;
-            S = CP_CAP - H;
+            S = CAP - H;
         } else {
             logW = 4;  // 16 residues = 128-B row segments
-            if (rows <= CP_CAP >> logW) {  // one band (no halo rows exist): widen the rows
-                S = rows;
-                while (logW < j0 && (rows << (logW + 1)) <= CP_CAP) ++logW;
+            if (rows + H <= CAP >> logW) {  // one band: widen the rows instead
+                S = rows;                        // (halo rows past L are dummies in LDS)
+                while (logW < j0 && ((rows + H) << (logW + 1)) <= CAP) ++logW;
             } else {
-                S = (CP_CAP >> logW) - H;
+                S = (CAP >> logW) - H;
             }
             if (logW > j0) logW = j0;
         }
@@ -149,10 +176,11 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
         if (grid == 0 || grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
-        auto k = fin == 0 ? compact_pass<0> : fin == 1 ? compact_pass<1> : compact_pass<2>;
-        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(CP_NT), 0, s, cur, oth, (uint32_t)L,
-                           (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out);
-        const hipError_t e = hipGetLastError();
+        const hipError_t e =
+            small ? launch_pass<4096, 256>(j0 == 0, fin, (unsigned)grid, s, cur, oth, (uint32_t)L,
+                                           (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out)
+                  : launch_pass<8192, 512>(j0 == 0, fin, (unsigned)grid, s, cur, oth, (uint32_t)L,
+                                           (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out);
         if (e != hipSuccess) return e;
         uint64_t *x = cur; cur = oth; oth = x;
         j0 += G;

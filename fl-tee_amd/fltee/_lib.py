@@ -78,6 +78,7 @@ EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_aes_block": (None, [_P, _P, _P]),
     "fltee_debug_set_dense_variant": (None, [ctypes.c_int]),
     "fltee_debug_set_advanced_compaction": (None, [ctypes.c_int]),
+    "fltee_debug_set_compact_variant": (None, [ctypes.c_int]),
 }
 
 _lib = None

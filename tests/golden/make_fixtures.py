@@ -1,13 +1,16 @@
 """Generate the committed golden fixtures from the REFERENCE's own client code.
 
 Run in the build container only (it needs /root/reference):
-    python tests/golden/make_fixtures.py
+    python tests/golden/make_fixtures.py [--wire-only]
 
 What it imports from the reference (read-only, never copied):
   src/utils.py  : zero_except_top_k_weights, serialize_sparse, serialize_dense,
                   encrypt_parameters, flatten_params, get_learnable_parameters
   src/update.py : l2clipping, diff_weights
   src/models.py : MLP (MLP-MNIST, d = 50,890)
+  src/secure_aggregation_pb2.py : the generated proto messages (wire.npz: request /
+                  response bytes as the reference's client serialises them; importable
+                  only with the pure-Python protobuf backend)
 utils.py loads 'src/libsgx_enc.so' relative to the cwd at import time.  The
 prebuilt binary shipped in the reference is NEVER loaded: we run from a scratch
 cwd whose src/libsgx_enc.so is oracle/_ref/libsgx_enc.so, compiled by
@@ -22,6 +25,10 @@ cannot run here): the aggregation arithmetic is parity-unpinned beyond the
 invariants in tests/test_oracle.py.
 """
 import os
+
+# the reference's old generated pb2 needs the pure-Python protobuf backend; the
+# backend is fixed at the first protobuf import, so set it before anything else
+os.environ.setdefault("PROTOCOL_BUFFERS_PYTHON_IMPLEMENTATION", "python")
 import shutil
 import sys
 import tempfile
@@ -68,7 +75,44 @@ def perturbed_diff(model, seed, scale=0.01):
     return OrderedDict(diff)
 
 
+def wire_fixtures():
+    """proto/secure_aggregation.proto messages serialised by the reference's pb2."""
+    sys.path.insert(0, REF_SRC)
+    import secure_aggregation_pb2 as pb
+    sp = np.load(os.path.join(OUT, "mnist_sparse.npz"))
+    ids = sp["client_ids"].astype(np.uint32)
+    d, k = int(sp["d"]), int(sp["k"])
+    upd = sp["oracle_advanced"].astype(np.float32)
+    start_req = dict(fl_id=0, client_ids=list(range(100)), sigma=1.12, clipping=1.0, alpha=0.1,
+                     sampling_ratio=0.3, aggregation_alg=1, num_of_parameters=d,
+                     num_of_sparse_parameters=k)
+    start_resp = dict(fl_id=0, round=0, client_ids=[int(x) for x in ids])
+    agg_req = dict(fl_id=0, round=0, encrypted_parameters=sp["ciphertext"].tobytes(),
+                   num_of_parameters=d, num_of_sparse_parameters=k, optimal_num_of_clients=100,
+                   aggregation_alg=1, client_ids=[int(x) for x in ids])
+    agg_resp = dict(updated_parameters=upd.tolist(), execution_time=0.125,
+                    client_ids=[int(x) for x in ids[::-1]], round=1)
+    big_ids = dict(fl_id=4294967295, round=70000, client_ids=[0, 127, 128, 16383, 16384, 4294967295])
+    out = {}
+    for name, cls, fields in [("start_req", pb.StartRequestParameters, start_req),
+                              ("start_resp", pb.StartResponseParameters, start_resp),
+                              ("agg_req", pb.AggregateRequestParameters, agg_req),
+                              ("agg_resp", pb.AggregateResponseParameters, agg_resp),
+                              ("start_resp_edge", pb.StartResponseParameters, big_ids),
+                              ("agg_req_empty", pb.AggregateRequestParameters, {})]:
+        out[name] = np.frombuffer(cls(**fields).SerializeToString(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "wire.npz"), **out, start_sigma=np.float32(1.12),
+                        start_clipping=np.float32(1.0), start_alpha=np.float32(0.1),
+                        start_ratio=np.float32(0.3), d=d, k=k, client_ids=ids, updated=upd,
+                        ciphertext=sp["ciphertext"], edge_ids=np.array(big_ids["client_ids"],
+                                                                        dtype=np.uint64))
+    print("wire", {k_: v.size for k_, v in out.items()})
+
+
 def main():
+    if "--wire-only" in sys.argv:
+        wire_fixtures()
+        return
     utils, update, models = import_reference()
     torch.manual_seed(1)
 
@@ -152,6 +196,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "ffi_test_kat.npz"), plaintext=np.frombuffer(src, np.uint8),
                         ciphertext=np.frombuffer(ct, np.uint8))
     print("ffi kat ok")
+    wire_fixtures()
 
 
 if __name__ == "__main__":
