@@ -81,6 +81,10 @@ hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint
 
 // k_bitonic.hip
 hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s);
+// stages up to log2(seg) only: aligned segments of seg records sorted, alternating
+// ascending (even segments) / descending (odd segments)
+hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
+                                 hipStream_t s);
 
 // k_fold.hip
 hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *dst,

@@ -382,9 +382,11 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
     return FLTEE_SUCCESS;
 }
 
-extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n,
-                                               const void *d_cipher, size_t bytes_per_client,
-                                               void *d_records, void *stream) {
+// AES-128-CTR over n client slices with the session keys of lib.rs:312-343 (key
+// bytes[4..8] = id BE; the client's 2-byte layout, utils.py:276-278, is the same for
+// every id it can encode).  CTR is its own inverse: decrypt == encrypt.
+static fltee_status_t aes_ctr_device(const uint32_t *client_ids, size_t n, const void *d_in,
+                                     size_t bytes_per_client, void *d_out, hipStream_t s) {
     std::lock_guard<std::recursive_mutex> lk(api_mutex());
     DeviceCtx *c = current_ctx();
     if (!c) return FLTEE_ERROR_INVALID_PARAMETER;
@@ -398,14 +400,75 @@ extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_
         key[7] = (uint8_t)client_ids[i];
         aes128_expand_key(key, &rk[i * 44]);
     }
-    hipStream_t s = (hipStream_t)stream;
     if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
-    if (launch_aes_ctr((const uint8_t *)d_cipher, n, bytes_per_client, bytes_per_client / 8,
-                       (const uint32_t *)c->round_keys.ptr, (uint8_t *)d_records, s) != hipSuccess)
+    if (launch_aes_ctr((const uint8_t *)d_in, n, bytes_per_client, bytes_per_client / 8,
+                       (const uint32_t *)c->round_keys.ptr, (uint8_t *)d_out, s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     // rk lives on this stack frame: wait for the (tiny) copy + kernel
     return hipStreamSynchronize(s) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n,
+                                               const void *d_cipher, size_t bytes_per_client,
+                                               void *d_records, void *stream) {
+    return aes_ctr_device(client_ids, n, d_cipher, bytes_per_client, d_records, (hipStream_t)stream);
+}
+
+// ------------------------------------------- client-side producers (§8f.4) ----
+extern "C" fltee_status_t fltee_encrypt_device(const uint32_t *client_ids, size_t n,
+                                               const void *d_plain, size_t bytes_per_client,
+                                               void *d_cipher, void *stream) {
+    for (size_t i = 0; i < n; ++i)  // encrypt_parameters: int(id).to_bytes(2, 'big')
+        if (client_ids[i] > 0xFFFFu) return FLTEE_ERROR_INVALID_PARAMETER;
+    return aes_ctr_device(client_ids, n, d_plain, bytes_per_client, d_cipher, (hipStream_t)stream);
+}
+
+namespace fltee {
+hipError_t launch_client_topk(const float *values, size_t n, size_t d, size_t k, uint64_t *keys,
+                              uint64_t *rec, hipStream_t s);
+size_t client_topk_workspace(size_t n, size_t d);
+hipError_t launch_client_dense(const float *values, size_t n, size_t d, uint64_t *rec,
+                               hipStream_t s);
+}  // namespace fltee
+
+extern "C" fltee_status_t fltee_client_topk_device(const float *d_values, size_t n, size_t d,
+                                                   size_t k, void *d_records, void *stream) {
+    if (n == 0 || d == 0 || k > d || d > 0xFFFFFFFFull) return FLTEE_ERROR_INVALID_PARAMETER;
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (k == 0) return FLTEE_SUCCESS;
+    if (!c->ws_client.reserve(client_topk_workspace(n, d))) return FLTEE_ERROR_OUT_OF_MEMORY;
+    return launch_client_topk(d_values, n, d, k, (uint64_t *)c->ws_client.ptr,
+                              (uint64_t *)d_records, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_client_serialize_dense_device(const float *d_values, size_t n,
+                                                              size_t d, void *d_records,
+                                                              void *stream) {
+    if (n == 0 || d == 0 || d > 0xFFFFFFFFull) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_client_dense(d_values, n, d, (uint64_t *)d_records, (hipStream_t)stream) ==
+                   hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_client_clip_device(void *d_records, size_t n, size_t k,
+                                                   float clipping, void *stream) {
+    if (n == 0) return FLTEE_ERROR_INVALID_PARAMETER;
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (!c->ws_client_coef.reserve(n * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
+    hipStream_t s = (hipStream_t)stream;
+    float *cf = (float *)c->ws_client_coef.ptr;
+    if (launch_client_clip_coef(d_records, n, k, clipping, cf, s) != hipSuccess ||
+        launch_apply_clip(d_records, n, k, cf, s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    return FLTEE_SUCCESS;
 }
 
 // CPU self-test hook: one AES-128 block with the library's tables (no GPU).

@@ -20,6 +20,7 @@ struct DeviceCtx {
     uint32_t *status = nullptr;  // library-owned device status word
     Buffer ws_a, ws_b, ws_mat, ws_r, ws_coef, ws_rec;  // aggregation scratch
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
+    Buffer ws_client, ws_client_coef;                   // client-side producers
     hipStream_t stream = nullptr;                        // ECALL stream
 };
 

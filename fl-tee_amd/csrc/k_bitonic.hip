@@ -227,11 +227,16 @@ static hipError_t launch_tiles(uint32_t E, unsigned grid, unsigned threads, size
     }
 }
 
+// Stages 1..slog of the network over m records (slog = log2 m: the full sort).  With
+// slog < log2 m every aligned segment of 2^slog records comes out sorted, ascending
+// where bit slog of its first position is 0 and descending where it is 1.
 template <int MODE>
-static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s) {
+static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s,
+                            uint32_t slog) {
     const int kMaxGlobalR = max_global_r();
     const uint32_t mlog = log2_pow2(m);
     uint32_t tlog = mlog < kMaxTileLog ? mlog : kMaxTileLog;
+    if (tlog > slog) tlog = slog;
     while (tlog > 11 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles to fill the CUs
     if (tlog < 1) tlog = 1;
     const unsigned tiles = 1u << (mlog - tlog);
@@ -246,7 +251,7 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     hipError_t e = launch_tiles<MODE, true>(E, grid, threads, lds, s, data, tlog, 0u, rmax, seed,
                                             tiles);
     if (e != hipSuccess) return e;
-    for (uint32_t ilog = tlog + 1; ilog <= mlog; ++ilog) {
+    for (uint32_t ilog = tlog + 1; ilog <= slog; ++ilog) {
         int jtop = (int)ilog - 1;
         const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
         const int passes = (nglobal + kMaxGlobalR - 1) / kMaxGlobalR;
@@ -265,10 +270,22 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
 
 hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s) {
     if (m < 2) return hipSuccess;
+    const uint32_t mlog = log2_pow2(m);
     switch (mode) {
-    case 0: return sort_impl<0>(data, m, seed, s);
-    case 1: return sort_impl<1>(data, m, seed, s);
-    default: return sort_impl<2>(data, m, seed, s);
+    case 0: return sort_impl<0>(data, m, seed, s, mlog);
+    case 1: return sort_impl<1>(data, m, seed, s, mlog);
+    default: return sort_impl<2>(data, m, seed, s, mlog);
+    }
+}
+
+hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
+                                 hipStream_t s) {
+    if (m < 2 || seg < 2) return hipSuccess;
+    const uint32_t slog = log2_pow2(seg);
+    switch (mode) {
+    case 0: return sort_impl<0>(data, m, 0, s, slog);
+    case 1: return sort_impl<1>(data, m, 0, s, slog);
+    default: return sort_impl<2>(data, m, 0, s, slog);
     }
 }
 

@@ -71,6 +71,10 @@ SIGNATURES = {
     "fltee_bitonic_device": (_U32, [_P, _S, _U32, _U32, _P]),
     "fltee_fold_device": (_U32, [_P, _P, _S, _S, _S, _P, _P]),
     "fltee_laplace_r_device": (_U32, [_S, _S, _S, _U64, _P, _P, _P]),
+    "fltee_client_topk_device": (_U32, [_P, _S, _S, _S, _P, _P]),
+    "fltee_client_serialize_dense_device": (_U32, [_P, _S, _S, _P, _P]),
+    "fltee_client_clip_device": (_U32, [_P, _S, _S, _F, _P]),
+    "fltee_encrypt_device": (_U32, [_P, _S, _P, _S, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_version": (ctypes.c_char_p, []),
 }

@@ -167,6 +167,26 @@ fltee_status_t fltee_reserve(uint32_t alg, size_t n, size_t k, size_t d,
 fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n, const void *d_cipher,
                                     size_t bytes_per_client, void *d_records, void *stream);
 
+/* ---- client-side producers (fl_main.py:221-238) -------
+ * For a GPU-resident client simulator: n clients' flattened updates d_values
+ * [n][d] (f32) -> the encrypted payload of the Aggregate request, in HBM. */
+/* utils.py:327-354 zero_except_top_k_weights + utils.py:193-209 serialize_sparse:
+ * per client the k records (idx, val) of largest |val|, in the reference's order
+ * (|val| descending, equal magnitudes by ascending idx; Python's stable sort). */
+fltee_status_t fltee_client_topk_device(const float *d_values, size_t n, size_t d, size_t k,
+                                        void *d_records, void *stream);
+/* utils.py:171-190 serialize_dense: records (i, v[i]), i < d, per client. */
+fltee_status_t fltee_client_serialize_dense_device(const float *d_values, size_t n, size_t d,
+                                                   void *d_records, void *stream);
+/* update.py:187-204 l2clipping on serialized records (n clients x k records, in
+ * place): val *= min(1, clipping / ||client's values||_2). */
+fltee_status_t fltee_client_clip_device(void *d_records, size_t n, size_t k, float clipping,
+                                        void *stream);
+/* utils.py:268-290 encrypt_parameters for n clients (ids < 65536: the client's
+ * 2-byte key layout), bytes_per_client each; the inverse of fltee_decrypt_device. */
+fltee_status_t fltee_encrypt_device(const uint32_t *client_ids, size_t n, const void *d_plain,
+                                    size_t bytes_per_client, void *d_cipher, void *stream);
+
 /* out[j] = coef * sum_r rows[r*d + j], rows added in order (exact fp32): the
  * root-side combine of per-GPU partial sums, in the batch order of alg 6
  * (lib.rs:564-573: global[i] += batch_sum[i], then average). */

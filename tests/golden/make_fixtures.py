@@ -1,7 +1,7 @@
 """Generate the committed golden fixtures from the REFERENCE's own client code.
 
 Run in the build container only (it needs /root/reference):
-    python tests/golden/make_fixtures.py [--wire-only]
+    python tests/golden/make_fixtures.py [--wire-only | --client-only]
 
 What it imports from the reference (read-only, never copied):
   src/utils.py  : zero_except_top_k_weights, serialize_sparse, serialize_dense,
@@ -109,11 +109,59 @@ def wire_fixtures():
     print("wire", {k_: v.size for k_, v in out.items()})
 
 
+def client_fixtures(utils, update, models):
+    """The client producers of fl_main.py:221-238 run by the reference's own functions
+    on explicit flat updates (stored, so the GPU test needs no reference import).
+    Clients 2 and 3 are quantised to multiples of 1e-3: heavy |val| ties exercise the
+    stable-sort tie order of zero_except_top_k_weights."""
+    from collections import OrderedDict
+    model = models.MLP(dim_in=784, dim_hidden=64, dim_out=10)
+    bn = utils.get_buffer_names(model)
+    d = utils.count_parameters(model)
+    k = int(0.1 * d)
+    ids = np.array([5, 77, 1234, 65535], dtype=np.uint32)
+    g = torch.Generator().manual_seed(4242)
+    flats = torch.randn(len(ids), d, generator=g) * 0.01
+    flats[2:] = torch.round(flats[2:] * 1000) / 1000
+    flats[3, :50] = 0.0
+    flats[3, 50:60] = -0.0
+
+    def as_state(flat):
+        st, off = OrderedDict(), 0
+        for key, val in model.state_dict().items():
+            st[key] = flat[off:off + val.numel()].reshape(val.shape).clone()
+            off += val.numel()
+        return st
+
+    topk, plain, plain_clip, cipher, dense_plain, dense_clip = [], [], [], [], [], []
+    for cid, flat in zip(ids, flats):
+        st = as_state(flat)
+        top, idxs = utils.zero_except_top_k_weights(st, bn, k)
+        topk.append(np.asarray(idxs, np.uint32))
+        b = utils.serialize_sparse(top, bn, idxs)
+        plain.append(np.frombuffer(b, np.uint8))
+        cipher.append(np.frombuffer(bytes(utils.encrypt_parameters(b, int(cid))), np.uint8))
+        bc = utils.serialize_sparse(update.l2clipping(top, bn, 1.0), bn, idxs)
+        plain_clip.append(np.frombuffer(bc, np.uint8))
+        dense_plain.append(np.frombuffer(utils.serialize_dense(st, bn, d), np.uint8))
+        dense_clip.append(np.frombuffer(utils.serialize_dense(update.l2clipping(st, bn, 0.05), bn, d),
+                                        np.uint8))
+    np.savez_compressed(os.path.join(OUT, "client_producer.npz"), client_ids=ids,
+                        flats=flats.numpy().astype(np.float32), d=d, k=k, topk=np.stack(topk),
+                        plain=np.concatenate(plain), plain_clip=np.concatenate(plain_clip),
+                        cipher=np.concatenate(cipher), dense_plain=np.concatenate(dense_plain),
+                        dense_clip=np.concatenate(dense_clip), clipping=1.0, dense_clipping=0.05)
+    print("client_producer d", d, "k", k)
+
+
 def main():
     if "--wire-only" in sys.argv:
         wire_fixtures()
         return
     utils, update, models = import_reference()
+    if "--client-only" in sys.argv:
+        client_fixtures(utils, update, models)
+        return
     torch.manual_seed(1)
 
     # ---------------- MLP-MNIST sparse (alpha = 0.1), fl_main.py:221-238 ----------
@@ -196,6 +244,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "ffi_test_kat.npz"), plaintext=np.frombuffer(src, np.uint8),
                         ciphertext=np.frombuffer(ct, np.uint8))
     print("ffi kat ok")
+    client_fixtures(utils, update, models)
     wire_fixtures()
 
 

@@ -1,0 +1,106 @@
+"""GPU: the client-side producers (fltee.client / k_client.hip) against the reference's
+own client functions (tests/golden/client_producer.npz, made by utils.py /
+update.py in tests/golden/make_fixtures.py) and a GPU-resident round.
+
+Bar: top-k order, serialisation and encryption bit-exact; l2clipping within 1e-6
+relative (the reference's coefficient comes from torch's fp32 norm, ours from an f64
+sum of squares: they can differ in the last bit).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return np.load(os.path.join(GOLDEN, "client_producer.npz"))
+
+
+@pytest.fixture(scope="module")
+def C():
+    import torch
+    torch.cuda.init()
+    from fltee import client
+    return client
+
+
+def _cuda(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _bytes(t):
+    return t.cpu().numpy().view(np.uint8).ravel()
+
+
+def test_topk_serialize_matches_reference(C, fx):
+    rec = C.zero_except_top_k_weights(_cuda(fx["flats"]), int(fx["k"]))
+    assert np.array_equal(_bytes(rec), fx["plain"])
+
+
+def test_l2clipping_matches_reference(C, fx):
+    n, k = len(fx["client_ids"]), int(fx["k"])
+    rec = C.zero_except_top_k_weights(_cuda(fx["flats"]), k)
+    C.l2clipping(rec, n, k, float(fx["clipping"]))
+    got = _bytes(rec).reshape(-1, 8)
+    ref = fx["plain_clip"].reshape(-1, 8)
+    assert np.array_equal(got[:, :4], ref[:, :4])
+    gv, rv = got[:, 4:].copy().view("<f4").ravel(), ref[:, 4:].copy().view("<f4").ravel()
+    np.testing.assert_allclose(gv, rv, rtol=1e-6, atol=0)
+
+
+def test_dense_serialize_and_clip_match_reference(C, fx):
+    n, d = fx["flats"].shape
+    rec = C.serialize_dense(_cuda(fx["flats"]))
+    assert np.array_equal(_bytes(rec), fx["dense_plain"])
+    C.l2clipping(rec, n, d, float(fx["dense_clipping"]))
+    got = _bytes(rec).reshape(-1, 8)
+    ref = fx["dense_clip"].reshape(-1, 8)
+    assert np.array_equal(got[:, :4], ref[:, :4])
+    np.testing.assert_allclose(got[:, 4:].copy().view("<f4").ravel(),
+                               ref[:, 4:].copy().view("<f4").ravel(), rtol=1e-6, atol=0)
+
+
+def test_encrypt_matches_reference_client(C, fx):
+    enc = C.encrypt_parameters(_cuda(fx["plain"].view(np.int64)), fx["client_ids"])
+    assert np.array_equal(_bytes(enc), fx["cipher"])
+    pay = C.produce_payloads(_cuda(fx["flats"]), fx["client_ids"], k=int(fx["k"]))
+    assert np.array_equal(_bytes(pay), fx["cipher"])
+
+
+def test_gpu_resident_round_matches_oracle(C, fx, oracle):
+    """producers -> ciphertext in HBM -> decrypt -> advanced, no host round trip."""
+    import torch
+
+    from fltee import device as D
+    ids, k = fx["client_ids"], int(fx["k"])
+    n, d = fx["flats"].shape
+    pay = C.produce_payloads(_cuda(fx["flats"]), ids, k=k)
+    rec = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    D.decrypt(ids, pay, k * 8, rec)
+    out = D.aggregate(1, rec, n, k, d).cpu().numpy()
+    w = oracle.decrypt_and_parse(ids, fx["cipher"])
+    ref, st = oracle.advanced(k, w, d, n)
+    assert st == 0 and np.array_equal(out.view(np.uint32), np.asarray(ref).view(np.uint32))
+
+
+@pytest.mark.parametrize("n,d,k", [(8, 1_000_000, 10_000), (3, 7, 7), (5, 1, 1), (2, 300, 0)])
+def test_topk_large_and_edge_shapes(C, n, d, k):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(n * d + k)
+    v = torch.randn(n, d, generator=g, device="cuda") * 0.01
+    v = torch.round(v * 4096) / 4096  # ties
+    rec = C.zero_except_top_k_weights(v, k).cpu().numpy().view(np.uint32).reshape(n, k, 2)
+    vh = v.cpu().numpy()
+    for c in range(n):
+        a = (vh[c].view(np.uint32) & np.uint32(0x7FFFFFFF)).astype(np.uint64)
+        key = ((np.uint64(0x7FFFFFFF) - a) << np.uint64(32)) | np.arange(d, dtype=np.uint64)
+        order = np.argsort(key, kind="stable")[:k].astype(np.uint32)
+        assert np.array_equal(rec[c, :, 0], order)
+        assert np.array_equal(rec[c, :, 1], vh[c][order].view(np.uint32))
