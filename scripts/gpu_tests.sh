@@ -1,0 +1,4 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu${TAG:-x}.log 2>&1; rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu${TAG:-x}.log; exit $rc

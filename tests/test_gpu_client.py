@@ -2,9 +2,9 @@
 own client functions (tests/golden/client_producer.npz, made by utils.py /
 update.py in tests/golden/make_fixtures.py) and a GPU-resident round.
 
-Bar: top-k order, serialisation and encryption bit-exact; l2clipping within 1e-6
-relative (the reference's coefficient comes from torch's fp32 norm, ours from an f64
-sum of squares: they can differ in the last bit).
+Bar: top-k order, serialisation and encryption bit-exact; l2clipping within 1 ulp of
+torch's arithmetic with an exactly rounded norm, and within 2e-6 relative of the
+reference (torch.norm's fp32 accumulation is off by up to ~1e-6 at d = 5e4).
 """
 import os
 
@@ -39,6 +39,24 @@ def _bytes(t):
     return t.cpu().numpy().view(np.uint8).ravel()
 
 
+def _vals(b):
+    return b.reshape(-1, 8)[:, 4:].copy().view("<f4").ravel()
+
+
+def _clip_model(vals, n, clipping):
+    """update.py:187-204 with an exactly rounded norm: norm32 = f32(sqrt(sum v^2)) (f64
+    sum), coef = min(1, f32(C / norm32)), v * coef in f32 — torch's arithmetic, minus
+    the fp32 accumulation error of torch.norm (relative ~sqrt(d) * 2^-24: ~1e-6 at
+    d = 5e4), which is why the reference itself is compared within 2e-6."""
+    out = []
+    for v in vals.reshape(n, -1):
+        norm32 = np.float32(np.sqrt(np.sum(v.astype(np.float64) ** 2)))
+        cf = np.float32(np.float32(clipping) / norm32)
+        cf = cf if cf < 1 else np.float32(1)
+        out.append((v * cf).astype(np.float32))
+    return np.concatenate(out)
+
+
 def test_topk_serialize_matches_reference(C, fx):
     rec = C.zero_except_top_k_weights(_cuda(fx["flats"]), int(fx["k"]))
     assert np.array_equal(_bytes(rec), fx["plain"])
@@ -48,11 +66,12 @@ def test_l2clipping_matches_reference(C, fx):
     n, k = len(fx["client_ids"]), int(fx["k"])
     rec = C.zero_except_top_k_weights(_cuda(fx["flats"]), k)
     C.l2clipping(rec, n, k, float(fx["clipping"]))
-    got = _bytes(rec).reshape(-1, 8)
-    ref = fx["plain_clip"].reshape(-1, 8)
+    got, ref = _bytes(rec).reshape(-1, 8), fx["plain_clip"].reshape(-1, 8)
     assert np.array_equal(got[:, :4], ref[:, :4])
-    gv, rv = got[:, 4:].copy().view("<f4").ravel(), ref[:, 4:].copy().view("<f4").ravel()
-    np.testing.assert_allclose(gv, rv, rtol=1e-6, atol=0)
+    model = _clip_model(_vals(fx["plain"]), n, float(fx["clipping"]))
+    assert np.abs(_vals(got).view(np.int32).astype(np.int64)
+                  - model.view(np.int32).astype(np.int64)).max() <= 1
+    np.testing.assert_allclose(_vals(got), _vals(ref), rtol=2e-6, atol=0)
 
 
 def test_dense_serialize_and_clip_match_reference(C, fx):
@@ -60,11 +79,12 @@ def test_dense_serialize_and_clip_match_reference(C, fx):
     rec = C.serialize_dense(_cuda(fx["flats"]))
     assert np.array_equal(_bytes(rec), fx["dense_plain"])
     C.l2clipping(rec, n, d, float(fx["dense_clipping"]))
-    got = _bytes(rec).reshape(-1, 8)
-    ref = fx["dense_clip"].reshape(-1, 8)
+    got, ref = _bytes(rec).reshape(-1, 8), fx["dense_clip"].reshape(-1, 8)
     assert np.array_equal(got[:, :4], ref[:, :4])
-    np.testing.assert_allclose(got[:, 4:].copy().view("<f4").ravel(),
-                               ref[:, 4:].copy().view("<f4").ravel(), rtol=1e-6, atol=0)
+    model = _clip_model(fx["flats"].ravel(), n, float(fx["dense_clipping"]))
+    assert np.abs(_vals(got).view(np.int32).astype(np.int64)
+                  - model.view(np.int32).astype(np.int64)).max() <= 1
+    np.testing.assert_allclose(_vals(got), _vals(ref), rtol=2e-6, atol=0)
 
 
 def test_encrypt_matches_reference_client(C, fx):
