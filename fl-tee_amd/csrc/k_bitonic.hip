@@ -71,81 +71,115 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 // ------------------------------------------------------------- LDS tile ----
 __device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
 
-// One LDS round: steps jtop..jtop-R+1 of stage ilog over the whole tile of
-// T = E * nt records.  Lane t handles the G = E >> R groups t + h*nt (R <= log2 E,
-// so every lane is busy).  nt is passed in, never read from blockDim inside the
-// rounds: hipcc reloads it with a vector load + vmcnt(0), which would drain the
-// tile prefetch in flight.
-template <int MODE, int R, int E>
-__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t nt, uint32_t base,
-                                          uint32_t ilog, uint32_t jtop, uint32_t seed) {
+// Tile maps.  A tile is T = 2^tlog records: W = 2^wlog consecutive positions times
+// T/W rows at stride 2^dtile (wlog <= dtile).  Contiguous tiles: wlog = dtile = tlog.
+// Tile t fixes the position bits outside the tile: bits [wlog, dtile) from t's low
+// bits, bits >= dtile + (tlog - wlog) from the rest.
+__device__ __forceinline__ uint32_t tile_base(uint32_t t, uint32_t tlog, uint32_t wlog,
+                                              uint32_t dtile) {
+    const uint32_t mid = dtile - wlog;
+    return ((t >> mid) << (dtile + tlog - wlog)) | ((t & ((1u << mid) - 1u)) << wlog);
+}
+__device__ __forceinline__ uint32_t tile_pos(uint32_t base, uint32_t e, uint32_t wlog,
+                                             uint32_t dtile) {
+    return base + (e & ((1u << wlog) - 1u)) + ((e >> wlog) << dtile);
+}
+
+// One LDS round: steps at tile-local bits jtop..jtop-R+1 of stage ilog over the whole
+// tile of T = E * NT records.  Lane t handles the G = E >> R groups t + h*NT (R <=
+// log2 E, so every lane is busy).  A round never straddles bit wlog, so the group's
+// global distance is 2^dlog_g and its first record sits at tile_pos(b).
+template <int MODE, int R, int E, int NT>
+__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t wlog,
+                                          uint32_t dtile, uint32_t ilog, uint32_t jtop,
+                                          uint32_t seed) {
     constexpr int G = E >> R;
     const uint32_t dlog = jtop - R + 1;
+    const uint32_t dlog_g = dlog >= wlog ? dlog - wlog + dtile : dlog;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
-        const uint32_t g = threadIdx.x + (uint32_t)h * nt;
+        const uint32_t g = threadIdx.x + (uint32_t)h * NT;
         const uint32_t b = spread(g, dlog, R);
         uint64_t v[1 << R];
 #pragma unroll
         for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << dlog))];
-        group_steps<MODE, R>(v, base + b, dlog, ilog, seed);
+        group_steps<MODE, R>(v, tile_pos(base, b, wlog, dtile), dlog_g, ilog, seed);
 #pragma unroll
         for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << dlog))] = v[q];
     }
 }
 
-template <int MODE, int E>
-__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t nt, uint32_t base, uint32_t ilog,
-                                          int jtop, uint32_t seed) {
+// tile-local steps jtop..jbot of stage ilog, up to log2(E) per barrier
+template <int MODE, int E, int NT>
+__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t wlog,
+                                          uint32_t dtile, uint32_t ilog, int jtop, int jbot,
+                                          uint32_t seed) {
     constexpr int rmax = E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1));
-    while (jtop >= 0) {
-        const int r = jtop + 1 < rmax ? jtop + 1 : rmax;
-        if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
-        else lds_round<MODE, 1, E>(sm, nt, base, ilog, (uint32_t)jtop, seed);
+    while (jtop >= jbot) {
+        const int left = jtop - jbot + 1;
+        const int r = left < rmax ? left : rmax;
+        if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else lds_round<MODE, 1, E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         __syncthreads();
         jtop -= r;
     }
 }
 
 // Persistent tile kernels: a block walks tiles blockIdx.x, +gridDim.x, ...; the
-// next tile's records are prefetched into registers (E <= 16 per lane, coalesced)
-// while the current tile runs its LDS rounds, so HBM and LDS work overlap
-// (T14-style issue-early / write-late staging).
-//   SORT  : all stages 2..T of each tile (first launch of a sort)
-//   !SORT : the steps j < T of stage ilog (merge after the global passes)
-// E = records per lane (T = E * blockDim) is a template parameter: a runtime
-// guard around each prefetch load makes hipcc branch and wait vmcnt(0) per load
-// (cdna_hip_programming.md §5 trap 4c), which serialises the prefetch.
-template <int MODE, bool SORT, int E>
-__global__ __launch_bounds__(512) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
-                                                     uint32_t ilog, uint32_t nt, uint32_t seed,
-                                                     uint32_t ntiles) {
+// next tile's records are prefetched into registers (E per lane) while the current
+// tile runs its LDS rounds, so HBM and LDS work overlap (T14-style issue-early /
+// write-late staging).
+//   SORT  : all stages 2..T of each contiguous tile (first launch of a sort)
+//   !SORT : contiguous (wlog == tlog): the steps j < T of stage ilog (merge);
+//           strided: the global steps dtile + tlog-wlog-1 .. dtile of stage ilog.
+// E (records per lane) and NT (lanes) are template parameters: a runtime guard
+// around each prefetch load makes hipcc branch and wait vmcnt(0) per load
+// (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
+// vector load + vmcnt(0) that drains the prefetch.
+template <int MODE, bool SORT, int E, int NT>
+__global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
+                                                    uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                                    uint32_t seed, uint32_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
+    // record r of this lane is tile element threadIdx.x + r*NT at position
+    // base + p_off + r*rstride (W <= NT for strided tiles, W = T for contiguous ones)
+    const uint32_t p_off = tile_pos(0u, threadIdx.x, wlog, dtile);
+    const uint32_t rstride = (uint32_t)NT << (dtile - wlog);
     uint64_t pf[E];
+    {
+        const uint64_t *src = data + tile_base(tile, tlog, wlog, dtile) + p_off;
 #pragma unroll
-    for (int r = 0; r < E; ++r) pf[r] = data[((size_t)tile << tlog) + threadIdx.x + r * nt];
+        for (int r = 0; r < E; ++r) pf[r] = src[(size_t)r * rstride];
+    }
     for (;;) {
-        const uint32_t base = tile << tlog;
+        const uint32_t base = tile_base(tile, tlog, wlog, dtile);
 #pragma unroll
-        for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * nt)] = pf[r];
+        for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
-        const uint32_t pft = next < ntiles ? next : tile;
+        {
+            const uint64_t *src =
+                data + tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) + p_off;
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = data[((size_t)pft << tlog) + threadIdx.x + r * nt];
+            for (int r = 0; r < E; ++r) pf[r] = src[(size_t)r * rstride];
+        }
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE, E>(sm, nt, base, il, (int)il - 1, seed);
+                lds_steps<MODE, E, NT>(sm, base, wlog, dtile, il, (int)il - 1, 0, seed);
         } else {
-            lds_steps<MODE, E>(sm, nt, base, ilog, (int)tlog - 1, seed);
+            lds_steps<MODE, E, NT>(sm, base, wlog, dtile, ilog, (int)tlog - 1,
+                                   wlog < tlog ? (int)wlog : 0, seed);
         }
+        {
+            uint64_t *dst = data + base + p_off;
 #pragma unroll
-        for (int r = 0; r < E; ++r) data[(size_t)base + threadIdx.x + r * nt] = sm[lpad(threadIdx.x + r * nt)];
+            for (int r = 0; r < E; ++r) dst[(size_t)r * rstride] = sm[lpad(threadIdx.x + r * NT)];
+        }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
         tile = next;
@@ -186,10 +220,10 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
     return hipGetLastError();
 }
 
-constexpr uint32_t kMaxTileLog = 13;  // 8192 records = 64 KB (+1/16 padding) of LDS
+constexpr uint32_t kMaxTileLog = 14;  // 16384 records = 128 KB (+1/16 padding) of LDS
 
-// Steps per global pass: 6 (64 records/lane; measured fastest at M = 2^24, 2^27); the
-// FLTEE_BITONIC_MAXR knob (1..6) exists for tuning runs only.
+// Steps per register-blocked global pass: 6 (64 records/lane; measured fastest at
+// M = 2^24, 2^27); the FLTEE_BITONIC_MAXR knob (1..6) exists for tuning runs only.
 static int max_global_r() {
     static int r = [] {
         const char *e = getenv("FLTEE_BITONIC_MAXR");
@@ -198,33 +232,53 @@ static int max_global_r() {
     }();
     return r;
 }
+// Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
+// disables them, for A/B runs).
+static bool strided_passes() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_STRIDED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
-template <int MODE, bool SORT, int E>
-static hipError_t launch_tiles_e(unsigned grid, unsigned threads, size_t lds, hipStream_t s,
-                                 uint64_t *data, uint32_t tlog, uint32_t ilog, int rmax,
+template <int MODE, bool SORT, int E, int NT>
+static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                 uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    (void)rmax;  // implied by E
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E>), dim3(grid), dim3(threads), lds, s, data,
-                       tlog, ilog, (uint32_t)threads, seed, tiles);
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
+                       tlog, ilog, wlog, dtile, seed, tiles);
     return hipGetLastError();
 }
 
+struct TileCfg {
+    uint32_t tlog, E, NT;
+    unsigned tiles, grid;
+    size_t lds;
+};
+
 template <int MODE, bool SORT>
-static hipError_t launch_tiles(uint32_t E, unsigned grid, unsigned threads, size_t lds,
-                               hipStream_t s, uint64_t *data, uint32_t tlog, uint32_t ilog,
-                               int rmax, uint32_t seed, uint32_t tiles) {
-    switch (E) {
-    case 2: return launch_tiles_e<MODE, SORT, 2>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
-    case 4: return launch_tiles_e<MODE, SORT, 4>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
-    case 8: return launch_tiles_e<MODE, SORT, 8>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
-    default: return launch_tiles_e<MODE, SORT, 16>(grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
+                               uint32_t wlog, uint32_t dtile, uint32_t seed) {
+#define BT_GO(E_, NT_) \
+    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles)
+    if (c.NT == 1024) BT_GO(16, 1024);
+    if (c.NT == 256) BT_GO(2, 256);
+    if (c.NT == 128) BT_GO(2, 128);
+    if (c.NT == 64) BT_GO(2, 64);
+    switch (c.E) {
+    case 2: BT_GO(2, 512);
+    case 4: BT_GO(4, 512);
+    case 8: BT_GO(8, 512);
+    default: BT_GO(16, 512);
     }
+#undef BT_GO
 }
 
 // Stages 1..slog of the network over m records (slog = log2 m: the full sort).  With
@@ -235,34 +289,59 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
                             uint32_t slog) {
     const int kMaxGlobalR = max_global_r();
     const uint32_t mlog = log2_pow2(m);
+    TileCfg c;
+    // 2^14-record tiles (1024 lanes x 16) when there are enough of them to fill the
+    // CUs; else up to 2^13 with 512 lanes; small sorts use E = 2 and T/2 lanes
     uint32_t tlog = mlog < kMaxTileLog ? mlog : kMaxTileLog;
     if (tlog > slog) tlog = slog;
-    while (tlog > 11 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles to fill the CUs
-    if (tlog < 1) tlog = 1;
-    const unsigned tiles = 1u << (mlog - tlog);
+    if (tlog == 14 && mlog - tlog < 8) tlog = 13;
+    while (tlog > 11 && tlog <= 13 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles
+    hipError_t e;
+    if (tlog <= 6) {  // tiles of <= 64 records: every stage is one register pass
+        for (uint32_t ilog = 1; ilog <= slog; ++ilog) {
+            e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    c.tlog = tlog;
     const uint32_t T = 1u << tlog;
-    // records per lane E = T/512 clamped to [2, 16]: 512 lanes per tile whenever T >= 1024
-    const uint32_t E = T / 512 < 2 ? 2 : (T / 512 > 16 ? 16 : T / 512);
-    const unsigned threads = T / E ? T / E : 1;
-    const int rmax = (int)log2_pow2(E);
-    const size_t lds = (size_t)(T + T / 16 + 1) * 8;
-    // persistent: two resident tiles per CU, each prefetching its next tile
-    const unsigned grid = tiles < 512 ? tiles : 512;
-    hipError_t e = launch_tiles<MODE, true>(E, grid, threads, lds, s, data, tlog, 0u, rmax, seed,
-                                            tiles);
+    if (tlog == 14) {
+        c.E = 16;
+        c.NT = 1024;
+    } else if (T >= 1024) {
+        c.E = T / 512 > 16 ? 16 : T / 512;  // 512 lanes
+        c.NT = 512;
+    } else {
+        c.E = 2;
+        c.NT = T / 2;  // 64, 128 or 256 lanes
+    }
+    c.tiles = 1u << (mlog - tlog);
+    c.lds = (size_t)(T + T / 16 + 1) * 8;
+    // persistent: one (2^14) or two resident tiles per CU, each prefetching its next tile
+    const unsigned resident = tlog == 14 ? 256 : 512;
+    c.grid = c.tiles < resident ? c.tiles : resident;
+    e = launch_tiles<MODE, true>(c, s, data, 0u, tlog, tlog, seed);
     if (e != hipSuccess) return e;
+    const int rs = (int)tlog - 4;  // global steps per strided LDS pass (W >= 16)
     for (uint32_t ilog = tlog + 1; ilog <= slog; ++ilog) {
         int jtop = (int)ilog - 1;
         const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
-        const int passes = (nglobal + kMaxGlobalR - 1) / kMaxGlobalR;
+        const int per = (strided_passes() && rs > kMaxGlobalR) ? rs : kMaxGlobalR;
+        const int passes = (nglobal + per - 1) / per;
         for (int p = 0; p < passes; ++p) {
             const int left = jtop - (int)tlog + 1;
             const int R = (left + (passes - p) - 1) / (passes - p);  // balanced split
-            e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s);
+            if (R > kMaxGlobalR && (T >> R) <= c.NT) {  // strided LDS tile: W = T / 2^R consecutive x 2^R rows
+                const uint32_t dtile = (uint32_t)(jtop - R + 1);
+                e = launch_tiles<MODE, false>(c, s, data, ilog, tlog - (uint32_t)R, dtile, seed);
+            } else {
+                e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s);
+            }
             if (e != hipSuccess) return e;
             jtop -= R;
         }
-        e = launch_tiles<MODE, false>(E, grid, threads, lds, s, data, tlog, ilog, rmax, seed, tiles);
+        e = launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -96,7 +96,8 @@ def test_non_oblivious_index_out_of_range(dev):
 
 
 # ---------------------------------------------------------- bitonic ---------
-@pytest.mark.parametrize("m", [2, 4, 64, 1024, 8192, 1 << 15, 1 << 18])
+# 2^18: 2^11 tiles + one strided LDS pass; 2^22: 2^14 tiles + strided passes
+@pytest.mark.parametrize("m", [2, 4, 64, 128, 1024, 8192, 1 << 15, 1 << 18, 1 << 22])
 def test_bitonic_idx_network_bit_exact(dev, oracle, m):
     import torch
     rng = np.random.default_rng(m)
@@ -110,7 +111,7 @@ def test_bitonic_idx_network_bit_exact(dev, oracle, m):
     assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
 
 
-@pytest.mark.parametrize("m", [2, 256, 8192, 1 << 16])
+@pytest.mark.parametrize("m", [2, 256, 8192, 1 << 16, 1 << 22])
 def test_keyed_shuffle_bit_exact(dev, oracle, m):
     import torch
     rng = np.random.default_rng(m + 1)
