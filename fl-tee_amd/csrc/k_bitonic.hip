@@ -109,7 +109,9 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t 
     }
 }
 
-// tile-local steps jtop..jbot of stage ilog, up to log2(E) per barrier
+// tile-local steps jtop..jbot of stage ilog, up to log2(E) per barrier.  (Tried:
+// wave-local rounds without block barriers for steps inside 64*E-record chunks —
+// slower on MI355X: +40 us per merge pass from the extra register pressure.)
 template <int MODE, int E, int NT>
 __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, int jtop, int jbot,
@@ -188,6 +190,15 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 
 // --------------------------------------------------------- global pass -----
 // Steps jtop..jtop-R+1 of stage ilog straight from HBM: lane t owns group t.
+// Record q of a group sits at byte (q << dlog) * 8 + b * 8: a wave-uniform part and
+// a per-lane part, issued as raw buffer loads/stores with the first in soffset (an
+// SGPR) and the second in voffset (one VGPR).  With plain pointers hipcc folds the
+// uniform part into 64 per-record 64-bit addresses that stay live across the
+// compare-exchanges (R = 6: ~290 VGPRs, one wave per SIMD).  Byte offsets are 32-bit:
+// M <= 2^29 (checked by the callers).
+typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kBufNT = 2;  // cache policy: nontemporal (streaming, each byte used once)
+
 template <int MODE, int R>
 __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
                                                       uint32_t jtop, uint32_t seed,
@@ -196,12 +207,21 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
     if (t >= ngroups) return;
     const uint32_t dlog = jtop - R + 1;
     const uint32_t b = spread(t, dlog, R);
+    const int voff = (int)(b * 8u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(data, (short)0, (int)0xFFFFFFFF, 0x00020000);
     uint64_t v[1 << R];
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) v[q] = __builtin_nontemporal_load(data + b + ((uint32_t)q << dlog));
+    for (int q = 0; q < (1 << R); ++q) {
+        const bt_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (int)((uint32_t)q << (dlog + 3)), kBufNT);
+        v[q] = ((uint64_t)x.y << 32) | x.x;
+    }
     group_steps<MODE, R>(v, b, dlog, ilog, seed);
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) __builtin_nontemporal_store(v[q], data + b + ((uint32_t)q << dlog));
+    for (int q = 0; q < (1 << R); ++q) {
+        const bt_u32x2 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, voff, (int)((uint32_t)q << (dlog + 3)), kBufNT);
+    }
 }
 
 template <int MODE>
@@ -231,6 +251,15 @@ static int max_global_r() {
         return v < 1 ? 1 : (v > 6 ? 6 : v);
     }();
     return r;
+}
+// Largest LDS tile, log2 (13 or 14; FLTEE_BITONIC_TLOG, for A/B runs).
+static uint32_t max_tile_log() {
+    static uint32_t t = [] {
+        const char *e = getenv("FLTEE_BITONIC_TLOG");
+        int v = e ? atoi(e) : (int)kMaxTileLog;
+        return (uint32_t)(v < 11 ? 11 : (v > 14 ? 14 : v));
+    }();
+    return t;
 }
 // Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
 // disables them, for A/B runs).
@@ -292,7 +321,8 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     TileCfg c;
     // 2^14-record tiles (1024 lanes x 16) when there are enough of them to fill the
     // CUs; else up to 2^13 with 512 lanes; small sorts use E = 2 and T/2 lanes
-    uint32_t tlog = mlog < kMaxTileLog ? mlog : kMaxTileLog;
+    const uint32_t tmax = max_tile_log();
+    uint32_t tlog = mlog < tmax ? mlog : tmax;
     if (tlog > slog) tlog = slog;
     if (tlog == 14 && mlog - tlog < 8) tlog = 13;
     while (tlog > 11 && tlog <= 13 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles
@@ -349,6 +379,7 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
 
 hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s) {
     if (m < 2) return hipSuccess;
+    if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets (4 GiB)
     const uint32_t mlog = log2_pow2(m);
     switch (mode) {
     case 0: return sort_impl<0>(data, m, seed, s, mlog);
@@ -360,6 +391,7 @@ hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, 
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
                                  hipStream_t s) {
     if (m < 2 || seg < 2) return hipSuccess;
+    if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
     const uint32_t slog = log2_pow2(seg);
     switch (mode) {
     case 0: return sort_impl<0>(data, m, 0, s, slog);
