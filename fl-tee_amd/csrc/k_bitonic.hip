@@ -68,6 +68,30 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
     }
 }
 
+// Raw buffer access: byte offset = soffset (wave-uniform, SGPR) + voffset (per lane).
+typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kBufNT = 2;  // cache policy: nontemporal (streaming, each byte used once)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bt_rsrc(uint64_t *data) {
+    return __builtin_amdgcn_make_buffer_rsrc(data, (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+template <int CP = kBufNT>
+__device__ __forceinline__ uint64_t bt_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+    const bt_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, CP);
+    return ((uint64_t)x.y << 32) | x.x;
+}
+template <int CP = kBufNT>
+__device__ __forceinline__ void bt_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff,
+                                         uint64_t v) {
+    const bt_u32x2 x = {(uint32_t)v, (uint32_t)(v >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b64(x, rs, (int)voff, (int)soff, CP);
+}
+// tile kernels: default cache policy (nontemporal measured slower there: 504 vs 469 us).
+// Where a 2^14-tile merge pass goes at M = 2^27 (MI355X, rocprofv3): 468 us in all;
+// 390 us with the LDS rounds skipped (load -> LDS -> store only), 340 us with the
+// global stores skipped; a register-only pass (bitonic_global R=1) streams at 321 us.
+constexpr int kTileCP = 0;
+
 // ------------------------------------------------------------- LDS tile ----
 __device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
 
@@ -149,13 +173,14 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     if (tile >= ntiles) return;
     // record r of this lane is tile element threadIdx.x + r*NT at position
     // base + p_off + r*rstride (W <= NT for strided tiles, W = T for contiguous ones)
-    const uint32_t p_off = tile_pos(0u, threadIdx.x, wlog, dtile);
-    const uint32_t rstride = (uint32_t)NT << (dtile - wlog);
+    const uint32_t voff = tile_pos(0u, threadIdx.x, wlog, dtile) * 8u;  // per-lane bytes
+    const uint32_t rstride = ((uint32_t)NT << (dtile - wlog)) * 8u;     // bytes, uniform
+    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t pf[E];
     {
-        const uint64_t *src = data + tile_base(tile, tlog, wlog, dtile) + p_off;
+        const uint32_t sb = tile_base(tile, tlog, wlog, dtile) * 8u;
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = src[(size_t)r * rstride];
+        for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
     for (;;) {
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
@@ -165,10 +190,9 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
         {
-            const uint64_t *src =
-                data + tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) + p_off;
+            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) * 8u;
 #pragma unroll
-            for (int r = 0; r < E; ++r) pf[r] = src[(size_t)r * rstride];
+            for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         }
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
@@ -178,9 +202,9 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                                    wlog < tlog ? (int)wlog : 0, seed);
         }
         {
-            uint64_t *dst = data + base + p_off;
+            const uint32_t sb = base * 8u;
 #pragma unroll
-            for (int r = 0; r < E; ++r) dst[(size_t)r * rstride] = sm[lpad(threadIdx.x + r * NT)];
+            for (int r = 0; r < E; ++r) bt_store<kTileCP>(rs, voff, sb + (uint32_t)r * rstride, sm[lpad(threadIdx.x + r * NT)]);
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
@@ -196,8 +220,6 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // uniform part into 64 per-record 64-bit addresses that stay live across the
 // compare-exchanges (R = 6: ~290 VGPRs, one wave per SIMD).  Byte offsets are 32-bit:
 // M <= 2^29 (checked by the callers).
-typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
-constexpr int kBufNT = 2;  // cache policy: nontemporal (streaming, each byte used once)
 
 template <int MODE, int R>
 __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
@@ -207,21 +229,14 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
     if (t >= ngroups) return;
     const uint32_t dlog = jtop - R + 1;
     const uint32_t b = spread(t, dlog, R);
-    const int voff = (int)(b * 8u);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(data, (short)0, (int)0xFFFFFFFF, 0x00020000);
+    const uint32_t voff = b * 8u;
+    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t v[1 << R];
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) {
-        const bt_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (int)((uint32_t)q << (dlog + 3)), kBufNT);
-        v[q] = ((uint64_t)x.y << 32) | x.x;
-    }
+    for (int q = 0; q < (1 << R); ++q) v[q] = bt_load(rs, voff, (uint32_t)q << (dlog + 3));
     group_steps<MODE, R>(v, b, dlog, ilog, seed);
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) {
-        const bt_u32x2 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32)};
-        __builtin_amdgcn_raw_buffer_store_b64(x, rs, voff, (int)((uint32_t)q << (dlog + 3)), kBufNT);
-    }
+    for (int q = 0; q < (1 << R); ++q) bt_store(rs, voff, (uint32_t)q << (dlog + 3), v[q]);
 }
 
 template <int MODE>
