@@ -217,7 +217,8 @@ def e2e_sample(torch, D, n, d, device, reps=3):
     return dict(value=n * d / wall, unit="client-params/s", ms_per_call=wall * 1e3,
                 load_ms=ph[0] * 1e3, decrypt_ms=ph[1] * 1e3, aggregate_ms=ph[2] * 1e3,
                 bytes_h2d=n * d * 8, note="ecall_secure_aggregation, pageable host ciphertext, "
-                "times = execution_time_results {load=H2D, decrypt=AES kernel, aggregate+D2H}")
+                "times = execution_time_results {load = H2D (AES pipelined under it), decrypt = "
+                "AES left after the last chunk landed, aggregate+D2H}")
 
 
 def traffic_from_profiles(name):

@@ -22,6 +22,9 @@ struct DeviceCtx {
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
     hipStream_t stream = nullptr;                        // ECALL stream
+    hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)
+    static constexpr int kCopyEvents = 64;
+    hipEvent_t copy_ev[kCopyEvents] = {};
 };
 
 // One process-wide lock: the enclave had a single TCS (Enclave.config.xml:6).
