@@ -90,6 +90,9 @@ __device__ __forceinline__ void bt_store(__amdgpu_buffer_rsrc_t rs, uint32_t vof
 // Where a 2^14-tile merge pass goes at M = 2^27 (MI355X, rocprofv3): 468 us in all;
 // 390 us with the LDS rounds skipped (load -> LDS -> store only), 340 us with the
 // global stores skipped; a register-only pass (bitonic_global R=1) streams at 321 us.
+// Tried and dropped: the steps below 2^10 in registers (lane exchanges by DPP /
+// v_permlane16/32_swap, no LDS) — correct, but 577 us per merge and 9.5 ms for the
+// tile sort (spills at 1024 lanes; ~12 VALU per record per cross-lane step).
 constexpr int kTileCP = 0;
 
 // ------------------------------------------------------------- LDS tile ----
