@@ -270,10 +270,13 @@ def main():
     kk = d if k is None else k
 
     recs = [make_records(torch, n, d, k, 17 + 101 * rank + b, device) for b in range(3)]
-    out = torch.empty(d, dtype=torch.float32, device=device)
+    # double-buffered shard outputs: step i's RCCL gather (async, RCCL's own stream)
+    # overlaps step i+1's kernel; step i+2 waits for it before reusing the buffer
+    outs = [torch.empty(d, dtype=torch.float32, device=device) for _ in range(2)]
     status = torch.zeros(1, dtype=torch.int32, device=device)
-    gathered = ([torch.empty(d, dtype=torch.float32, device=device) for _ in range(world)]
-                if (world > 1 and rank == 0) else None)
+    gathered = ([[torch.empty(d, dtype=torch.float32, device=device) for _ in range(world)]
+                 for _ in range(2)] if (world > 1 and rank == 0) else None)
+    works = {}
     kw = dict(dense=k is None, status=status)
     if w.get("dp"):
         kw.update(dp=True, sigma=1.12, clipping=1.0, seed=7)
@@ -283,16 +286,25 @@ def main():
            for _ in range(args.steps)]
 
     def step(i, ev=None):
+        b = i % 2
+        if (i - 2) in works:
+            works.pop(i - 2).wait()  # the stream waits for the gather that read outs[b]
         if ev is not None:
             ev[0].record(stream)
-        D.aggregate(w["alg"], recs[i % 3], n, kk, d, out=out, **kw)
+        D.aggregate(w["alg"], recs[i % 3], n, kk, d, out=outs[b], **kw)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:  # final RCCL step: averaged shards -> root over xGMI
-            dist.gather(out, gathered, dst=0)
+            works[i] = dist.gather(outs[b], gathered[b] if rank == 0 else None, dst=0,
+                                   async_op=True)
+
+    def drain():
+        for j in sorted(works):
+            works.pop(j).wait()
 
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -300,6 +312,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, kev[i])
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -329,7 +342,8 @@ def main():
             "config": {"workload": w["desc"], "alg": ALG_NAMES[w["alg"]], "n_clients": n,
                        "d_per_gpu": d, "k": kk, "record_bytes": 8,
                        "parallelism": f"param-range shard x{world}" +
-                                      (", RCCL gather to rank 0" if world > 1 else "")},
+                                      (f", {backend} gather to rank 0 (async, overlapped with the "
+                                       "next step)" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": algo_bytes / kern / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": algo_bytes / kern / 1e9 / HBM_PEAK_GBS,
                          "traffic": traffic_from_profiles(args.workload),
