@@ -45,87 +45,125 @@ __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint3
     return mv ? right : (st ? self : CP_DUMMY);
 }
 
+typedef unsigned int cp_u32x2 __attribute__((ext_vector_type(2)));
+
 // FIRST: src holds folded records (idx, val); else (c, val).
 // FINAL: 0 = write (c, val) records, 1 = out[i] = val*coef, 2 = out[i] += val.
-template <int CAP, int NT, bool FIRST, int FINAL>
+// Persistent: block b walks tiles b, b + grid, ...; the next tile's records are
+// prefetched into registers (raw buffer loads, out-of-range lanes selected to the
+// dummy afterwards: no per-load branch) while the current tile runs its levels.
+template <int NT, int PER, bool FIRST, int FINAL>
 __global__ __launch_bounds__(NT) void compact_pass(const uint64_t *__restrict__ src,
                                                    uint64_t *__restrict__ dst, uint32_t L,
                                                    uint32_t d, uint32_t j0, uint32_t G,
                                                    uint32_t logW, uint32_t S, uint32_t rows,
                                                    uint32_t ngroups, float coef,
-                                                   float *__restrict__ out) {
-    constexpr uint32_t PER = CAP / NT;
+                                                   float *__restrict__ out, uint32_t ntiles) {
+    constexpr uint32_t CAP = (uint32_t)NT * PER;
     __shared__ uint64_t sm[CAP];
     const uint32_t W = 1u << logW, H = (1u << G) - 1;
-    const uint32_t band = blockIdx.x / ngroups, grp = blockIdx.x - band * ngroups;
-    const uint32_t s0 = band * S, b0 = grp << logW;
     const uint32_t t = threadIdx.x;
-    const uint32_t nld = min(S + H, rows - s0) << logW;  // tile slots that map below L's rows
-    auto pos_of = [&](uint32_t f) -> uint32_t {
-        return ((s0 + (f >> logW)) << j0) + b0 + (f & (W - 1));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)src, (short)0, (int)(L * 8u), 0x00020000);
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    // global position of tile slot f (64-bit: rows past L may exceed 2^32 at large j0)
+    auto pos_of = [&](uint32_t tl, uint32_t f) -> uint64_t {
+        const uint32_t band = tl / ngroups, grp = tl - band * ngroups;
+        return ((uint64_t)(band * S + (f >> logW)) << j0) + (grp << logW) + (f & (W - 1));
     };
+    uint64_t pf[PER];
+    auto prefetch = [&](uint32_t tl) {
 #pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) {
-        const uint32_t f = t + i * NT;
-        uint64_t v = CP_DUMMY;
-        if (f < nld) {
-            const uint32_t p = pos_of(f);
-            if (p < L) {
-                v = src[p];
-                if (FIRST) {
-                    const uint32_t idx = (uint32_t)v;
-                    v = (v & 0xFFFFFFFF00000000ull) | (idx < d ? (uint64_t)(p - idx) : CP_DUMMY);
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint64_t p = pos_of(tl, t + i * NT);
+            const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
+                rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
+            pf[i] = p < L ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
+        }
+    };
+    prefetch(tile);
+    for (;;) {
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) {
+            uint64_t v = pf[i];
+            if (FIRST) {  // key -> shift c = p - idx (u32::MAX when not selected)
+                const uint32_t p = (uint32_t)pos_of(tile, t + i * NT), idx = (uint32_t)v;
+                v = (v & 0xFFFFFFFF00000000ull) | (idx < d ? (uint64_t)(p - idx) : CP_DUMMY);
+            }
+            sm[t + i * NT] = v;
+        }
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        prefetch(next < ntiles ? next : tile);
+        // Levels two per LDS round: z[f] = pick_{g+1}(pick_g(x[f], x[f+s]),
+        // pick_g(x[f+2s], x[f+3s])) — 4 reads + 1 write per record per two levels
+        // instead of 2 + 1 per level (ds_write_b64 costs ~3x a ds_read_b64), half the
+        // barriers.  After level g the rows still needed are S + H - (2^(g+1) - 1).
+        uint64_t nv[PER];
+        for (uint32_t g = 0; g < G;) {
+            const uint32_t stepf = W << g;
+            const uint32_t j = j0 + g;
+            const bool two = g + 1 < G;
+            const uint32_t gl = two ? g + 1 : g;
+            const uint32_t lim = (S + H - ((2u << gl) - 1)) << logW;
+            if (two) {
+#pragma unroll
+                for (uint32_t i = 0; i < PER; ++i) {
+                    const uint32_t f = t + i * NT;
+                    if (f < lim) {
+                        const uint64_t y0 = cp_pick(sm[f], sm[f + stepf], j);
+                        const uint64_t y2 = cp_pick(sm[f + 2 * stepf], sm[f + 3 * stepf], j);
+                        nv[i] = cp_pick(y0, y2, j + 1);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < PER; ++i) {
+                    const uint32_t f = t + i * NT;
+                    if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], j);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t i = 0; i < PER; ++i) {
+                const uint32_t f = t + i * NT;
+                if (f < lim) sm[f] = nv[i];
+            }
+            __syncthreads();
+            g += two ? 2 : 1;
+        }
+        const uint32_t nout = S << logW;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t f = t + i * NT;
+            if (f < nout) {
+                const uint64_t p = pos_of(tile, f);
+                if (FINAL == 0) {
+                    if (p < L) dst[p] = sm[f];
+                } else if (p < d) {
+                    const float v = rec_val(sm[f]);
+                    out[p] = FINAL == 2 ? __fadd_rn(out[p], v) : __fmul_rn(v, coef);
                 }
             }
         }
-        sm[f] = v;
-    }
-    __syncthreads();
-    uint64_t nv[PER];
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t stepf = W << g;
-        const uint32_t lim = (S + H - ((2u << g) - 1)) << logW;  // rows still needed after g
-        const uint32_t j = j0 + g;
-#pragma unroll
-        for (uint32_t i = 0; i < PER; ++i) {
-            const uint32_t f = t + i * NT;
-            if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], j);
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t i = 0; i < PER; ++i) {
-            const uint32_t f = t + i * NT;
-            if (f < lim) sm[f] = nv[i];
-        }
-        __syncthreads();
-    }
-    const uint32_t nout = min(S << logW, nld);
-#pragma unroll
-    for (uint32_t i = 0; i < PER; ++i) {
-        const uint32_t f = t + i * NT;
-        if (f < nout) {
-            const uint32_t p = pos_of(f);
-            if (FINAL == 0) {
-                if (p < L) dst[p] = sm[f];
-            } else if (p < d) {
-                const float v = rec_val(sm[f]);
-                out[p] = FINAL == 2 ? __fadd_rn(out[p], v) : __fmul_rn(v, coef);
-            }
-        }
+        if (next >= ntiles) break;
+        __syncthreads();  // this tile's LDS reads retire before the next tile lands
+        tile = next;
     }
 }
 
-static int g_compact_variant = 0;  // fltee_debug_set_compact_variant (A/B): 0 = 64 KiB tiles
+static int g_compact_variant = 1;  // fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB
 void set_compact_variant(int v) { g_compact_variant = v; }
 
-template <int CAP, int NT>
+template <int NT, int PER>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
                               uint64_t *dst, uint32_t L, uint32_t d, uint32_t j0, uint32_t G,
                               uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
-                              float coef, float *out) {
-#define CP_GO(F, X)                                                                           \
-    hipLaunchKernelGGL((compact_pass<CAP, NT, F, X>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
-                       d, j0, G, logW, S, rows, ngroups, coef, out)
+                              float coef, float *out, uint32_t ntiles) {
+#define CP_GO(F, X)                                                                              \
+    hipLaunchKernelGGL((compact_pass<NT, PER, F, X>), dim3(grid), dim3(NT), 0, s, src, dst, L, d, \
+                       j0, G, logW, S, rows, ngroups, coef, out, ntiles)
     if (first) {
         if (fin == 0) CP_GO(true, 0); else if (fin == 1) CP_GO(true, 1); else CP_GO(true, 2);
     } else {
@@ -148,6 +186,7 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
     if (d == 0) return hipSuccess;
     const uint32_t nlev = L > d ? bitlen(L - d) : 0;
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
+    if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets
     const bool small = g_compact_variant == 1;
     const uint32_t CAP = small ? 4096 : 8192;
     uint64_t *cur = src, *oth = tmp;
@@ -172,15 +211,17 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
         }
         const uint32_t ngroups = (uint32_t)(((uint64_t)1 << j0) >> logW);
         const uint64_t bands = (rows + S - 1) / S;
-        const uint64_t grid = bands * ngroups;
-        if (grid == 0 || grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        const uint64_t ntiles = bands * ngroups;
+        if (ntiles == 0 || ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
+        // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
+        const unsigned grid = (unsigned)(ntiles < (small ? 512u : 256u) ? ntiles : (small ? 512u : 256u));
         const hipError_t e =
-            small ? launch_pass<4096, 256>(j0 == 0, fin, (unsigned)grid, s, cur, oth, (uint32_t)L,
-                                           (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out)
-                  : launch_pass<8192, 512>(j0 == 0, fin, (unsigned)grid, s, cur, oth, (uint32_t)L,
-                                           (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out);
+            small ? launch_pass<512, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
+                                        G, logW, S, rows, ngroups, coef, out, (uint32_t)ntiles)
+                  : launch_pass<1024, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
+                                         G, logW, S, rows, ngroups, coef, out, (uint32_t)ntiles);
         if (e != hipSuccess) return e;
         uint64_t *x = cur; cur = oth; oth = x;
         j0 += G;

@@ -55,7 +55,7 @@ def main():
                 times[v].append(a.elapsed_time(b) / args.launches)
     finally:
         L.lib().fltee_debug_set_advanced_compaction(1)
-        L.lib().fltee_debug_set_compact_variant(0)
+        L.lib().fltee_debug_set_compact_variant(1)
     assert int(st.item()) == 0
     for v, t in times.items():
         print(json.dumps({"workload": args.workload, "variant": v, "median_ms": float(np.median(t)),
