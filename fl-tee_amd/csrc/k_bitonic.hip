@@ -143,11 +143,12 @@ template <int MODE, int E, int NT>
 __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, int jtop, int jbot,
                                           uint32_t seed) {
-    constexpr int rmax = E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1));
+    constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     while (jtop >= jbot) {
         const int left = jtop - jbot + 1;
         const int r = left < rmax ? left : rmax;
-        if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        if (rmax >= 5 && r == 5) lds_round<MODE, (rmax >= 5 ? 5 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         else lds_round<MODE, 1, E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
@@ -279,6 +280,16 @@ static uint32_t max_tile_log() {
     }();
     return t;
 }
+// 2^14 tiles as 512 lanes x 32 records (5 steps per LDS round: 3 rounds per merge
+// instead of 4) instead of 1024 x 16 — A/B knob; measured no faster at M = 2^27
+// (merge 468 us either way, tile sort 2.51 vs 2.40 ms), so off by default.
+static bool tile32() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_TILE32");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 // Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
 // disables them, for A/B runs).
 static bool strided_passes() {
@@ -316,6 +327,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles)
     if (c.NT == 1024) BT_GO(16, 1024);
+    if (c.E == 32) BT_GO(32, 512);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
     if (c.NT == 64) BT_GO(2, 64);
@@ -354,9 +366,10 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     }
     c.tlog = tlog;
     const uint32_t T = 1u << tlog;
-    if (tlog == 14) {
-        c.E = 16;
-        c.NT = 1024;
+    if (tlog == 14) {  // FLTEE_BITONIC_TILE32=1: 512 lanes x 32 records (5 steps per round)
+        const bool e32 = tile32();
+        c.E = e32 ? 32 : 16;
+        c.NT = e32 ? 512 : 1024;
     } else if (T >= 1024) {
         c.E = T / 512 > 16 ? 16 : T / 512;  // 512 lanes
         c.NT = 512;
