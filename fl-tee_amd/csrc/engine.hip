@@ -23,6 +23,17 @@ hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t 
                                     uint32_t *status, hipStream_t s);
 hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
                                   bool accumulate, hipStream_t s);
+hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uint32_t *mat,
+                              uint32_t *dup, float coef, float *out, bool accumulate,
+                              uint32_t *status, hipStream_t s);
+
+// Sparse non_oblivious: scatter into per-client rows (k_accumulate.hip) when the
+// [n][d] row matrix costs less HBM traffic than the stable sort it replaces
+// (rows: ~8*n*d bytes; sort: >= 16*M bytes per pass, tens of passes).
+static bool use_scatter_rows(size_t n, size_t k, size_t d) {
+    const size_t cells = n * d;
+    return cells <= ((size_t)1 << 30) && cells <= 64 * next_pow2_sz(n * k);
+}
 
 static DeviceCtx g_ctx[kMaxDevices];
 static std::mutex g_ctx_mu;
@@ -104,7 +115,10 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         if (!dense) p.mat_bytes = n * d * 4;
         break;
     case FLTEE_ALG_NON_OBLIVIOUS:
-        if (!dense) p.a_bytes = next_pow2_sz(n * k) * 8;
+        if (!dense) {
+            if (use_scatter_rows(n, k, d)) p.mat_bytes = n * d * 4;
+            else p.a_bytes = next_pow2_sz(n * k) * 8;
+        }
         break;
     case FLTEE_ALG_ADVANCED:
         p.a_bytes = p.b_bytes = next_pow2_sz(n * k + d) * 8;
@@ -191,6 +205,9 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (dense) {
             e = launch_dense_accumulate(rec, n, d, coef, out, ccoef, acc, status, s);
+        } else if (alg == FLTEE_ALG_NON_OBLIVIOUS && use_scatter_rows(n, k, d)) {
+            e = launch_scatter_sum(rec, n, k, d, (uint32_t *)c->ws_mat.ptr, c->status + 16, coef,
+                                   out, acc, status, s);
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
             const size_t M = next_pow2_sz(n * k);
             uint64_t *K = (uint64_t *)c->ws_a.ptr;

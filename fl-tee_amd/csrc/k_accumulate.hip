@@ -350,6 +350,122 @@ hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float
     return hipGetLastError();
 }
 
+// ------------------------------------------------- sparse non_oblivious ----
+// non_oblivious.rs:6-15 is a plain scatter-add with no obliviousness to keep, so
+// its GPU form is a scatter too.  Client c's records land at mat[c][idx] (mat
+// pre-filled with the empty sentinel), then the rows are summed in client order
+// with the sentinel read as +0.0 — adding +0.0 to a running sum that started at
+// +0.0 is the identity (such a sum is never -0.0), so every output is the
+// reference's in-order sum, bit for bit.  That needs a client's indices to be
+// distinct (top-k, utils.py:327-354): a repeated index, or a value whose bits are
+// the sentinel, sets *dup and the row pass switches (uniformly, same launch) to
+// the in-order sequential sweep over every record.  Traffic: n*k*8 + n*d*4*2 + d*4.
+constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restrict__ rec, size_t n,
+                                                           size_t k, size_t d,
+                                                           uint32_t *__restrict__ mat,
+                                                           uint32_t *dup, uint32_t *status) {
+    uint32_t bad = 0, rep = 0;
+    for (size_t c = blockIdx.y; c < n; c += gridDim.y) {
+        for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < k; e += (size_t)gridDim.x * 256) {
+            const uint2 r = rec[c * k + e];
+            if (r.x >= d) { bad = 1; continue; }
+            const uint32_t old = atomicCAS(mat + c * d + r.x, kEmptySlot, r.y);
+            rep |= (old != kEmptySlot) | (r.y == kEmptySlot);
+        }
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, FLTEE_DEV_ERR_INDEX_RANGE);
+    if (__any(rep) && (threadIdx.x & 63) == 0) atomicOr(dup, 1u);
+}
+
+// Lane t owns outputs 4t..4t+3.  VEC: d % 4 == 0 (16-B rows).
+template <bool VEC, bool ACC>
+__global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restrict__ mat, size_t d,
+                                                        uint32_t n, const uint2 *__restrict__ rec,
+                                                        size_t nrec, const uint32_t *dup,
+                                                        float coef, float *__restrict__ out) {
+    const size_t j0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    bool hit[4] = {false, false, false, false};
+    if (*dup == 0) {
+        if (j0 >= d) return;
+        for (uint32_t c = 0; c < n; ++c) {
+            uint32_t x[4];
+            const uint32_t *row = mat + (size_t)c * d + j0;
+            if (VEC) {
+                const uint4 v = ld_nt(reinterpret_cast<const uint4 *>(row));
+                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = (j0 + i < d) ? row[i] : kEmptySlot;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool h = x[i] != kEmptySlot;
+                acc[i] = __fadd_rn(acc[i], h ? __uint_as_float(x[i]) : 0.0f);
+                hit[i] |= h;
+            }
+        }
+    } else {  // a client repeated an index: every record, in upload order
+        __shared__ uint2 tile[SW_CHUNK];
+        for (size_t c0 = 0; c0 < nrec; c0 += SW_CHUNK) {
+            const uint32_t m = (uint32_t)((nrec - c0) < SW_CHUNK ? (nrec - c0) : SW_CHUNK);
+            __syncthreads();
+            for (uint32_t e = threadIdx.x; e < m; e += 256) tile[e] = rec[c0 + e];
+            __syncthreads();
+            for (uint32_t q = 0; q < m; ++q) {
+                const uint2 r = tile[q];
+                const size_t delta = (size_t)r.x - j0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const bool h = delta == (size_t)i;
+                    acc[i] = __fadd_rn(acc[i], h ? __uint_as_float(r.y) : 0.0f);
+                    hit[i] |= h;
+                }
+            }
+        }
+        if (j0 >= d) return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (j0 + i >= d) break;
+        if (ACC) {
+            if (hit[i]) out[j0 + i] = __fadd_rn(out[j0 + i], acc[i]);
+        } else {
+            out[j0 + i] = __fmul_rn(acc[i], coef);
+        }
+    }
+}
+
+hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uint32_t *mat,
+                              uint32_t *dup, float coef, float *out, bool accumulate,
+                              uint32_t *status, hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(mat, 0xFF, n * d * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(dup, 0, 4, s);
+    if (e != hipSuccess) return e;
+    if (k) {
+        const size_t bx = (k + 255) / 256 < 1024 ? (k + 255) / 256 : 1024;
+        const size_t by = n < 65535 ? n : 65535;
+        hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, s,
+                           (const uint2 *)rec, n, k, d, mat, dup, status);
+    }
+    const unsigned blocks = (unsigned)((d + 1023) / 1024);
+    const bool vec = d % 4 == 0 && (uintptr_t)mat % 16 == 0;
+    const size_t nrec = n * k;
+#define FLTEE_SRS(V, A)                                                                      \
+    hipLaunchKernelGGL((scatter_rows_sum<V, A>), dim3(blocks), dim3(256), 0, s, mat, d,     \
+                       (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out)
+    if (vec) {
+        if (accumulate) FLTEE_SRS(true, true); else FLTEE_SRS(true, false);
+    } else {
+        if (accumulate) FLTEE_SRS(false, true); else FLTEE_SRS(false, false);
+    }
+#undef FLTEE_SRS
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------- helpers -----
 __global__ void scale_kernel(float *out, size_t d, float coef) {
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;

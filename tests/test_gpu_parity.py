@@ -67,7 +67,10 @@ def test_dense_order_violation_is_reported(dev):
     assert dev.status() & 0x1
 
 
-@pytest.mark.parametrize("n,d,k", [(1, 10, 3), (4, 1000, 100), (30, 50890, 5089), (7, 3001, 2999)])
+# (2, 2M, 100): non_oblivious takes the stable-sort path (the [n][d] scatter rows would
+# cost more than the sort); the others take the scatter-rows path
+@pytest.mark.parametrize("n,d,k", [(1, 10, 3), (4, 1000, 100), (30, 50890, 5089), (7, 3001, 2999),
+                                   (2, 2_000_000, 100)])
 @pytest.mark.parametrize("alg", [3, 4, 5])
 def test_sparse_bit_exact(dev, oracle, n, d, k, alg):
     rng = np.random.default_rng(n + d + k)
@@ -87,6 +90,22 @@ def test_sparse_repeated_index_flagged(dev):
     out = dev.aggregate(4, rec, 2, 2, 8).cpu().numpy()  # non_oblivious handles it exactly
     assert dev.status() == 0
     assert out.tolist() == [0, 1.0, 0.5, 0.5, 0, 0, 0, 0]
+
+
+def test_non_oblivious_scatter_sentinel_value(dev, oracle):
+    # a value whose bits equal the scatter's empty-slot sentinel (a NaN) takes the
+    # in-order sweep, like a repeated index; every other output stays bit-exact
+    rng = np.random.default_rng(3)
+    n, d, k = 3, 500, 50
+    idx, val = rand_sparse(rng, n, d, k)
+    val[7] = np.uint32(0xFFFFFFFF).view(np.float32)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(4, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    nan = np.isnan(ref)
+    assert st == 0 and nan.sum() == 1 and np.isnan(out[nan]).all()
+    assert bits_equal(out[~nan], ref[~nan])
 
 
 def test_non_oblivious_index_out_of_range(dev):
