@@ -85,10 +85,26 @@ hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, 
 // ascending (even segments) / descending (odd segments)
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
                                  hipStream_t s);
+// one range [pbase, pbase + m) of a larger network (pbase a multiple of m): stages
+// 1..log2 m; the steps j < m of stage ilog; the step 2^jlog >= m of stage ilog
+// between this range and the partner range pos_theirs = pos_mine ^ 2^jlog
+hipError_t bitonic_sort_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                              uint32_t pbase, hipStream_t s);
+hipError_t bitonic_merge_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                               uint32_t ilog, uint32_t pbase, hipStream_t s);
+hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, uint32_t pos_mine,
+                            uint32_t pos_theirs, uint32_t mode, uint32_t seed, uint32_t ilog,
+                            uint32_t jlog, hipStream_t s);
 
 // k_fold.hip
 hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *dst,
                                 hipStream_t s);
+hipError_t launch_advanced_init_range(const void *rec, size_t nrec, size_t d, size_t pbase,
+                                      size_t m, uint64_t *dst, hipStream_t s);
+size_t fold_context(size_t halo);  // records of context the fold re-reads: halo rounded to 16
+hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
+                             size_t end, long long pbase, size_t fold_len, size_t halo,
+                             uint32_t *status, hipStream_t s);
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
                        uint32_t *status, hipStream_t s);
 hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
@@ -96,6 +112,8 @@ hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out,
 // k_compact.hip
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
                                   float *out, bool accumulate, hipStream_t s);
+hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint64_t *buf,
+                                 uint64_t *tmp, float coef, float *out, hipStream_t s);
 hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,
                                  uint32_t *status, hipStream_t s);
 hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,

@@ -364,6 +364,87 @@ extern "C" fltee_status_t fltee_laplace_r_device(size_t d, size_t k, size_t n, u
                : FLTEE_ERROR_UNEXPECTED;
 }
 
+// ---- position-range pieces of `advanced` (SURVEY §8e Option B) ----------
+static bool range_ok(size_t m, size_t pos_base) {
+    return m >= 2 && !(m & (m - 1)) && pos_base % m == 0 && pos_base + m <= ((size_t)1 << 31);
+}
+
+extern "C" fltee_status_t fltee_advanced_init_range_device(const void *d_records, size_t nrec,
+                                                           size_t d, size_t pos_base, size_t m,
+                                                           void *d_dst, void *stream) {
+    return launch_advanced_init_range(d_records, nrec, d, pos_base, m, (uint64_t *)d_dst,
+                                      (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_bitonic_range_sort_device(void *d_records, size_t m,
+                                                          size_t pos_base, uint32_t mode,
+                                                          uint32_t seed, void *stream) {
+    if (!range_ok(m, pos_base)) return FLTEE_ERROR_INVALID_PARAMETER;
+    return bitonic_sort_range((uint64_t *)d_records, m, mode, seed, (uint32_t)pos_base,
+                              (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_bitonic_range_merge_device(void *d_records, size_t m,
+                                                           size_t pos_base, uint32_t mode,
+                                                           uint32_t seed, uint32_t stage_log,
+                                                           void *stream) {
+    if (!range_ok(m, pos_base) || ((size_t)1 << stage_log) <= m || stage_log > 31)
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    return bitonic_merge_range((uint64_t *)d_records, m, mode, seed, stage_log,
+                               (uint32_t)pos_base, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_bitonic_range_exchange_device(void *d_mine, const void *d_theirs,
+                                                              size_t m, size_t pos_mine,
+                                                              size_t pos_theirs, uint32_t mode,
+                                                              uint32_t seed, uint32_t stage_log,
+                                                              void *stream) {
+    if (!range_ok(m, pos_mine) || !range_ok(m, pos_theirs) || stage_log > 31)
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    const size_t j = pos_mine > pos_theirs ? pos_mine - pos_theirs : pos_theirs - pos_mine;
+    if ((j & (j - 1)) || j < m || j >= ((size_t)1 << stage_log) || (pos_mine ^ pos_theirs) != j)
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    return bitonic_exchange((uint64_t *)d_mine, (const uint64_t *)d_theirs, m, (uint32_t)pos_mine,
+                            (uint32_t)pos_theirs, mode, seed, stage_log, log2_pow2(j),
+                            (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" size_t fltee_fold_context(size_t halo) { return fold_context(halo); }
+
+extern "C" fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m,
+                                                  size_t origin, size_t end, int64_t pos_base,
+                                                  size_t fold_len, size_t halo,
+                                                  uint32_t *d_status, void *stream) {
+    if (!d_status || origin < fold_context(halo) || end > m || origin >= end || (origin & 1) ||
+        (end & 1) || (m & 1))
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    if (end < m ? false : (int64_t)end + pos_base < (int64_t)fold_len)
+        return FLTEE_ERROR_INVALID_PARAMETER;  // needs the next range's first record
+    return launch_fold_range((const uint64_t *)d_src, (uint64_t *)d_dst, m, origin, end,
+                             (long long)pos_base, fold_len, halo, d_status,
+                             (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_compact_range_device(const void *d_chunk, size_t c, size_t d,
+                                                     void *d_buf, void *d_tmp, float coef,
+                                                     float *d_out, void *stream) {
+    if (d + c >= ((size_t)1 << 29)) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_compact_offset((const uint64_t *)d_chunk, c, d, (uint64_t *)d_buf,
+                                 (uint64_t *)d_tmp, coef, d_out, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
 
 extern "C" fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d,

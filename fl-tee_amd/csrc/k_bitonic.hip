@@ -171,7 +171,7 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
 template <int MODE, bool SORT, int E, int NT>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                                    uint32_t seed, uint32_t ntiles) {
+                                                    uint32_t seed, uint32_t ntiles, uint32_t pbase) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -200,9 +200,9 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         }
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base, wlog, dtile, il, (int)il - 1, 0, seed);
+                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
         } else {
-            lds_steps<MODE, E, NT>(sm, base, wlog, dtile, ilog, (int)tlog - 1,
+            lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
                                    wlog < tlog ? (int)wlog : 0, seed);
         }
         {
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 template <int MODE, int R>
 __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
                                                       uint32_t jtop, uint32_t seed,
-                                                      uint32_t ngroups) {
+                                                      uint32_t ngroups, uint32_t pbase) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     if (t >= ngroups) return;
     const uint32_t dlog = jtop - R + 1;
@@ -238,23 +238,23 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
     uint64_t v[1 << R];
 #pragma unroll
     for (int q = 0; q < (1 << R); ++q) v[q] = bt_load(rs, voff, (uint32_t)q << (dlog + 3));
-    group_steps<MODE, R>(v, b, dlog, ilog, seed);
+    group_steps<MODE, R>(v, b + pbase, dlog, ilog, seed);
 #pragma unroll
     for (int q = 0; q < (1 << R); ++q) bt_store(rs, voff, (uint32_t)q << (dlog + 3), v[q]);
 }
 
 template <int MODE>
 static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jtop,
-                                int R, uint32_t seed, hipStream_t s) {
+                                int R, uint32_t seed, hipStream_t s, uint32_t pbase) {
     const uint32_t ngroups = 1u << (mlog - R);
     const unsigned blocks = (ngroups + 255) / 256;
     switch (R) {
-    case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
-    case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
-    case 3: hipLaunchKernelGGL((bitonic_global<MODE, 3>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
-    case 4: hipLaunchKernelGGL((bitonic_global<MODE, 4>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
-    case 5: hipLaunchKernelGGL((bitonic_global<MODE, 5>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
-    default: hipLaunchKernelGGL((bitonic_global<MODE, 6>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups); break;
+    case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    case 3: hipLaunchKernelGGL((bitonic_global<MODE, 3>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    case 4: hipLaunchKernelGGL((bitonic_global<MODE, 4>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    case 5: hipLaunchKernelGGL((bitonic_global<MODE, 5>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    default: hipLaunchKernelGGL((bitonic_global<MODE, 6>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
     }
     return hipGetLastError();
 }
@@ -303,7 +303,7 @@ static bool strided_passes() {
 template <int MODE, bool SORT, int E, int NT>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                 uint32_t seed, uint32_t tiles) {
+                                 uint32_t seed, uint32_t tiles, uint32_t pbase) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT>,
@@ -311,7 +311,7 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
         attr = true;
     }
     hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
-                       tlog, ilog, wlog, dtile, seed, tiles);
+                       tlog, ilog, wlog, dtile, seed, tiles, pbase);
     return hipGetLastError();
 }
 
@@ -323,9 +323,9 @@ struct TileCfg {
 
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
-                               uint32_t wlog, uint32_t dtile, uint32_t seed) {
+                               uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
 #define BT_GO(E_, NT_) \
-    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles)
+    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
     if (c.NT == 1024) BT_GO(16, 1024);
     if (c.E == 32) BT_GO(32, 512);
     if (c.NT == 256) BT_GO(2, 256);
@@ -340,31 +340,19 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 #undef BT_GO
 }
 
-// Stages 1..slog of the network over m records (slog = log2 m: the full sort).  With
-// slog < log2 m every aligned segment of 2^slog records comes out sorted, ascending
-// where bit slog of its first position is 0 and descending where it is 1.
-template <int MODE>
-static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s,
-                            uint32_t slog) {
-    const int kMaxGlobalR = max_global_r();
-    const uint32_t mlog = log2_pow2(m);
-    TileCfg c;
-    // 2^14-record tiles (1024 lanes x 16) when there are enough of them to fill the
-    // CUs; else up to 2^13 with 512 lanes; small sorts use E = 2 and T/2 lanes
+// Tile configuration for an m = 2^mlog record array whose sort runs stages 1..slog.
+// 2^14-record tiles (1024 lanes x 16) when there are enough of them to fill the CUs;
+// else up to 2^13 with 512 lanes; small sorts use E = 2 and T/2 lanes; tlog <= 6
+// means every stage is one register pass (no tiles).
+static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
+    TileCfg c{};
     const uint32_t tmax = max_tile_log();
     uint32_t tlog = mlog < tmax ? mlog : tmax;
     if (tlog > slog) tlog = slog;
     if (tlog == 14 && mlog - tlog < 8) tlog = 13;
     while (tlog > 11 && tlog <= 13 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles
-    hipError_t e;
-    if (tlog <= 6) {  // tiles of <= 64 records: every stage is one register pass
-        for (uint32_t ilog = 1; ilog <= slog; ++ilog) {
-            e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s);
-            if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
-    }
     c.tlog = tlog;
+    if (tlog <= 6) return c;
     const uint32_t T = 1u << tlog;
     if (tlog == 14) {  // FLTEE_BITONIC_TILE32=1: 512 lanes x 32 records (5 steps per round)
         const bool e32 = tile32();
@@ -382,12 +370,21 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     // persistent: one (2^14) or two resident tiles per CU, each prefetching its next tile
     const unsigned resident = tlog == 14 ? 256 : 512;
     c.grid = c.tiles < resident ? c.tiles : resident;
-    e = launch_tiles<MODE, true>(c, s, data, 0u, tlog, tlog, seed);
-    if (e != hipSuccess) return e;
+    return c;
+}
+
+// Steps jtop..0 of stage ilog (ilog > c.tlog) over the m = 2^mlog records at global
+// positions pbase..pbase+m-1: the steps with j >= T in register passes (up to 6 steps)
+// or strided LDS passes (more than 6), then one merge tile pass for the steps j < T.
+template <int MODE>
+static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, uint32_t ilog,
+                              int jtop, uint32_t seed, uint32_t pbase, hipStream_t s) {
+    const int kMaxGlobalR = max_global_r();
+    const uint32_t tlog = c.tlog, T = 1u << tlog;
     const int rs = (int)tlog - 4;  // global steps per strided LDS pass (W >= 16)
-    for (uint32_t ilog = tlog + 1; ilog <= slog; ++ilog) {
-        int jtop = (int)ilog - 1;
-        const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
+    const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
+    hipError_t e;
+    if (nglobal > 0) {
         const int per = (strided_passes() && rs > kMaxGlobalR) ? rs : kMaxGlobalR;
         const int passes = (nglobal + per - 1) / per;
         for (int p = 0; p < passes; ++p) {
@@ -395,17 +392,85 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
             const int R = (left + (passes - p) - 1) / (passes - p);  // balanced split
             if (R > kMaxGlobalR && (T >> R) <= c.NT) {  // strided LDS tile: W = T / 2^R consecutive x 2^R rows
                 const uint32_t dtile = (uint32_t)(jtop - R + 1);
-                e = launch_tiles<MODE, false>(c, s, data, ilog, tlog - (uint32_t)R, dtile, seed);
+                e = launch_tiles<MODE, false>(c, s, data, ilog, tlog - (uint32_t)R, dtile, seed, pbase);
             } else {
-                e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s);
+                e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s, pbase);
             }
             if (e != hipSuccess) return e;
             jtop -= R;
         }
-        e = launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed);
+    }
+    return launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed, pbase);
+}
+
+// Stages 1..slog of the network over m records at global positions pbase.. (pbase a
+// multiple of m; slog = log2 m: the full sort of this range, ascending where bit slog
+// of pbase is 0 and descending where it is 1 — the reference network's direction).
+// With slog < log2 m every aligned segment of 2^slog records comes out sorted,
+// ascending where bit slog of its first position is 0 and descending where it is 1.
+template <int MODE>
+static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s,
+                            uint32_t slog, uint32_t pbase) {
+    const uint32_t mlog = log2_pow2(m);
+    const TileCfg c = make_cfg(mlog, slog);
+    hipError_t e;
+    if (c.tlog <= 6) {  // tiles of <= 64 records: every stage is one register pass
+        for (uint32_t ilog = 1; ilog <= slog; ++ilog) {
+            e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s, pbase);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    e = launch_tiles<MODE, true>(c, s, data, 0u, c.tlog, c.tlog, seed, pbase);
+    if (e != hipSuccess) return e;
+    for (uint32_t ilog = c.tlog + 1; ilog <= slog; ++ilog) {
+        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, pbase, s);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// The steps j = m/2 .. 1 of stage ilog > log2 m on the m records at global positions
+// pbase..: what a stage leaves to each range once its steps j >= m (the exchanges
+// between ranges, bitonic_exchange) are done.
+template <int MODE>
+static hipError_t merge_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s,
+                             uint32_t ilog, uint32_t pbase) {
+    const uint32_t mlog = log2_pow2(m);
+    if (mlog == 0) return hipSuccess;
+    const TileCfg c = make_cfg(mlog, mlog);
+    if (c.tlog <= 6)
+        return launch_global<MODE>(data, mlog, ilog, mlog - 1, (int)mlog, seed, s, pbase);
+    return stage_steps<MODE>(data, mlog, c, ilog, (int)mlog - 1, seed, pbase, s);
+}
+
+// Step j = 2^jlog >= m of stage ilog between two ranges of m records, `mine` at
+// positions pos_mine.. and the partner's copy `theirs` at pos_mine ^ j..: position x
+// of one pairs with position x of the other (l = the lower one, m = l + j), and
+// `mine` takes the partner's record iff that pair swaps.  Same comparator as
+// group_steps, so the ranges together run the reference network's step exactly.
+template <int MODE>
+__global__ __launch_bounds__(256) void bitonic_exchange_kernel(uint4 *__restrict__ mine,
+                                                               const uint4 *__restrict__ theirs,
+                                                               size_t m2, uint32_t pos_lo,
+                                                               uint32_t lower, uint32_t ilog,
+                                                               uint32_t key) {
+    for (size_t x = (size_t)blockIdx.x * 256 + threadIdx.x; x < m2; x += (size_t)gridDim.x * 256) {
+        const uint4 a4 = mine[x], b4 = theirs[x];
+        const uint64_t a[2] = {((uint64_t)a4.y << 32) | a4.x, ((uint64_t)a4.w << 32) | a4.z};
+        const uint64_t b[2] = {((uint64_t)b4.y << 32) | b4.x, ((uint64_t)b4.w << 32) | b4.z};
+        uint64_t r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t lo = lower ? a[h] : b[h], hi = lower ? b[h] : a[h];
+            const uint32_t l = pos_lo + (uint32_t)(2 * x + h);
+            const bool asc = (l & (1u << ilog)) == 0;
+            const bool sw = asc ^ cond2<MODE>(lo, hi, l, key);
+            r[h] = sw ? b[h] : a[h];
+        }
+        mine[x] = make_uint4((uint32_t)r[0], (uint32_t)(r[0] >> 32), (uint32_t)r[1],
+                             (uint32_t)(r[1] >> 32));
+    }
 }
 
 hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s) {
@@ -413,9 +478,9 @@ hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, 
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets (4 GiB)
     const uint32_t mlog = log2_pow2(m);
     switch (mode) {
-    case 0: return sort_impl<0>(data, m, seed, s, mlog);
-    case 1: return sort_impl<1>(data, m, seed, s, mlog);
-    default: return sort_impl<2>(data, m, seed, s, mlog);
+    case 0: return sort_impl<0>(data, m, seed, s, mlog, 0u);
+    case 1: return sort_impl<1>(data, m, seed, s, mlog, 0u);
+    default: return sort_impl<2>(data, m, seed, s, mlog, 0u);
     }
 }
 
@@ -425,10 +490,57 @@ hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t 
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
     const uint32_t slog = log2_pow2(seg);
     switch (mode) {
-    case 0: return sort_impl<0>(data, m, 0, s, slog);
-    case 1: return sort_impl<1>(data, m, 0, s, slog);
-    default: return sort_impl<2>(data, m, 0, s, slog);
+    case 0: return sort_impl<0>(data, m, 0, s, slog, 0u);
+    case 1: return sort_impl<1>(data, m, 0, s, slog, 0u);
+    default: return sort_impl<2>(data, m, 0, s, slog, 0u);
     }
+}
+
+// ---------------------------------------------- position-range pieces -----
+// One range of an M-record network split into M/m ranges of m records (one per GPU,
+// SURVEY §8e Option B): the caller runs sort_range on every range, then for each
+// stage ilog > log2 m the exchange steps j >= m (bitonic_exchange with the partner
+// range pbase ^ j) and merge_range.  Together: the reference network, step for step.
+hipError_t bitonic_sort_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                              uint32_t pbase, hipStream_t s) {
+    if (m < 2) return hipSuccess;
+    if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
+    const uint32_t mlog = log2_pow2(m);
+    switch (mode) {
+    case 0: return sort_impl<0>(data, m, seed, s, mlog, pbase);
+    case 1: return sort_impl<1>(data, m, seed, s, mlog, pbase);
+    default: return sort_impl<2>(data, m, seed, s, mlog, pbase);
+    }
+}
+
+hipError_t bitonic_merge_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                               uint32_t ilog, uint32_t pbase, hipStream_t s) {
+    if (m < 2) return hipSuccess;
+    if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
+    switch (mode) {
+    case 0: return merge_impl<0>(data, m, seed, s, ilog, pbase);
+    case 1: return merge_impl<1>(data, m, seed, s, ilog, pbase);
+    default: return merge_impl<2>(data, m, seed, s, ilog, pbase);
+    }
+}
+
+hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, uint32_t pos_mine,
+                            uint32_t pos_theirs, uint32_t mode, uint32_t seed, uint32_t ilog,
+                            uint32_t jlog, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    if (m & 1) return hipErrorInvalidValue;  // 16-B pairs of records
+    const size_t m2 = m / 2;
+    size_t blocks = (m2 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    const uint32_t lower = pos_mine < pos_theirs;
+    const uint32_t pos_lo = lower ? pos_mine : pos_theirs;
+    const uint32_t key = mode == 2 ? shuffle_step_key(seed, ilog, jlog) : 0u;
+#define BX_GO(MD)                                                                                  \
+    hipLaunchKernelGGL((bitonic_exchange_kernel<MD>), dim3((unsigned)blocks), dim3(256), 0, s,     \
+                       (uint4 *)mine, (const uint4 *)theirs, m2, pos_lo, lower, ilog, key)
+    if (mode == 0) BX_GO(0); else if (mode == 1) BX_GO(1); else BX_GO(2);
+#undef BX_GO
+    return hipGetLastError();
 }
 
 }  // namespace fltee

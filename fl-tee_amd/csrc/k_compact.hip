@@ -180,11 +180,14 @@ static uint32_t bitlen(uint64_t x) {
 }
 
 // src holds the folded array (positions [0, L) meaningful); tmp is scratch of L
-// records.  Both are clobbered.
-hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
-                                  float *out, bool accumulate, hipStream_t s) {
+// records.  Both are clobbered.  max_shift bounds every selected record's shift
+// c = p - idx (L - d for a whole folded array: c counts the unselected records in
+// front of p); it sets the number of levels, bitlen(max_shift).
+static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t d,
+                                 size_t max_shift, float coef, float *out, bool accumulate,
+                                 hipStream_t s) {
     if (d == 0) return hipSuccess;
-    const uint32_t nlev = L > d ? bitlen(L - d) : 0;
+    const uint32_t nlev = bitlen(max_shift);
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
     if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets
     const bool small = g_compact_variant == 1;
@@ -227,6 +230,43 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
         j0 += G;
     }
     return hipSuccess;
+}
+
+hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
+                                  float *out, bool accumulate, hipStream_t s) {
+    return compact_levels(src, tmp, L, d, L > d ? L - d : 0, coef, out, accumulate, s);
+}
+
+// ------------------------------------------------ one range of the array ---
+// Position-sharded `advanced` (SURVEY §8e Option B): after the fold, one GPU holds a
+// range of c folded records whose run representatives are some indices in [0, d),
+// each at most once, in ascending order.  buf = d unselected entries (u32::MAX, +0.0)
+// followed by the range: every representative then sits at a position p >= d > idx,
+// so the same left-moving network brings each to position idx — fixed addresses,
+// no data-dependent offset (the range's first index is never used).  out[i] gets
+// val * coef where this range holds index i and +0.0 elsewhere; the ranges' outputs
+// are then summed (RCCL reduce): exactly one range holds each index, so the sum is
+// that value, bit for bit (x + 0.0 == x: a run sum includes the +0.0 initial entry
+// and is never -0.0).
+__global__ void offset_copy_kernel(const uint64_t *__restrict__ chunk, size_t c, size_t d,
+                                   uint64_t *__restrict__ buf) {
+    const size_t L = d + c;
+    for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < L; p += (size_t)gridDim.x * 256)
+        buf[p] = p < d ? CP_DUMMY : chunk[p - d];
+}
+
+hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint64_t *buf,
+                                 uint64_t *tmp, float coef, float *out, hipStream_t s) {
+    if (d == 0) return hipSuccess;
+    const size_t L = d + c;
+    if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;
+    size_t blocks = (L + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(offset_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, chunk, c, d,
+                       buf);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return compact_levels(buf, tmp, L, d, L - 1, coef, out, false, s);
 }
 
 }  // namespace fltee

@@ -32,24 +32,33 @@
 
 namespace fltee {
 
+// dst[x] = entry pbase + x of the padded array; rec[x] is the record at position
+// pbase + x (read only where pbase + x < nrec).  pbase = 0: the whole array.
 __global__ void advanced_init_kernel(const uint64_t *__restrict__ rec, size_t nrec, size_t d,
-                                     size_t m, uint64_t *__restrict__ dst) {
-    for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (size_t)gridDim.x * 256) {
+                                     size_t pbase, size_t m, uint64_t *__restrict__ dst) {
+    for (size_t x = (size_t)blockIdx.x * 256 + threadIdx.x; x < m; x += (size_t)gridDim.x * 256) {
+        const size_t p = pbase + x;
         uint64_t v;
-        if (p < nrec) v = rec[p];
+        if (p < nrec) v = rec[x];
         else if (p < nrec + d) v = (uint64_t)(uint32_t)(p - nrec);  // (i, +0.0)
         else v = (uint64_t)0xFFFFFFFFu;                               // (u32::MAX, +0.0)
-        dst[p] = v;
+        dst[x] = v;
     }
+}
+
+hipError_t launch_advanced_init_range(const void *rec, size_t nrec, size_t d, size_t pbase,
+                                      size_t m, uint64_t *dst, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    size_t blocks = (m + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(advanced_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint64_t *)rec, nrec, d, pbase, m, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *dst,
                                 hipStream_t s) {
-    size_t blocks = (m + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(advanced_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const uint64_t *)rec, nrec, d, m, dst);
-    return hipGetLastError();
+    return launch_advanced_init_range(rec, nrec, d, 0, m, dst, s);
 }
 
 constexpr uint32_t FS_W = 16;    // records per window (one 128-B line)
@@ -61,20 +70,28 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// One wave per block; lane l of wave w owns positions [a, a + C), a = (w*64 + l)*C.
+// One wave per block; lane l of wave w owns positions [a, a + C), a = origin + (w*64 + l)*C,
+// up to `end`.  Positions are local to src/dst (length m); pbase + position is the
+// global position, which decides fold_len and the dummies' idx.  Range mode (one
+// GPU's part of a position-sharded array, SURVEY §8e Option B): [0, origin) holds
+// >= Hr records of context from the previous range, and src[end] is the next
+// range's first record (or end + pbase >= fold_len).
 __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restrict__ src,
                                                          uint64_t *__restrict__ dst, long long m,
-                                                         long long fold_len, uint32_t Hr,
-                                                         uint32_t C, uint32_t *status) {
+                                                         long long origin, long long end,
+                                                         long long pbase, long long fold_len,
+                                                         uint32_t Hr, uint32_t C,
+                                                         uint32_t *status) {
     __shared__ uint64_t win[2][64 * FS_ROW];
     const uint32_t l = threadIdx.x;
-    const long long wave0 = (long long)blockIdx.x * 64 * C;  // first position of lane 0
+    const long long wave0 = origin + (long long)blockIdx.x * 64 * C;  // first position of lane 0
     const long long a = wave0 + (long long)l * C;
     const uint32_t nstage = (Hr + C + FS_W) / FS_W;
     const uint32_t hw = Hr / FS_W;  // stage s holds window u = s - hw of the chunk
 
     // carry check (see header): only the first owned position consumes the carry
-    if (a < fold_len && a - (long long)Hr - 1 >= 0 && a < m) {
+    if (a < end && a + pbase < fold_len && a - (long long)Hr - 1 >= 0 &&
+        a + pbase - (long long)Hr - 1 >= 0) {
         const uint32_t k1 = rec_idx(src[a - 1]);
         if (rec_idx(src[a - Hr - 1]) == k1 && rec_idx(src[a]) == k1)
             atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
@@ -118,15 +135,16 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 #pragma unroll
         for (uint32_t t = 0; t < FS_W; ++t) {
             const long long q = q0 + t;  // this step reads position q, emits position q - 1
+            const long long qg = q + pbase;
             const uint32_t ci = rec_idx(r[t]);
             const bool eq = started && ci == pre_idx;
             const uint64_t emit =
-                (q - 1 >= fold_len) ? prev
-                : (q < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(q - 1))  // (MAX-p, +0.0)
-                                       : make_rec(pre_idx, pre_val);
+                (qg - 1 >= fold_len) ? prev
+                : (qg < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
+                                        : make_rec(pre_idx, pre_val);
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
-            if (q >= 0) {
+            if (q >= 0 && qg >= 0) {
                 pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
                 pre_idx = ci;
                 started = true;
@@ -141,7 +159,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             for (int i = 0; i < 8; ++i) {
                 const uint32_t w = (l >> 3) + 8 * i;
                 const long long g = wave0 + (long long)w * C + u * FS_W + part;
-                if (g < m) {
+                if (g < end) {
                     const uint64_t x0 = old[w * FS_ROW + part], x1 = old[w * FS_ROW + part + 1];
                     const fs_u32x4 v = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1,
                                         (uint32_t)(x1 >> 32)};
@@ -153,22 +171,33 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     }
 }
 
+size_t fold_context(size_t halo) { return (halo + FS_W - 1) / FS_W * FS_W; }
+
+hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
+                             size_t end, long long pbase, size_t fold_len, size_t halo,
+                             uint32_t *status, hipStream_t s) {
+    const size_t Hr = fold_context(halo);
+    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
+    if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
+    const size_t span = end - origin;
+    size_t C = 64;
+    while (C < Hr) C <<= 1;
+    while (C > 64 && span / (64 * C) < 1024) C >>= 1;  // keep >= ~1024 waves when halo allows
+    const size_t lanes = (span + C - 1) / C;
+    const size_t blocks = (lanes + 63) / 64;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fold_stream_kernel, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
+                       (long long)m, (long long)origin, (long long)end, pbase,
+                       (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
+    return hipGetLastError();
+}
+
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
                        uint32_t *status, hipStream_t s) {
     if (m == 1)  // nothing to fold: position 0 receives itself (:102-103)
         return hipMemcpyAsync(dst, src, 8, hipMemcpyDeviceToDevice, s);
     if (m == 0 || (m & 1)) return hipErrorInvalidValue;  // m = next_pow2: 16-B windows
-    const size_t Hr = (halo + FS_W - 1) / FS_W * FS_W;
-    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
-    size_t C = 64;
-    while (C < Hr) C <<= 1;
-    while (C > 64 && m / (64 * C) < 1024) C >>= 1;  // keep >= ~1024 waves when halo allows
-    const size_t lanes = (m + C - 1) / C;
-    const size_t blocks = (lanes + 63) / 64;
-    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(fold_stream_kernel, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
-                       (long long)m, (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
-    return hipGetLastError();
+    return launch_fold_range(src, dst, m, 0, m, 0, fold_len, halo, status, s);
 }
 
 template <bool ACC>

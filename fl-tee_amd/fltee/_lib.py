@@ -75,6 +75,13 @@ SIGNATURES = {
     "fltee_client_serialize_dense_device": (_U32, [_P, _S, _S, _P, _P]),
     "fltee_client_clip_device": (_U32, [_P, _S, _S, _F, _P]),
     "fltee_encrypt_device": (_U32, [_P, _S, _P, _S, _P, _P]),
+    "fltee_advanced_init_range_device": (_U32, [_P, _S, _S, _S, _S, _P, _P]),
+    "fltee_bitonic_range_sort_device": (_U32, [_P, _S, _S, _U32, _U32, _P]),
+    "fltee_bitonic_range_merge_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _P]),
+    "fltee_bitonic_range_exchange_device": (_U32, [_P, _P, _S, _S, _S, _U32, _U32, _U32, _P]),
+    "fltee_fold_context": (_S, [_S]),
+    "fltee_fold_range_device": (_U32, [_P, _P, _S, _S, _S, ctypes.c_int64, _S, _S, _P, _P]),
+    "fltee_compact_range_device": (_U32, [_P, _S, _S, _P, _P, _F, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_version": (ctypes.c_char_p, []),
 }

@@ -130,3 +130,61 @@ def dp_noise(out, sigma, clipping, n, seed=0, stream=None):
     _check(L.lib().fltee_dp_noise_device(_ptr(out), out.numel(), sigma, clipping, n, seed,
                                          _stream(stream)), "fltee_dp_noise_device")
     return out
+
+
+# ---- position-range pieces of `advanced` (multi-GPU Option B, fltee/parallel.py) ----
+def advanced_init_range(records, nrec, d, pos_base, m, out=None, stream=None):
+    """Entries pos_base..pos_base+m-1 of advanced's padded array (advanced.rs:116-142);
+    records[x] is the record at position pos_base + x (read where < nrec)."""
+    if out is None:
+        out = torch.empty(m, dtype=torch.int64, device=records.device)
+    _check(L.lib().fltee_advanced_init_range_device(_ptr(records), nrec, d, pos_base, m, _ptr(out),
+                                                    _stream(stream)),
+           "fltee_advanced_init_range_device")
+    return out
+
+
+def bitonic_range_sort(records, pos_base, mode=0, seed=0, stream=None):
+    _check(L.lib().fltee_bitonic_range_sort_device(_ptr(records), records.numel(), pos_base, mode,
+                                                   seed, _stream(stream)),
+           "fltee_bitonic_range_sort_device")
+    return records
+
+
+def bitonic_range_merge(records, pos_base, stage_log, mode=0, seed=0, stream=None):
+    _check(L.lib().fltee_bitonic_range_merge_device(_ptr(records), records.numel(), pos_base, mode,
+                                                    seed, stage_log, _stream(stream)),
+           "fltee_bitonic_range_merge_device")
+    return records
+
+
+def bitonic_range_exchange(mine, theirs, pos_mine, pos_theirs, stage_log, mode=0, seed=0,
+                           stream=None):
+    assert theirs.numel() == mine.numel()
+    _check(L.lib().fltee_bitonic_range_exchange_device(_ptr(mine), _ptr(theirs), mine.numel(),
+                                                       pos_mine, pos_theirs, mode, seed, stage_log,
+                                                       _stream(stream)),
+           "fltee_bitonic_range_exchange_device")
+    return mine
+
+
+def fold_context(halo):
+    return L.lib().fltee_fold_context(halo)
+
+
+def fold_range(src, dst, origin, end, pos_base, fold_len, halo, status_word, stream=None):
+    _check(L.lib().fltee_fold_range_device(_ptr(src), _ptr(dst), src.numel(), origin, end, pos_base,
+                                           fold_len, halo, _ptr(status_word), _stream(stream)),
+           "fltee_fold_range_device")
+    return dst
+
+
+def compact_range(chunk, d, coef, buf, tmp, out=None, stream=None):
+    if out is None:
+        out = torch.empty(d, dtype=torch.float32, device=chunk.device)
+    c = chunk.numel()
+    assert buf.numel() >= d + c and tmp.numel() >= d + c
+    _check(L.lib().fltee_compact_range_device(_ptr(chunk), c, d, _ptr(buf), _ptr(tmp), coef,
+                                              _ptr(out), _stream(stream)),
+           "fltee_compact_range_device")
+    return out

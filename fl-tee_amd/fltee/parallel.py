@@ -15,10 +15,21 @@ two partitionings the path admits:
   (fltee_sum_rows_device), scales by 1f32/n and adds DP noise.  With equal shards
   this is bit-identical to alg 6 with batch = n / world.
 
+* Position-range sharding (advanced, Option B = the north star's "parameter-index
+  range" sharding, configs[4]): `advanced`'s padded array of M entries is split into
+  `world` contiguous ranges, one per GPU.  The bitonic network runs distributed — the
+  steps with j >= M/world are pairwise exchanges of whole ranges with the partner
+  GPU r ^ (j / (M/world)) — so after the sort GPU r holds an index range.  The fold
+  takes one halo exchange with the neighbours; each GPU compacts its run
+  representatives to their indices and ONE RCCL reduce (sum) over xGMI assembles the
+  aggregate on the root.  Same network, same fold: bit-identical to single-GPU
+  `advanced`, and every transfer has a fixed size (oblivious).
+
 Collectives go through torch.distributed ("nccl" = RCCL on ROCm; "gloo" in the CPU
 tests).  The per-rank compute and the root combine are injectable so the CPU tests
 can stand the oracle in for the kernels.
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -101,4 +112,190 @@ def client_sharded_advanced(local_records, n_local, k, d, n_total, world, rank, 
     if dp is not None:
         from . import device as D
         D.dp_noise(out, dp["sigma"], dp["clipping"], n_total, dp.get("seed", 0))
+    return out
+
+
+# ------------------------------------------------ Option B: position ranges ----
+PAD_RECORD = 0xFFFFFFFF  # (u32::MAX, +0.0) as an int64 record (advanced.rs:133-142)
+
+
+class DeviceRangeOps:
+    """The HIP range pieces (include/fltee_agg.h, fltee.device) as the per-range steps
+    of index_sharded_advanced; scratch buffers are kept between calls."""
+
+    def __init__(self):
+        from . import device as D
+        self.D = D
+        self._scratch = {}
+
+    def _buf(self, name, n, dtype, device):
+        t = self._scratch.get(name)
+        if t is None or t.numel() < n or t.device != device:
+            t = torch.empty(n, dtype=dtype, device=device)
+            self._scratch[name] = t
+        return t[:n]
+
+    def pads(self, n, like):
+        return torch.full((n,), PAD_RECORD, dtype=torch.int64, device=like.device)
+
+    def fold_context(self, halo):
+        return self.D.fold_context(halo)
+
+    def sort(self, x, pos):
+        self.D.bitonic_range_sort(x, pos)
+
+    def merge(self, x, pos, stage_log):
+        self.D.bitonic_range_merge(x, pos, stage_log)
+
+    def exchange(self, x, theirs, pos, pos_theirs, stage_log):
+        self.D.bitonic_range_exchange(x, theirs, pos, pos_theirs, stage_log)
+
+    def fold(self, buf, origin, end, pos_base, fold_len, halo, key=0):
+        dst = self._buf(("fold", key), buf.numel(), torch.int64, buf.device)
+        st = self._buf(("st", key), 1, torch.int32, buf.device)
+        st.zero_()
+        self.D.fold_range(buf, dst, origin, end, pos_base, fold_len, halo, st)
+        return dst[origin:end], st
+
+    def ok(self, statuses):
+        return all(int(s.item()) == 0 for s in statuses)
+
+    def compact(self, chunk, d, key=0):
+        n = chunk.numel() + d
+        buf = self._buf(("cbuf", key), n, torch.int64, chunk.device)
+        tmp = self._buf(("ctmp", key), n, torch.int64, chunk.device)
+        return self.D.compact_range(chunk, d, 1.0, buf, tmp)
+
+    def finish(self, out, coef):
+        return self.D.sum_rows(out.view(1, -1), coef)
+
+    def dp(self, out, sigma, clipping, n, seed):
+        self.D.dp_noise(out, sigma, clipping, n, seed)
+
+
+class VirtualRanks:
+    """Every range lives in this process (the 1-GPU parity tests): exchanges are copies."""
+
+    def __init__(self, world):
+        self.world = world
+
+    def swap(self, chunks, partner):
+        return {r: chunks[partner(r)].clone() for r in chunks}
+
+    def neighbours(self, chunks, h, t, pads):
+        w = self.world
+        prev = {r: chunks[r - 1][-h:].clone() if r > 0 else pads(h, chunks[r]) for r in chunks}
+        nxt = {r: chunks[r + 1][:t].clone() if r < w - 1 else pads(t, chunks[r]) for r in chunks}
+        return prev, nxt
+
+    def all_true(self, flag):
+        return flag
+
+    def reduce(self, outs, root):
+        out = outs[0].clone()
+        for r in range(1, self.world):
+            out += outs[r]
+        return out
+
+
+class DistRanks:
+    """One range per process over torch.distributed (RCCL on the GPUs, gloo on CPU)."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def _run(ops):
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+    def swap(self, chunks, partner):
+        x = chunks[self.rank]
+        theirs = torch.empty_like(x)
+        p = partner(self.rank)
+        self._run([dist.P2POp(dist.isend, x, p), dist.P2POp(dist.irecv, theirs, p)])
+        return {self.rank: theirs}
+
+    def neighbours(self, chunks, h, t, pads):
+        r, w, x = self.rank, self.world, chunks[self.rank]
+        prev = torch.empty(h, dtype=x.dtype, device=x.device) if r > 0 else pads(h, x)
+        nxt = torch.empty(t, dtype=x.dtype, device=x.device) if r < w - 1 else pads(t, x)
+        ops = []
+        if r > 0:
+            ops += [dist.P2POp(dist.isend, x[:t].contiguous(), r - 1),
+                    dist.P2POp(dist.irecv, prev, r - 1)]
+        if r < w - 1:
+            ops += [dist.P2POp(dist.isend, x[-h:].contiguous(), r + 1),
+                    dist.P2POp(dist.irecv, nxt, r + 1)]
+        self._run(ops)
+        return {r: prev}, {r: nxt}
+
+    def all_true(self, flag):
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def reduce(self, outs, root):
+        out = outs[self.rank]
+        dist.reduce(out, dst=root, op=dist.ReduceOp.SUM)
+        return out if self.rank == root else None
+
+
+def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None, halo=None,
+                           root=0, dp=None):
+    """Option B: `advanced` over the padded array of M = next_pow2(n_total*k + d)
+    entries split into `world` ranges of C = M / world.  `chunks` maps a range index r
+    to its C entries (positions [r*C, (r+1)*C), built by fltee_advanced_init_range);
+    one entry per process under DistRanks, all of them under VirtualRanks.  The
+    chunks are sorted in place.  Returns the averaged f32[d] on the root (None
+    elsewhere); dp = dict(sigma, clipping, seed) adds the noise there (lib.rs:399-408).
+
+    advanced.rs:39-113 step by step: the network (:147-176) = per-range stages up to
+    C, then per stage the exchange steps (j >= C, partner r ^ j/C) and the range's
+    own steps (j < C); the fold (:66-101) with fold_context(halo) records of the
+    previous range in front and the next range's first records behind; the second
+    sort's [0, d) prefix (:106-111, :32-34) = each range's compacted representatives,
+    summed over the ranges by one reduce, then x 1f32/n (common.rs:14-19)."""
+    assert world & (world - 1) == 0 and M % world == 0
+    ops = ops if ops is not None else DeviceRangeOps()
+    comm = comm if comm is not None else VirtualRanks(world)
+    C = M // world
+    clog, mlog = C.bit_length() - 1, M.bit_length() - 1
+    assert 1 << clog == C and 1 << mlog == M
+    for r, x in chunks.items():
+        ops.sort(x, r * C)
+    for stage in range(clog + 1, mlog + 1):
+        for j in range(stage - 1, clog - 1, -1):
+            bit = 1 << (j - clog)
+            theirs = comm.swap(chunks, lambda q: q ^ bit)
+            for r, x in chunks.items():
+                ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
+            del theirs
+        for r, x in chunks.items():
+            ops.merge(x, r * C, stage)
+    fold_len = n_total * k + d
+    h = n_total if halo is None else halo
+    while True:
+        H = ops.fold_context(h)
+        if H > C:
+            raise ValueError(f"fold context {H} exceeds the range size {C}")
+        prev, nxt = comm.neighbours(chunks, H, 16, ops.pads)
+        folded, statuses = {}, []
+        for r, x in chunks.items():
+            buf = torch.cat([prev[r], x, nxt[r]])
+            folded[r], st = ops.fold(buf, H, H + C, r * C - H, fold_len, h, key=r)
+            statuses.append(st)
+        if comm.all_true(ops.ok(statuses)):
+            break
+        h = h * 4 + 16  # a run longer than the halo (a client repeated an index)
+    outs = {r: ops.compact(f, d, key=r) for r, f in folded.items()}
+    out = comm.reduce(outs, root)
+    if out is None:
+        return None
+    coef = float(np.float32(1.0) / np.float32(n_total))
+    out = ops.finish(out, coef)
+    if dp is not None:
+        ops.dp(out, dp["sigma"], dp["clipping"], n_total, dp.get("seed", 0))
     return out

@@ -214,6 +214,52 @@ fltee_status_t fltee_fold_device(const void *d_src, void *d_dst, size_t m, size_
 fltee_status_t fltee_laplace_r_device(size_t d, size_t k, size_t n, uint64_t seed, uint32_t *d_r,
                                       float *T_out, void *stream);
 
+/* ---- position-range pieces of `advanced` (multi-GPU, SURVEY §8e Option B) --
+ * The padded array of advanced.rs:116-142 (M = 2^m entries) is split into W
+ * contiguous ranges of m = M/W records, one per GPU; range r holds global
+ * positions [r*m, (r+1)*m).  Run on every range, in this order, these pieces are
+ * the reference's network and fold step for step (fl-tee_amd/fltee/parallel.py
+ * drives them over RCCL):
+ *   init_range -> range_sort -> for each stage 2^s > m: (range_exchange with the
+ *   partner range for every step 2^j >= m) then range_merge -> fold_range ->
+ *   compact_range -> sum of the W outputs (RCCL reduce) on the root.          */
+/* entries pos_base .. pos_base+m-1 of records ++ (i, 0.0) for i < d ++ (u32::MAX,
+ * 0.0) pads (advanced.rs:116-142); d_records holds the records at positions
+ * pos_base.. (read where position < nrec). */
+fltee_status_t fltee_advanced_init_range_device(const void *d_records, size_t nrec, size_t d,
+                                                size_t pos_base, size_t m, void *d_dst,
+                                                void *stream);
+/* stages 2 .. m of the bitonic network (advanced.rs:147-176) on one range; the
+ * direction of every compare-exchange comes from its GLOBAL position. */
+fltee_status_t fltee_bitonic_range_sort_device(void *d_records, size_t m, size_t pos_base,
+                                               uint32_t mode, uint32_t seed, void *stream);
+/* the steps j = m/2 .. 1 of stage 2^stage_log (> m) on one range. */
+fltee_status_t fltee_bitonic_range_merge_device(void *d_records, size_t m, size_t pos_base,
+                                                uint32_t mode, uint32_t seed, uint32_t stage_log,
+                                                void *stream);
+/* the step j = |pos_mine - pos_theirs| (>= m, a power of two) of stage 2^stage_log
+ * between this range and a copy of its partner's: d_mine takes the partner's
+ * record wherever that compare-exchange swaps. */
+fltee_status_t fltee_bitonic_range_exchange_device(void *d_mine, const void *d_theirs, size_t m,
+                                                   size_t pos_mine, size_t pos_theirs,
+                                                   uint32_t mode, uint32_t seed,
+                                                   uint32_t stage_log, void *stream);
+/* records of context the fold needs in front of a range: halo rounded up to 16. */
+size_t fltee_fold_context(size_t halo);
+/* advanced.rs:66-101 on [origin, end) of d_src (length m, global position =
+ * pos_base + local): [0, origin) holds >= fltee_fold_context(halo) records of the
+ * previous range, d_src[end] the next range's first record (unless end + pos_base
+ * >= fold_len).  Writes d_dst[origin, end). */
+fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m, size_t origin,
+                                       size_t end, int64_t pos_base, size_t fold_len, size_t halo,
+                                       uint32_t *d_status, void *stream);
+/* one folded range (c records) -> d_out[d]: val * coef at each run representative's
+ * index i < d held by this range, +0.0 elsewhere (oblivious compaction; scratch
+ * d_buf, d_tmp of d + c records each).  The sum of every range's d_out is the
+ * aggregate, bit for bit. */
+fltee_status_t fltee_compact_range_device(const void *d_chunk, size_t c, size_t d, void *d_buf,
+                                          void *d_tmp, float coef, float *d_out, void *stream);
+
 /* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
 void fltee_debug_set_seed(uint64_t seed);
 /* Library build/version string. */

@@ -1,0 +1,103 @@
+"""GPU parity of position-range sharded `advanced` (SURVEY §8e Option B): the HIP
+range pieces driven by fltee.parallel.index_sharded_advanced with every range on one
+GPU (VirtualRanks: the exchanges are device copies) must reproduce the oracle's
+single-process network permutation and `advanced` output bit for bit."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    from fltee import device as D
+    torch.cuda.init()
+    return D
+
+
+def case(seed, n, d, k, idx_hi=None):
+    rng = np.random.default_rng(seed)
+    if idx_hi is None:
+        idx = np.concatenate([rng.choice(d, k, replace=False) for _ in range(n)]).astype(np.uint32)
+    else:
+        idx = rng.integers(0, idx_hi, n * k).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    return idx, val
+
+
+def init_chunks(dev, rec, nrec, d, world, M):
+    C = M // world
+    return {r: dev.advanced_init_range(rec[r * C:] if r * C < nrec else rec, nrec, d, r * C, C)
+            for r in range(world)}
+
+
+@pytest.mark.parametrize("world,m", [(2, 1 << 10), (4, 1 << 15), (8, 1 << 20), (8, 512), (2, 1 << 22)])
+def test_distributed_network_equals_single_sort(dev, oracle, world, m):
+    """Range sorts + exchanges + range merges == the reference network on all M."""
+    import torch
+
+    from fltee.parallel import DeviceRangeOps, VirtualRanks
+    rng = np.random.default_rng(m + world)
+    idx = rng.integers(0, max(2, m // 8), m).astype(np.uint32)   # heavy ties
+    val = np.arange(m, dtype=np.float32)                          # identity tracking
+    full = torch.from_numpy(dev.pack_records(idx, val)).cuda()
+    C = m // world
+    chunks = {r: full[r * C:(r + 1) * C].clone() for r in range(world)}
+    ops, comm = DeviceRangeOps(), VirtualRanks(world)
+    clog, mlog = C.bit_length() - 1, m.bit_length() - 1
+    for r, x in chunks.items():
+        ops.sort(x, r * C)
+    for stage in range(clog + 1, mlog + 1):
+        for j in range(stage - 1, clog - 1, -1):
+            bit = 1 << (j - clog)
+            theirs = comm.swap(chunks, lambda q: q ^ bit)
+            for r, x in chunks.items():
+                ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
+        for r, x in chunks.items():
+            ops.merge(x, r * C, stage)
+    got = torch.cat([chunks[r] for r in range(world)]).cpu().numpy()
+    gi, gv = dev.unpack_records(got)
+    ref = oracle.bitonic_sort(oracle.as_weights(idx, val))
+    assert np.array_equal(gi, ref["idx"]) and np.array_equal(gv.view(np.uint32), ref["val"].view(np.uint32))
+
+
+@pytest.mark.parametrize("world,n,d,k,idx_hi", [(2, 20, 3000, 400, None), (4, 20, 3000, 400, None),
+                                                (8, 4, 100, 50, None), (8, 100, 50890, 5089, None),
+                                                (2, 7, 3333, 1, None), (4, 20, 3000, 400, 64),
+                                                (4, 30, 2000, 300, 2100)])
+def test_index_sharded_advanced_bit_exact(dev, oracle, world, n, d, k, idx_hi):
+    """idx_hi = 64: runs far longer than n + 1 (the fold's halo retry); 2100 > d: indices
+    outside [0, d) fold into their own runs and never reach the output."""
+    import torch
+
+    from fltee.parallel import VirtualRanks, index_sharded_advanced
+    idx, val = case(world * 1000 + n + d, n, d, k, idx_hi)
+    rec = torch.from_numpy(dev.pack_records(idx, val)).cuda()
+    M = oracle.next_pow2(n * k + d)
+    chunks = init_chunks(dev, rec, n * k, d, world, M)
+    out = index_sharded_advanced(chunks, world, M, n, k, d, comm=VirtualRanks(world))
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0
+    got = out.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_index_sharded_matches_single_gpu_at_scale(dev):
+    """configs[2]-like shape at 2^21: sharded x4 == fltee_aggregate_device(advanced)."""
+    import torch
+
+    from fltee.parallel import VirtualRanks, index_sharded_advanced
+    n, d, k = 300, 50890, 5089
+    idx, val = case(5, n, d, k)
+    rec = torch.from_numpy(dev.pack_records(idx, val)).cuda()
+    single = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    M = 1 << (n * k + d - 1).bit_length()
+    out = index_sharded_advanced(init_chunks(dev, rec, n * k, d, 4, M), 4, M, n, k, d,
+                                 comm=VirtualRanks(4)).cpu().numpy()
+    assert np.array_equal(out.view(np.uint32), single.view(np.uint32))

@@ -104,3 +104,46 @@ def test_shard_ranges_cover():
             assert spans[0][0] == 0 and spans[-1][1] == total
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+# ---- position-range sharding (advanced, Option B): DistRanks over gloo ----
+def case_b():
+    rng = np.random.default_rng(7)
+    n, d, k = 6, 300, 40
+    idx = np.concatenate([rng.choice(d, k, replace=False) for _ in range(n)]).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    return n, d, k, idx, val
+
+
+def worker_b(rank, world, port, outdir):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "fl-tee_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    from range_ops_np import NumpyRangeOps, init_range
+
+    from fltee import parallel as P
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    n, d, k, idx, val = case_b()
+    M = 1 << (n * k + d - 1).bit_length()
+    C = M // world
+    chunks = {rank: init_range(idx, val, d, rank * C, C)}
+    out = P.index_sharded_advanced(chunks, world, M, n, k, d, ops=NumpyRangeOps(),
+                                   comm=P.DistRanks(rank, world))
+    if rank == 0:
+        np.save(os.path.join(outdir, "adv_b.npy"), out.numpy())
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_index_sharded_advanced_gloo(oracle, tmp_path, world):
+    mp.spawn(worker_b, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    n, d, k, idx, val = case_b()
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0
+    got = np.load(tmp_path / "adv_b.npy")
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

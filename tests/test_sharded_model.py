@@ -1,0 +1,33 @@
+"""Option B (position-range sharded `advanced`) on CPU: the driver in
+fltee.parallel with numpy stand-ins for the range pieces, every range in one process
+(VirtualRanks) — must equal the oracle's single-process `advanced` bit for bit."""
+import numpy as np
+import pytest
+
+from range_ops_np import NumpyRangeOps, init_range
+
+
+def case(seed, n, d, k, idx_hi=None):
+    rng = np.random.default_rng(seed)
+    if idx_hi is None:
+        idx = np.concatenate([rng.choice(d, k, replace=False) for _ in range(n)]).astype(np.uint32)
+    else:
+        idx = rng.integers(0, idx_hi, n * k).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    return idx, val
+
+
+@pytest.mark.parametrize("world,n,d,k,idx_hi", [(1, 5, 200, 30, None), (2, 5, 200, 30, None),
+                                                (4, 6, 300, 20, None), (8, 4, 100, 50, None),
+                                                (4, 10, 150, 40, 40), (2, 7, 333, 1, None)])
+def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi):
+    from fltee.parallel import VirtualRanks, index_sharded_advanced
+    idx, val = case(world * 100 + n, n, d, k, idx_hi)
+    M = oracle.next_pow2(n * k + d)
+    C = M // world
+    chunks = {r: init_range(idx, val, d, r * C, C) for r in range(world)}
+    out = index_sharded_advanced(chunks, world, M, n, k, d, ops=NumpyRangeOps(),
+                                 comm=VirtualRanks(world))
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0
+    assert np.array_equal(out.numpy().view(np.uint32), ref.view(np.uint32))
