@@ -152,6 +152,58 @@ def bench_c5_sharded(torch, D, dist, world, rank, device, steps, warmup):
                 unit="client-params/s", scaling="strong")
 
 
+def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
+    """configs[4] as BASELINE.json states it — "param-range sharded across 8 MI355X via
+    RCCL/xGMI" (SURVEY §8e Option B, strong scaling): `advanced`'s padded array of
+    M = 2^27 entries is split into `world` position ranges; the bitonic network runs
+    distributed (range sorts, then per stage the pairwise RCCL exchanges of whole
+    ranges with partner r ^ j/C and the range merges), one halo exchange feeds the
+    fold, each rank compacts its run representatives and one RCCL reduce assembles
+    the aggregate on rank 0 (fltee/parallel.py).  Rank r holds the records at
+    positions [r*C, (r+1)*C) (same synthetic shape as `c5`)."""
+    from fltee import parallel as P
+    w = WORKLOADS["c5"]
+    n, d, k = w["n"], w["d"], w["k"]
+    nrec = n * k
+    M = 1 << (nrec + d - 1).bit_length()
+    C = M // world
+    lo = rank * C
+    cnt = max(1, min(C, nrec - lo))
+    g = torch.Generator(device=device).manual_seed(6000 + rank)
+    p = lo + torch.arange(cnt, device=device, dtype=torch.int64)
+    off = torch.randint(0, d, (n,), generator=g, device=device)
+    idx = (off[torch.clamp(p // k, max=n - 1)] + p % k) % d
+    vals = torch.randn(cnt, generator=g, device=device) * 0.01
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).contiguous()
+    del p, idx, vals
+    chunk = torch.empty(C, dtype=torch.int64, device=device)
+    ops, comm = P.DeviceRangeOps(), P.DistRanks(rank, world)
+
+    def step():
+        D.advanced_init_range(rec, nrec, d, lo, C, out=chunk)
+        P.index_sharded_advanced({rank: chunk}, world, M, n, k, d, ops=ops, comm=comm)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    del rec, chunk, ops
+    wall = float(t[0]) / steps
+    return dict(desc=w["desc"] + f", position-range sharded x{world}: distributed bitonic "
+                "(RCCL pairwise range exchanges) + halo fold + one RCCL reduce",
+                alg="advanced", n=n, d=d, k=k, M=M, range_records=C, ms_per_step=wall * 1e3,
+                value=n * k / wall, unit="client-params/s", scaling="strong")
+
+
 def cpu_baseline_sample(d, n, seconds):
     """The oracle's `baseline` (baseline.rs o_update: one cmov RMW per 64-B line of the
     d-float output per record) on a bounded prefix of client 0's dense records,
@@ -330,8 +382,11 @@ def main():
     del recs, gathered
     sharded = None
     if world > 1 and not args.no_extra:
-        sharded = bench_c5_sharded(torch, D, dist, world, rank, device,
-                                   steps=max(3, args.steps // 10), warmup=1)
+        sharded = {"c5_sharded": bench_c5_sharded(torch, D, dist, world, rank, device,
+                                                  steps=max(3, args.steps // 10), warmup=1)}
+        if world & (world - 1) == 0:
+            sharded["c5_index_sharded"] = bench_c5_index_sharded(
+                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
 
     if rank == 0:
         line = {
@@ -365,7 +420,7 @@ def main():
                                    unit="client-params/s")
             line["extra"] = extra
         if sharded is not None:
-            line["extra"] = {"c5_sharded": sharded}
+            line["extra"] = sharded
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

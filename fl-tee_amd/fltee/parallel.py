@@ -206,15 +206,27 @@ class DistRanks:
 
     @staticmethod
     def _run(ops):
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        """ops: (send?, tensor, peer).  RCCL: one batched group; gloo (CPU tests, the
+        one-GPU rehearsal) moves host copies of device tensors."""
+        if not ops:
+            return
+        staged = dist.get_backend() == "gloo" and any(t.is_cuda for _, t, _ in ops)
+        p2p, back = [], []
+        for send, t, peer in ops:
+            h = t.cpu() if (staged and send) else (torch.empty(t.shape, dtype=t.dtype) if staged else t)
+            if staged and not send:
+                back.append((h, t))
+            p2p.append(dist.P2POp(dist.isend if send else dist.irecv, h, peer))
+        for req in dist.batch_isend_irecv(p2p):
+            req.wait()
+        for h, t in back:
+            t.copy_(h)
 
     def swap(self, chunks, partner):
         x = chunks[self.rank]
         theirs = torch.empty_like(x)
         p = partner(self.rank)
-        self._run([dist.P2POp(dist.isend, x, p), dist.P2POp(dist.irecv, theirs, p)])
+        self._run([(True, x, p), (False, theirs, p)])
         return {self.rank: theirs}
 
     def neighbours(self, chunks, h, t, pads):
@@ -223,11 +235,9 @@ class DistRanks:
         nxt = torch.empty(t, dtype=x.dtype, device=x.device) if r < w - 1 else pads(t, x)
         ops = []
         if r > 0:
-            ops += [dist.P2POp(dist.isend, x[:t].contiguous(), r - 1),
-                    dist.P2POp(dist.irecv, prev, r - 1)]
+            ops += [(True, x[:t].contiguous(), r - 1), (False, prev, r - 1)]
         if r < w - 1:
-            ops += [dist.P2POp(dist.isend, x[-h:].contiguous(), r + 1),
-                    dist.P2POp(dist.irecv, nxt, r + 1)]
+            ops += [(True, x[-h:].contiguous(), r + 1), (False, nxt, r + 1)]
         self._run(ops)
         return {r: prev}, {r: nxt}
 
@@ -239,7 +249,12 @@ class DistRanks:
 
     def reduce(self, outs, root):
         out = outs[self.rank]
-        dist.reduce(out, dst=root, op=dist.ReduceOp.SUM)
+        if dist.get_backend() == "gloo" and out.is_cuda:
+            h = out.cpu()
+            dist.reduce(h, dst=root, op=dist.ReduceOp.SUM)
+            out.copy_(h)
+        else:
+            dist.reduce(out, dst=root, op=dist.ReduceOp.SUM)
         return out if self.rank == root else None
 
 
