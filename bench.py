@@ -361,16 +361,25 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    region = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    region[0].record(stream)
     for i in range(args.steps):
-        step(args.warmup + i, kev[i])
+        # N = 1: the K launches run back to back and one event pair brackets them all
+        # (per-launch event pairs would add their own gaps); N > 1: per-step pairs, since
+        # the stream also waits for the gathers between the kernels
+        step(args.warmup + i, kev[i] if world > 1 else None)
+    region[1].record(stream)
     drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern = sum(a.elapsed_time(b) for a, b in kev) / args.steps / 1e3
+    if world > 1:
+        kern = sum(a.elapsed_time(b) for a, b in kev) / args.steps / 1e3
+    else:
+        kern = region[0].elapsed_time(region[1]) / args.steps / 1e3
     if world > 1:
         t = torch.tensor([elapsed, kern], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -44,26 +44,26 @@ static __device__ __forceinline__ float4 ld_nt(const float4 *p) {
 
 // ---------------------------------------------------------------- dense ----
 // rec viewed as uint4 = two records {idx0, val0, idx1, val1}; row stride d2 = d/2.
-// A block covers V*256 consecutive uint4 columns; lane t owns columns
-// base + t + v*256 (v < V), so every load instruction of a wave is 1 KB contiguous.
+// A block covers V*NTH consecutive uint4 columns; lane t owns columns
+// base + t + v*NTH (v < V), so every load instruction of a wave is 1 KB contiguous.
 template <typename T4>
 static __device__ __forceinline__ uint4 ld4(const uint4 *p, bool nt) {
     return nt ? ld_nt(p) : *p;
 }
 
-template <int V, int U, bool CLIP, bool ACC, bool NT>
-__global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
+template <int V, int U, bool CLIP, bool ACC, bool NT, int NTH = 256>
+__global__ __launch_bounds__(NTH) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
                                                           uint32_t n, float coef,
                                                           float *__restrict__ out,
                                                           const float *__restrict__ ccoef,
                                                           uint32_t *status) {
-    const size_t base = (size_t)blockIdx.x * (256 * V) + threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * (NTH * V) + threadIdx.x;
     float acc[2 * V];
     bool live[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
         acc[2 * v] = acc[2 * v + 1] = 0.0f;
-        live[v] = base + (size_t)v * 256 < d2;
+        live[v] = base + (size_t)v * NTH < d2;
     }
     if (!live[0]) return;
     uint32_t bad = 0;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restric
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[u][v] = ld4<uint4>(p + (size_t)(c + u) * d2 + v * 256, NT);
+                for (int v = 0; v < V; ++v) x[u][v] = ld4<uint4>(p + (size_t)(c + u) * d2 + v * NTH, NT);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const float cc = CLIP ? ccoef[c + u] : 1.0f;
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restric
                     if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
                     acc[2 * v] = __fadd_rn(acc[2 * v], a);
                     acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
-                    const uint32_t j = (uint32_t)(2 * (base + (size_t)v * 256));
+                    const uint32_t j = (uint32_t)(2 * (base + (size_t)v * NTH));
                     bad |= (x[u][v].x ^ j) | (x[u][v].z ^ (j + 1));
                 }
             }
@@ -97,12 +97,12 @@ __global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restric
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             if (!live[v]) continue;
-            const uint4 x = ld4<uint4>(p + (size_t)c * d2 + v * 256, NT);
+            const uint4 x = ld4<uint4>(p + (size_t)c * d2 + v * NTH, NT);
             float a = __uint_as_float(x.y), b = __uint_as_float(x.w);
             if (CLIP) { a = __fmul_rn(a, cc); b = __fmul_rn(b, cc); }
             acc[2 * v] = __fadd_rn(acc[2 * v], a);
             acc[2 * v + 1] = __fadd_rn(acc[2 * v + 1], b);
-            const uint32_t j = (uint32_t)(2 * (base + (size_t)v * 256));
+            const uint32_t j = (uint32_t)(2 * (base + (size_t)v * NTH));
             bad |= (x.x ^ j) | (x.z ^ (j + 1));
         }
     }
@@ -112,12 +112,12 @@ __global__ __launch_bounds__(256) void dense_accumulate_v(const uint4 *__restric
         if (!live[v]) continue;
         float2 r;
         if (ACC) {
-            const float2 prev = o[v * 256];
+            const float2 prev = o[v * NTH];
             r = make_float2(__fadd_rn(prev.x, acc[2 * v]), __fadd_rn(prev.y, acc[2 * v + 1]));
         } else {
             r = make_float2(__fmul_rn(acc[2 * v], coef), __fmul_rn(acc[2 * v + 1], coef));
         }
-        o[v * 256] = r;
+        o[v * NTH] = r;
     }
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
@@ -144,15 +144,56 @@ __global__ __launch_bounds__(256) void dense_accumulate_s(const uint2 *__restric
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
 
+// one record (8 B) per lane and client, U clients in flight (A/B variant)
+template <int U, bool CLIP, bool ACC>
+__global__ __launch_bounds__(256) void dense_accumulate_r(const uint2 *__restrict__ rec, size_t d,
+                                                          uint32_t n, float coef,
+                                                          float *__restrict__ out,
+                                                          const float *__restrict__ ccoef,
+                                                          uint32_t *status) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= d) return;
+    const uint2 *p = rec + j;
+    float acc = 0.0f;
+    uint32_t bad = 0, c = 0;
+    for (; c + U <= n; c += U) {
+        uint2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld_nt(p + (size_t)(c + u) * d);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float a = __uint_as_float(x[u].y);
+            if (CLIP) a = __fmul_rn(a, ccoef[c + u]);
+            acc = __fadd_rn(acc, a);
+            bad |= x[u].x ^ (uint32_t)j;
+        }
+    }
+    for (; c < n; ++c) {
+        const uint2 x = ld_nt(p + (size_t)c * d);
+        float a = __uint_as_float(x.y);
+        if (CLIP) a = __fmul_rn(a, ccoef[c]);
+        acc = __fadd_rn(acc, a);
+        bad |= x.x ^ (uint32_t)j;
+    }
+    out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+    if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
 // Tuning hook (fltee_debug_set_dense_variant): 0 is the shipped configuration.
 static int g_dense_variant = 0;
 
-template <int V, int U, bool CLIP, bool ACC, bool NT>
+template <int V, int U, bool CLIP, bool ACC, bool NT, int NTH = 256>
 static void launch_v(const void *rec, size_t n, size_t d2, float coef, float *out,
                      const float *ccoef, uint32_t *status, hipStream_t s) {
-    const unsigned blocks = (unsigned)((d2 + 256 * V - 1) / (256 * V));
-    hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC, NT>), dim3(blocks), dim3(256), 0, s,
+    const unsigned blocks = (unsigned)((d2 + NTH * V - 1) / (NTH * V));
+    hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC, NT, NTH>), dim3(blocks), dim3(NTH), 0, s,
                        (const uint4 *)rec, d2, (uint32_t)n, coef, out, ccoef, status);
+}
+template <int U, bool CLIP, bool ACC>
+static void launch_r(const void *rec, size_t n, size_t d, float coef, float *out,
+                     const float *ccoef, uint32_t *status, hipStream_t s) {
+    hipLaunchKernelGGL((dense_accumulate_r<U, CLIP, ACC>), dim3((unsigned)((d + 255) / 256)), dim3(256),
+                       0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
 }
 
 template <bool CLIP, bool ACC>
@@ -169,7 +210,14 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         case 5: launch_v<1, 16, CLIP, ACC, false>(rec, n, d2, coef, out, ccoef, status, s); break;
         case 6: launch_v<4, 4, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
         case 7: launch_v<4, 8, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
-        default: launch_v<1, 16, CLIP, ACC, true>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 9: launch_v<1, 16, CLIP, ACC, true, 128>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 10: launch_r<16, CLIP, ACC>(rec, n, d, coef, out, ccoef, status, s); break;
+        case 11: launch_r<32, CLIP, ACC>(rec, n, d, coef, out, ccoef, status, s); break;
+        case 12: launch_v<1, 16, CLIP, ACC, true, 64>(rec, n, d2, coef, out, ccoef, status, s); break;
+        case 13: launch_v<1, 16, CLIP, ACC, true, 256>(rec, n, d2, coef, out, ccoef, status, s); break;
+        // shipped: 512-lane blocks, 16 clients in flight, 16-B nontemporal loads
+        // (A/B, 100 x 1M: 122.3 us vs 124.2 us for 256-lane blocks; profiles/r01/dense_variants_ab2.jsonl)
+        default: launch_v<1, 16, CLIP, ACC, true, 512>(rec, n, d2, coef, out, ccoef, status, s); break;
         }
     } else {
         const unsigned blocks = (unsigned)((d + 255) / 256);

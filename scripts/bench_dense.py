@@ -12,8 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fl-tee_amd"))
 sys.path.insert(0, ROOT)
 
-VARIANTS = {0: "V1 U16 nt", 1: "V1 U8 nt", 2: "V1 U32 nt", 3: "V2 U8 nt", 4: "V2 U16 nt",
-            5: "V1 U16 plain", 6: "V4 U4 nt", 7: "V4 U8 nt"}
+VARIANTS = {0: "V1 U16 nt 512 lanes (shipped)", 1: "V1 U8 nt", 2: "V1 U32 nt", 3: "V2 U8 nt", 4: "V2 U16 nt",
+            5: "V1 U16 plain", 6: "V4 U4 nt", 7: "V4 U8 nt", 8: "= variant 0",
+            9: "V1 U16 nt 128 lanes", 10: "8 B/lane U16", 11: "8 B/lane U32", 12: "V1 U16 nt 64 lanes",
+            13: "V1 U16 nt 256 lanes (round-1 default)"}
 
 
 def main():
