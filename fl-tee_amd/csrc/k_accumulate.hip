@@ -427,33 +427,36 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restri
     if (__any(rep) && (threadIdx.x & 63) == 0) atomicOr(dup, 1u);
 }
 
-// Lane t owns outputs 4t..4t+3.  VEC: d % 4 == 0 (16-B rows).
-template <bool VEC, bool ACC>
+// One lane per output j: the n rows' slots j are read U at a time (wave-coalesced
+// 256-B loads) and added in client order.
+template <bool ACC, int U>
 __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restrict__ mat, size_t d,
                                                         uint32_t n, const uint2 *__restrict__ rec,
                                                         size_t nrec, const uint32_t *dup,
                                                         float coef, float *__restrict__ out) {
-    const size_t j0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    bool hit[4] = {false, false, false, false};
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    float acc = 0.0f;
+    bool hit = false;
     if (*dup == 0) {
-        if (j0 >= d) return;
-        for (uint32_t c = 0; c < n; ++c) {
-            uint32_t x[4];
-            const uint32_t *row = mat + (size_t)c * d + j0;
-            if (VEC) {
-                const uint4 v = ld_nt(reinterpret_cast<const uint4 *>(row));
-                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-            } else {
+        if (j >= d) return;
+        const uint32_t *col = mat + j;
+        uint32_t c = 0;
+        for (; c + U <= n; c += U) {
+            uint32_t x[U];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[i] = (j0 + i < d) ? row[i] : kEmptySlot;
-            }
+            for (int u = 0; u < U; ++u) x[u] = __builtin_nontemporal_load(col + (size_t)(c + u) * d);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const bool h = x[i] != kEmptySlot;
-                acc[i] = __fadd_rn(acc[i], h ? __uint_as_float(x[i]) : 0.0f);
-                hit[i] |= h;
+            for (int u = 0; u < U; ++u) {
+                const bool h = x[u] != kEmptySlot;
+                acc = __fadd_rn(acc, h ? __uint_as_float(x[u]) : 0.0f);
+                hit |= h;
             }
+        }
+        for (; c < n; ++c) {
+            const uint32_t x = col[(size_t)c * d];
+            const bool h = x != kEmptySlot;
+            acc = __fadd_rn(acc, h ? __uint_as_float(x) : 0.0f);
+            hit |= h;
         }
     } else {  // a client repeated an index: every record, in upload order
         __shared__ uint2 tile[SW_CHUNK];
@@ -464,25 +467,17 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
             __syncthreads();
             for (uint32_t q = 0; q < m; ++q) {
                 const uint2 r = tile[q];
-                const size_t delta = (size_t)r.x - j0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const bool h = delta == (size_t)i;
-                    acc[i] = __fadd_rn(acc[i], h ? __uint_as_float(r.y) : 0.0f);
-                    hit[i] |= h;
-                }
+                const bool h = r.x == j;
+                acc = __fadd_rn(acc, h ? __uint_as_float(r.y) : 0.0f);
+                hit |= h;
             }
         }
-        if (j0 >= d) return;
+        if (j >= d) return;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (j0 + i >= d) break;
-        if (ACC) {
-            if (hit[i]) out[j0 + i] = __fadd_rn(out[j0 + i], acc[i]);
-        } else {
-            out[j0 + i] = __fmul_rn(acc[i], coef);
-        }
+    if (ACC) {
+        if (hit) out[j] = __fadd_rn(out[j], acc);
+    } else {
+        out[j] = __fmul_rn(acc, coef);
     }
 }
 
@@ -499,18 +494,14 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
         hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, s,
                            (const uint2 *)rec, n, k, d, mat, dup, status);
     }
-    const unsigned blocks = (unsigned)((d + 1023) / 1024);
-    const bool vec = d % 4 == 0 && (uintptr_t)mat % 16 == 0;
+    const unsigned blocks = (unsigned)((d + 255) / 256);
     const size_t nrec = n * k;
-#define FLTEE_SRS(V, A)                                                                      \
-    hipLaunchKernelGGL((scatter_rows_sum<V, A>), dim3(blocks), dim3(256), 0, s, mat, d,     \
-                       (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out)
-    if (vec) {
-        if (accumulate) FLTEE_SRS(true, true); else FLTEE_SRS(true, false);
-    } else {
-        if (accumulate) FLTEE_SRS(false, true); else FLTEE_SRS(false, false);
-    }
-#undef FLTEE_SRS
+    if (accumulate)
+        hipLaunchKernelGGL((scatter_rows_sum<true, 16>), dim3(blocks), dim3(256), 0, s, mat, d,
+                           (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out);
+    else
+        hipLaunchKernelGGL((scatter_rows_sum<false, 16>), dim3(blocks), dim3(256), 0, s, mat, d,
+                           (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out);
     return hipGetLastError();
 }
 

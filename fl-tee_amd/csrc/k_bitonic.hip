@@ -290,6 +290,16 @@ static bool tile32() {
     }();
     return on;
 }
+// Smaller tiles until there are at least 2^mt of them (FLTEE_BITONIC_MINTILES_LOG,
+// default 8 = 256 tiles, one per CU; for A/B runs).
+static uint32_t min_tiles_log() {
+    static uint32_t t = [] {
+        const char *e = getenv("FLTEE_BITONIC_MINTILES_LOG");
+        int v = e ? atoi(e) : 8;
+        return (uint32_t)(v < 0 ? 0 : (v > 12 ? 12 : v));
+    }();
+    return t;
+}
 // Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
 // disables them, for A/B runs).
 static bool strided_passes() {
@@ -349,8 +359,9 @@ static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
     const uint32_t tmax = max_tile_log();
     uint32_t tlog = mlog < tmax ? mlog : tmax;
     if (tlog > slog) tlog = slog;
-    if (tlog == 14 && mlog - tlog < 8) tlog = 13;
-    while (tlog > 11 && tlog <= 13 && (mlog - tlog) < 8) --tlog;  // >= 256 tiles
+    const uint32_t mt = min_tiles_log();
+    if (tlog == 14 && mlog - tlog < mt) tlog = 13;
+    while (tlog > 11 && tlog <= 13 && (mlog - tlog) < mt) --tlog;  // >= 2^mt tiles
     c.tlog = tlog;
     if (tlog <= 6) return c;
     const uint32_t T = 1u << tlog;
