@@ -7,28 +7,37 @@ streaming read) + WRITE_SIZE (KB) x 1024.  Writes/updates profiles/traffic.json.
 import csv
 import json
 import os
-import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, counter, sub):
-    vals, kern = [], None
+COLS = ["Dispatch_Id", "Kernel", "Grid_Size", "Workgroup_Size", "VGPR_Count", "SGPR_Count",
+        "Counter_Name", "Counter_Value", "Start_Timestamp", "End_Timestamp"]
+
+
+def per_launch(path, counter, sub, out_path):
+    """Mean counter value per launch of the kernels matching sub; the matching rows are
+    written (trimmed to COLS) to out_path."""
+    vals, kern, rows = [], None, []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Counter_Name"] == counter and sub in row["Kernel"]:
+            name = row.get("Kernel", row.get("Kernel_Name"))
+            if row["Counter_Name"] == counter and sub in name:
                 vals.append(float(row["Counter_Value"]))
-                kern = row["Kernel"]
+                kern = name
+                rows.append({c: (name if c == "Kernel" else row.get(c, "")) for c in COLS})
+    with open(out_path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=COLS)
+        w.writeheader()
+        w.writerows(rows)
     return sum(vals) / len(vals), len(vals), kern
 
 
 def main():
     name, sub, fetch_csv, write_csv, out_f, out_w = sys.argv[1:7]
-    fkb, nf, kern = per_launch(fetch_csv, "FETCH_SIZE", sub)
-    wkb, nw, _ = per_launch(write_csv, "WRITE_SIZE", sub)
-    shutil.copy(fetch_csv, os.path.join(ROOT, out_f))
-    shutil.copy(write_csv, os.path.join(ROOT, out_w))
+    fkb, nf, kern = per_launch(fetch_csv, "FETCH_SIZE", sub, os.path.join(ROOT, out_f))
+    wkb, nw, _ = per_launch(write_csv, "WRITE_SIZE", sub, os.path.join(ROOT, out_w))
     path = os.path.join(ROOT, "profiles", "traffic.json")
     t = json.load(open(path)) if os.path.exists(path) else {}
     t[name] = dict(hbm_bytes_per_launch=fkb * 1024 * 2 + wkb * 1024, fetch_size_kb=fkb,
