@@ -152,12 +152,15 @@ def bench_c5_sharded(torch, D, dist, world, rank, device, steps, warmup):
                 unit="client-params/s", scaling="strong")
 
 
-def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
+def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup,
+                           exchange="transpose"):
     """configs[4] as BASELINE.json states it — "param-range sharded across 8 MI355X via
     RCCL/xGMI" (SURVEY §8e Option B, strong scaling): `advanced`'s padded array of
     M = 2^27 entries is split into `world` position ranges; the bitonic network runs
-    distributed (range sorts, then per stage the pairwise RCCL exchanges of whole
-    ranges with partner r ^ j/C and the range merges), one halo exchange feeds the
+    distributed (range sorts; per stage, two RCCL all-to-alls transpose the rank bits of
+    the position into the range so the cross-range steps run locally — or, with
+    exchange="pairwise", RCCL exchanges of whole ranges with partner r ^ j/C — then the
+    range merges), one halo exchange feeds the
     fold, each rank compacts its run representatives and one RCCL reduce assembles
     the aggregate on rank 0 (fltee/parallel.py).  Rank r holds the records at
     positions [r*C, (r+1)*C) (same synthetic shape as `c5`)."""
@@ -177,11 +180,13 @@ def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
     rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).contiguous()
     del p, idx, vals
     chunk = torch.empty(C, dtype=torch.int64, device=device)
+    spare = {rank: torch.empty_like(chunk)}
     ops, comm = P.DeviceRangeOps(), P.DistRanks(rank, world)
 
     def step():
         D.advanced_init_range(rec, nrec, d, lo, C, out=chunk)
-        P.index_sharded_advanced({rank: chunk}, world, M, n, k, d, ops=ops, comm=comm)
+        P.index_sharded_advanced({rank: chunk}, world, M, n, k, d, ops=ops, comm=comm,
+                                 exchange=exchange, spare=spare)
 
     for _ in range(warmup):
         step()
@@ -196,10 +201,12 @@ def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
     torch.cuda.synchronize()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    del rec, chunk, ops
+    del rec, chunk, spare, ops
     wall = float(t[0]) / steps
+    how = ("per stage two RCCL all-to-alls transpose the rank bits into the range"
+           if exchange == "transpose" else "RCCL pairwise range exchanges")
     return dict(desc=w["desc"] + f", position-range sharded x{world}: distributed bitonic "
-                "(RCCL pairwise range exchanges) + halo fold + one RCCL reduce",
+                f"({how}) + halo fold + one RCCL reduce", exchange=exchange,
                 alg="advanced", n=n, d=d, k=k, M=M, range_records=C, ms_per_step=wall * 1e3,
                 value=n * k / wall, unit="client-params/s", scaling="strong")
 
@@ -396,6 +403,9 @@ def main():
         if world & (world - 1) == 0:
             sharded["c5_index_sharded"] = bench_c5_index_sharded(
                 torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
+            sharded["c5_index_sharded_pairwise"] = bench_c5_index_sharded(
+                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1,
+                exchange="pairwise")
 
     if rank == 0:
         line = {

@@ -92,6 +92,9 @@ hipError_t bitonic_sort_range(uint64_t *data, size_t m, uint32_t mode, uint32_t 
                               uint32_t pbase, hipStream_t s);
 hipError_t bitonic_merge_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
                                uint32_t ilog, uint32_t pbase, hipStream_t s);
+hipError_t bitonic_steps_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                               uint32_t ilog, uint32_t jtop, uint32_t jbot, uint32_t pbase,
+                               hipStream_t s);
 hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, uint32_t pos_mine,
                             uint32_t pos_theirs, uint32_t mode, uint32_t seed, uint32_t ilog,
                             uint32_t jlog, hipStream_t s);

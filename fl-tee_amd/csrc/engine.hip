@@ -417,6 +417,20 @@ extern "C" fltee_status_t fltee_bitonic_range_exchange_device(void *d_mine, cons
                : FLTEE_ERROR_UNEXPECTED;
 }
 
+extern "C" fltee_status_t fltee_bitonic_range_steps_device(void *d_records, size_t m,
+                                                           size_t pos_base, uint32_t mode,
+                                                           uint32_t seed, uint32_t stage_log,
+                                                           uint32_t step_top, uint32_t step_bot,
+                                                           void *stream) {
+    if (!range_ok(m, pos_base) || stage_log > 31 || step_bot > step_top ||
+        step_top >= stage_log || ((size_t)1 << step_top) >= m)
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    return bitonic_steps_range((uint64_t *)d_records, m, mode, seed, stage_log, step_top,
+                               step_bot, (uint32_t)pos_base, (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
 extern "C" size_t fltee_fold_context(size_t halo) { return fold_context(halo); }
 
 extern "C" fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m,

@@ -535,6 +535,30 @@ hipError_t bitonic_merge_range(uint64_t *data, size_t m, uint32_t mode, uint32_t
     }
 }
 
+// Steps 2^jtop .. 2^jbot (jtop < ilog, all < log2 m) of stage ilog on the m records at
+// positions pbase.. as register passes of up to 6 steps (the few high steps a
+// transposed range runs, fltee/parallel.py).
+hipError_t bitonic_steps_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
+                               uint32_t ilog, uint32_t jtop, uint32_t jbot, uint32_t pbase,
+                               hipStream_t s) {
+    if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
+    const uint32_t mlog = log2_pow2(m);
+    if (jtop >= mlog || jbot > jtop || jtop >= ilog) return hipErrorInvalidValue;
+    const int kMaxGlobalR = max_global_r();
+    int top = (int)jtop;
+    while (top >= (int)jbot) {
+        const int left = top - (int)jbot + 1;
+        const int R = left < kMaxGlobalR ? left : kMaxGlobalR;
+        hipError_t e;
+        if (mode == 0) e = launch_global<0>(data, mlog, ilog, (uint32_t)top, R, seed, s, pbase);
+        else if (mode == 1) e = launch_global<1>(data, mlog, ilog, (uint32_t)top, R, seed, s, pbase);
+        else e = launch_global<2>(data, mlog, ilog, (uint32_t)top, R, seed, s, pbase);
+        if (e != hipSuccess) return e;
+        top -= R;
+    }
+    return hipSuccess;
+}
+
 hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, uint32_t pos_mine,
                             uint32_t pos_theirs, uint32_t mode, uint32_t seed, uint32_t ilog,
                             uint32_t jlog, hipStream_t s) {

@@ -79,6 +79,7 @@ SIGNATURES = {
     "fltee_bitonic_range_sort_device": (_U32, [_P, _S, _S, _U32, _U32, _P]),
     "fltee_bitonic_range_merge_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _P]),
     "fltee_bitonic_range_exchange_device": (_U32, [_P, _P, _S, _S, _S, _U32, _U32, _U32, _P]),
+    "fltee_bitonic_range_steps_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _U32, _U32, _P]),
     "fltee_fold_context": (_S, [_S]),
     "fltee_fold_range_device": (_U32, [_P, _P, _S, _S, _S, ctypes.c_int64, _S, _S, _P, _P]),
     "fltee_compact_range_device": (_U32, [_P, _S, _S, _P, _P, _F, _P, _P]),

@@ -168,6 +168,15 @@ def bitonic_range_exchange(mine, theirs, pos_mine, pos_theirs, stage_log, mode=0
     return mine
 
 
+def bitonic_range_steps(records, pos_base, stage_log, step_top, step_bot, mode=0, seed=0,
+                        stream=None):
+    _check(L.lib().fltee_bitonic_range_steps_device(_ptr(records), records.numel(), pos_base, mode,
+                                                    seed, stage_log, step_top, step_bot,
+                                                    _stream(stream)),
+           "fltee_bitonic_range_steps_device")
+    return records
+
+
 def fold_context(halo):
     return L.lib().fltee_fold_context(halo)
 

@@ -150,6 +150,9 @@ class DeviceRangeOps:
     def exchange(self, x, theirs, pos, pos_theirs, stage_log):
         self.D.bitonic_range_exchange(x, theirs, pos, pos_theirs, stage_log)
 
+    def steps(self, x, pos, stage_log, step_top, step_bot):
+        self.D.bitonic_range_steps(x, pos, stage_log, step_top, step_bot)
+
     def fold(self, buf, origin, end, pos_base, fold_len, halo, key=0):
         dst = self._buf(("fold", key), buf.numel(), torch.int64, buf.device)
         st = self._buf(("st", key), 1, torch.int32, buf.device)
@@ -181,6 +184,13 @@ class VirtualRanks:
 
     def swap(self, chunks, partner):
         return {r: chunks[partner(r)].clone() for r in chunks}
+
+    def transpose(self, chunks, outs):
+        w = self.world
+        b = chunks[0].numel() // w
+        for r in range(w):
+            for q in range(w):
+                outs[q][r * b:(r + 1) * b].copy_(chunks[r][q * b:(q + 1) * b])
 
     def neighbours(self, chunks, h, t, pads):
         w = self.world
@@ -229,6 +239,17 @@ class DistRanks:
         self._run([(True, x, p), (False, theirs, p)])
         return {self.rank: theirs}
 
+    def transpose(self, chunks, outs):
+        """Block q of this range -> block `rank` of range q (one RCCL all-to-all: every
+        xGMI link carries C/W records at once)."""
+        x, out = chunks[self.rank], outs[self.rank]
+        if dist.get_backend() == "gloo" and x.is_cuda:
+            h = torch.empty(x.shape, dtype=x.dtype)
+            dist.all_to_all_single(h, x.cpu())
+            out.copy_(h)
+        else:
+            dist.all_to_all_single(out, x)
+
     def neighbours(self, chunks, h, t, pads):
         r, w, x = self.rank, self.world, chunks[self.rank]
         prev = torch.empty(h, dtype=x.dtype, device=x.device) if r > 0 else pads(h, x)
@@ -259,7 +280,7 @@ class DistRanks:
 
 
 def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None, halo=None,
-                           root=0, dp=None):
+                           root=0, dp=None, exchange="transpose", spare=None):
     """Option B: `advanced` over the padded array of M = next_pow2(n_total*k + d)
     entries split into `world` ranges of C = M / world.  `chunks` maps a range index r
     to its C entries (positions [r*C, (r+1)*C), built by fltee_advanced_init_range);
@@ -272,7 +293,17 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     own steps (j < C); the fold (:66-101) with fold_context(halo) records of the
     previous range in front and the next range's first records behind; the second
     sort's [0, d) prefix (:106-111, :32-34) = each range's compacted representatives,
-    summed over the ranges by one reduce, then x 1f32/n (common.rs:14-19)."""
+    summed over the ranges by one reduce, then x 1f32/n (common.rs:14-19).
+
+    exchange = "pairwise": every cross-range step swaps whole ranges with the partner
+    (one xGMI link per pair, W = 8: six steps of C records).  "transpose" (default): per
+    stage, one all-to-all swaps the rank bits of the position with the top log2 W local
+    bits (block q of range r <-> block r of range q: contiguous blocks, no packing), the
+    stage's cross-range steps then run locally as register passes
+    (fltee_bitonic_range_steps_device; mode 0 only needs the direction, which is global
+    bit `stage` = local bit stage - log2 W of the transposed range), and a second
+    all-to-all restores the layout before the range's own steps.  Every link carries
+    C/W records per all-to-all.  `spare` = {r: tensor like chunks[r]} reuses buffers."""
     assert world & (world - 1) == 0 and M % world == 0
     ops = ops if ops is not None else DeviceRangeOps()
     comm = comm if comm is not None else VirtualRanks(world)
@@ -281,13 +312,26 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     assert 1 << clog == C and 1 << mlog == M
     for r, x in chunks.items():
         ops.sort(x, r * C)
+    wlog = world.bit_length() - 1
+    if exchange == "transpose" and world > 1:
+        assert clog >= wlog
+        spare = spare if spare is not None else {r: torch.empty_like(x) for r, x in chunks.items()}
+        chunks = dict(chunks)
     for stage in range(clog + 1, mlog + 1):
-        for j in range(stage - 1, clog - 1, -1):
-            bit = 1 << (j - clog)
-            theirs = comm.swap(chunks, lambda q: q ^ bit)
-            for r, x in chunks.items():
-                ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
-            del theirs
+        if exchange == "transpose":
+            comm.transpose(chunks, spare)
+            chunks, spare = spare, chunks
+            for r, x in chunks.items():  # transposed: global bits clog.. are local bits clog-wlog..
+                ops.steps(x, 0, stage - wlog, stage - 1 - wlog, clog - wlog)
+            comm.transpose(chunks, spare)
+            chunks, spare = spare, chunks
+        else:
+            for j in range(stage - 1, clog - 1, -1):
+                bit = 1 << (j - clog)
+                theirs = comm.swap(chunks, lambda q: q ^ bit)
+                for r, x in chunks.items():
+                    ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
+                del theirs
         for r, x in chunks.items():
             ops.merge(x, r * C, stage)
     fold_len = n_total * k + d

@@ -244,6 +244,14 @@ fltee_status_t fltee_bitonic_range_exchange_device(void *d_mine, const void *d_t
                                                    size_t pos_mine, size_t pos_theirs,
                                                    uint32_t mode, uint32_t seed,
                                                    uint32_t stage_log, void *stream);
+/* the steps j = 2^step_top .. 2^step_bot (< m, step_top < stage_log) of stage
+ * 2^stage_log on one range (register passes).  Mode 0 only needs directions, so a
+ * range whose position bits were permuted by an all-to-all can run its cross-range
+ * steps locally through this call (fltee/parallel.py, transposed exchange). */
+fltee_status_t fltee_bitonic_range_steps_device(void *d_records, size_t m, size_t pos_base,
+                                                uint32_t mode, uint32_t seed, uint32_t stage_log,
+                                                uint32_t step_top, uint32_t step_bot,
+                                                void *stream);
 /* records of context the fold needs in front of a range: halo rounded up to 16. */
 size_t fltee_fold_context(size_t halo);
 /* advanced.rs:66-101 on [origin, end) of d_src (length m, global position =

@@ -32,7 +32,8 @@ def main():
     nrec = n * k
     M = 1 << (nrec + d - 1).bit_length()
     ops = P.DeviceRangeOps()
-    for world in [int(x) for x in args.worlds.split(",")]:
+    for world, exchange in [(int(x), e) for x in args.worlds.split(",")
+                            for e in ("transpose", "pairwise")]:
         C = M // world
         chunks = {r: torch.empty(C, dtype=torch.int64, device="cuda") for r in range(world)}
         comm = P.VirtualRanks(world)
@@ -43,13 +44,14 @@ def main():
             for r in range(world):
                 D.advanced_init_range(rec[r * C:] if r * C < nrec else rec, nrec, d, r * C, C,
                                       out=chunks[r])
-            out = P.index_sharded_advanced(chunks, world, M, n, k, d, ops=ops, comm=comm)
+            out = P.index_sharded_advanced(chunks, world, M, n, k, d, ops=ops, comm=comm,
+                                           exchange=exchange)
             torch.cuda.synchronize()
             if i:
                 times.append(time.perf_counter() - t0)
         same = bool(np.array_equal(out.cpu().numpy().view(np.uint32), ref))
         t = float(np.median(times))
-        print(json.dumps(dict(world=world, M=M, range_records=C, ms_all_ranks_one_gpu=t * 1e3,
+        print(json.dumps(dict(world=world, exchange=exchange, M=M, range_records=C, ms_all_ranks_one_gpu=t * 1e3,
                               ms_per_range_est=t * 1e3 / world, bit_exact_vs_single_gpu=same)),
               flush=True)
         assert same

@@ -54,6 +54,11 @@ class NumpyRangeOps:
         sw = asc ^ ((lo & MASK) < (hi & MASK))
         a[:] = np.where(sw, b, a)
 
+    def steps(self, x, pos, stage_log, step_top, step_bot):
+        a = _u(x)
+        for jlog in range(step_top, step_bot - 1, -1):
+            _step(a, pos, stage_log, jlog)
+
     def fold(self, buf, origin, end, pos_base, fold_len, halo, key=0):
         """fo_fold (advanced.rs:66-101) over the buffer's global positions, started
         fresh at its first position: the context in front makes the carry exact."""

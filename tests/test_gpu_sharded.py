@@ -66,11 +66,12 @@ def test_distributed_network_equals_single_sort(dev, oracle, world, m):
     assert np.array_equal(gi, ref["idx"]) and np.array_equal(gv.view(np.uint32), ref["val"].view(np.uint32))
 
 
+@pytest.mark.parametrize("exchange", ["transpose", "pairwise"])
 @pytest.mark.parametrize("world,n,d,k,idx_hi", [(2, 20, 3000, 400, None), (4, 20, 3000, 400, None),
                                                 (8, 4, 100, 50, None), (8, 100, 50890, 5089, None),
                                                 (2, 7, 3333, 1, None), (4, 20, 3000, 400, 64),
                                                 (4, 30, 2000, 300, 2100)])
-def test_index_sharded_advanced_bit_exact(dev, oracle, world, n, d, k, idx_hi):
+def test_index_sharded_advanced_bit_exact(dev, oracle, world, n, d, k, idx_hi, exchange):
     """idx_hi = 64: runs far longer than n + 1 (the fold's halo retry); 2100 > d: indices
     outside [0, d) fold into their own runs and never reach the output."""
     import torch
@@ -80,7 +81,8 @@ def test_index_sharded_advanced_bit_exact(dev, oracle, world, n, d, k, idx_hi):
     rec = torch.from_numpy(dev.pack_records(idx, val)).cuda()
     M = oracle.next_pow2(n * k + d)
     chunks = init_chunks(dev, rec, n * k, d, world, M)
-    out = index_sharded_advanced(chunks, world, M, n, k, d, comm=VirtualRanks(world))
+    out = index_sharded_advanced(chunks, world, M, n, k, d, comm=VirtualRanks(world),
+                                 exchange=exchange)
     ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
     assert st == 0
     got = out.cpu().numpy()

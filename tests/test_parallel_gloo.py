@@ -115,7 +115,7 @@ def case_b():
     return n, d, k, idx, val
 
 
-def worker_b(rank, world, port, outdir):
+def worker_b(rank, world, port, outdir, exchange):
     import sys
     for p in (ROOT, os.path.join(ROOT, "fl-tee_amd"), os.path.join(ROOT, "oracle"),
               os.path.join(ROOT, "tests")):
@@ -130,7 +130,7 @@ def worker_b(rank, world, port, outdir):
     C = M // world
     chunks = {rank: init_range(idx, val, d, rank * C, C)}
     out = P.index_sharded_advanced(chunks, world, M, n, k, d, ops=NumpyRangeOps(),
-                                   comm=P.DistRanks(rank, world))
+                                   comm=P.DistRanks(rank, world), exchange=exchange)
     if rank == 0:
         np.save(os.path.join(outdir, "adv_b.npy"), out.numpy())
     else:
@@ -139,9 +139,10 @@ def worker_b(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("exchange", ["transpose", "pairwise"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_index_sharded_advanced_gloo(oracle, tmp_path, world):
-    mp.spawn(worker_b, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+def test_index_sharded_advanced_gloo(oracle, tmp_path, world, exchange):
+    mp.spawn(worker_b, args=(world, free_port(), str(tmp_path), exchange), nprocs=world, join=True)
     n, d, k, idx, val = case_b()
     ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
     assert st == 0

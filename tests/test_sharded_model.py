@@ -17,17 +17,18 @@ def case(seed, n, d, k, idx_hi=None):
     return idx, val
 
 
+@pytest.mark.parametrize("exchange", ["transpose", "pairwise"])
 @pytest.mark.parametrize("world,n,d,k,idx_hi", [(1, 5, 200, 30, None), (2, 5, 200, 30, None),
                                                 (4, 6, 300, 20, None), (8, 4, 100, 50, None),
                                                 (4, 10, 150, 40, 40), (2, 7, 333, 1, None)])
-def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi):
+def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi, exchange):
     from fltee.parallel import VirtualRanks, index_sharded_advanced
     idx, val = case(world * 100 + n, n, d, k, idx_hi)
     M = oracle.next_pow2(n * k + d)
     C = M // world
     chunks = {r: init_range(idx, val, d, r * C, C) for r in range(world)}
     out = index_sharded_advanced(chunks, world, M, n, k, d, ops=NumpyRangeOps(),
-                                 comm=VirtualRanks(world))
+                                 comm=VirtualRanks(world), exchange=exchange)
     ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
     assert st == 0
     assert np.array_equal(out.numpy().view(np.uint32), ref.view(np.uint32))
