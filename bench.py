@@ -211,6 +211,89 @@ def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup,
                 value=n * k / wall, unit="client-params/s", scaling="strong")
 
 
+# The reference's own published bench files for one configuration (SURVEY §6,
+# secure_aggregation/results/*-50890-5089-10000-*.txt: d = 50890, k = 5089, 10000 users
+# sampled at 0.3 -> n = 3000; "Aggregation" column, seconds, single-threaded SGX enclave).
+REF_PUBLISHED = {
+    "advanced": dict(alg=1, ref_s=288.2, src="results/advanced-50890-5089-10000-20221121045110UTC.txt"),
+    "baseline": dict(alg=3, ref_s=54.3, src="results/baseline-50890-5089-10000-20221121043548UTC.txt"),
+    "non_oblivious": dict(alg=4, ref_s=0.456,
+                          src="results/non_oblivious-50890-5089-10000-20221121072225UTC.txt"),
+    "optimized": dict(alg=6, batch=93, ref_s=10.11, src="results/optimized-93-50890-5089-10000-*.txt (Total)"),
+}
+
+
+def bench_reference_configs(torch, D, device, steps=3):
+    """Each algorithm on the exact shape of the reference's published n = 3000 runs,
+    device-resident, one GPU; speedup = published enclave seconds / ours."""
+    n, d, k = 3000, 50890, 5089
+    rec = make_records(torch, n, d, k, 3000, device)
+    out = torch.empty(d, dtype=torch.float32, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    res = {}
+    for name, r in REF_PUBLISHED.items():
+        kw = dict(status=status)
+        if "batch" in r:
+            kw["batch"] = r["batch"]
+        D.aggregate(r["alg"], rec, n, k, d, out=out, **kw)  # warm (grow-only scratch)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(steps):
+            D.aggregate(r["alg"], rec, n, k, d, out=out, **kw)
+        b.record()
+        torch.cuda.synchronize()
+        t = a.elapsed_time(b) / steps / 1e3
+        res[name] = dict(ms=t * 1e3, ref_s=r["ref_s"], speedup=r["ref_s"] / t, ref_src=r["src"],
+                         value=n * k / t, unit="client-params/s")
+    assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
+    del rec
+    return dict(config="d=50890 (MLP-MNIST), k=5089, n=3000 (num_users=10000, ratio 0.3)", **res)
+
+
+def bench_next_rows(torch, D, device, steps=5):
+    """SURVEY §8f rows on one GPU, device-resident: the GPU AES-128-CTR decrypt of the
+    headline payload (lib.rs:312-343) and the client-side producers (utils.py:327-354,
+    update.py:187-204, utils.py:268-290) for 100 MLP-MNIST clients at alpha = 0.1."""
+    from fltee import client as CL
+    res = {}
+    n, d = 100, 1_000_000
+    ids = np.arange(n, dtype=np.uint32)
+    rec = make_records(torch, n, d, None, 41, device)
+    cipher = torch.empty_like(rec)
+    D.decrypt(ids, rec, d * 8, cipher)  # CTR: encryption == decryption
+    plain = torch.empty_like(rec)
+    ts = []
+    for _ in range(steps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        D.decrypt(ids, cipher, d * 8, plain)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3)
+    assert torch.equal(plain, rec)
+    t = min(ts)
+    res["aes_ctr_decrypt"] = dict(bytes=n * d * 8, ms=t * 1e3, gbs=2 * n * d * 8 / t / 1e9,
+                                  value=n * d / t, unit="client-params/s",
+                                  note="100 clients x 8 MB ciphertext -> records (read + write)")
+    del rec, cipher, plain
+    nc, dc, kc = 100, 50890, 5089
+    g = torch.Generator(device=device).manual_seed(43)
+    vals = torch.randn(nc, dc, generator=g, device=device) * 0.01
+    cids = np.arange(nc, dtype=np.uint32)
+    CL.produce_payloads(vals, cids, k=kc, clipping=1.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        CL.produce_payloads(vals, cids, k=kc, clipping=1.0)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / steps
+    res["client_producers"] = dict(ms=t * 1e3, n=nc, d=dc, k=kc, unit="ms per round (all clients)",
+                                   note="top-k by |v| + l2clipping + serialize_sparse + AES-CTR, "
+                                        "wall time incl. the per-call key upload")
+    return res
+
+
 def cpu_baseline_sample(d, n, seconds):
     """The oracle's `baseline` (baseline.rs o_update: one cmov RMW per 64-B line of the
     d-float output per record) on a bounded prefix of client 0's dense records,
@@ -438,6 +521,8 @@ def main():
                                    kernel_ms=r["kernel_s"] * 1e3, value=r["rate"],
                                    unit="client-params/s")
             line["extra"] = extra
+            line["reference_configs"] = bench_reference_configs(torch, D, device)
+            line["next_rows"] = bench_next_rows(torch, D, device)
         if sharded is not None:
             line["extra"] = sharded
         print(json.dumps(line), flush=True)
