@@ -99,8 +99,10 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 
     // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
     const uint32_t part = (l & 7) * 2;
-    fs_u32x4 pf[8];
-    auto load_stage = [&](uint32_t s) {
+    // prefetch two stages ahead (pa / pb alternate): at small m every wave walks only
+    // a few dozen stages and the load latency, not the bytes, sets the time
+    fs_u32x4 pa[8], pb[8];
+    auto load_stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t w = (l >> 3) + 8 * i;
@@ -112,13 +114,14 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             }
         }
     };
-    load_stage(0);
+    load_stage(pa, 0);
+    if (1 < nstage) load_stage(pb, 1);
 
     uint32_t pre_idx = 0;
     float pre_val = 0.0f;
     bool started = false;
     uint64_t prev = 0;
-    for (uint32_t s = 0; s < nstage; ++s) {
+    auto stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
         uint64_t *cur = win[s & 1], *old = win[(s + 1) & 1];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             cur[w * FS_ROW + part] = ((uint64_t)pf[i].y << 32) | pf[i].x;
             cur[w * FS_ROW + part + 1] = ((uint64_t)pf[i].w << 32) | pf[i].z;
         }
-        if (s + 1 < nstage) load_stage(s + 1);
+        if (s + 2 < nstage) load_stage(pf, s + 2);
         wave_sync_lds();
         uint64_t r[FS_W];
 #pragma unroll
@@ -168,6 +171,10 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             }
         }
         wave_sync_lds();
+    };
+    for (uint32_t s = 0; s < nstage; s += 2) {
+        stage(pa, s);
+        if (s + 1 < nstage) stage(pb, s + 1);
     }
 }
 

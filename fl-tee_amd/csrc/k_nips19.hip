@@ -81,12 +81,16 @@ __global__ __launch_bounds__(1024) void safe_aggregate_kernel(const uint2 *__res
                                                               size_t m, size_t d,
                                                               float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float acc[];
-    const size_t seg_lo = (size_t)blockIdx.y * SA_SEG;
+    // 1-D grid, segment fastest: the blocks of every segment of one chunk are dispatched
+    // back to back, so all but the first read that chunk from the Infinity Cache
+    const uint32_t nseg = (uint32_t)((d + SA_SEG - 1) / SA_SEG);
+    const uint32_t seg = blockIdx.x % nseg, chunk = blockIdx.x / nseg, nchunks = gridDim.x / nseg;
+    const size_t seg_lo = (size_t)seg * SA_SEG;
     const uint32_t seg_n = (uint32_t)((d - seg_lo) < SA_SEG ? (d - seg_lo) : SA_SEG);
     for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) acc[e] = 0.0f;
     __syncthreads();
-    const size_t per = (m + gridDim.x - 1) / gridDim.x;
-    const size_t lo = (size_t)blockIdx.x * per;
+    const size_t per = (m + nchunks - 1) / nchunks;
+    const size_t lo = (size_t)chunk * per;
     const size_t hi = lo + per < m ? lo + per : m;
     for (size_t p = lo + threadIdx.x; p < hi; p += 1024) {
         const uint2 w = src[p];
@@ -110,7 +114,7 @@ hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float 
     size_t chunks = (m + 8191) / 8192;
     if (chunks > SA_CHUNKS) chunks = SA_CHUNKS;
     const size_t lds = (d < SA_SEG ? d : SA_SEG) * 4;
-    hipLaunchKernelGGL(safe_aggregate_kernel, dim3((unsigned)chunks, segs), dim3(1024), lds, s,
+    hipLaunchKernelGGL(safe_aggregate_kernel, dim3((unsigned)(chunks * segs)), dim3(1024), lds, s,
                        (const uint2 *)src, m, d, out);
     return hipGetLastError();
 }
