@@ -76,6 +76,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // GPU's part of a position-sharded array, SURVEY §8e Option B): [0, origin) holds
 // >= Hr records of context from the previous range, and src[end] is the next
 // range's first record (or end + pbase >= fold_len).
+template <int DEPTH>
 __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restrict__ src,
                                                          uint64_t *__restrict__ dst, long long m,
                                                          long long origin, long long end,
@@ -99,8 +100,9 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 
     // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
     const uint32_t part = (l & 7) * 2;
-    // prefetch two stages ahead (pa / pb alternate): at small m every wave walks only
-    // a few dozen stages and the load latency, not the bytes, sets the time
+    // prefetch DEPTH stages ahead (DEPTH 2: pa / pb alternate).  Two help when there are
+    // few waves (small m: the load latency sets the time); one is faster at full chip
+    // occupancy (C5: 692 vs 741 us).
     fs_u32x4 pa[8], pb[8];
     auto load_stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
 #pragma unroll
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         }
     };
     load_stage(pa, 0);
-    if (1 < nstage) load_stage(pb, 1);
+    if (DEPTH == 2 && 1 < nstage) load_stage(pb, 1);
 
     uint32_t pre_idx = 0;
     float pre_val = 0.0f;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             cur[w * FS_ROW + part] = ((uint64_t)pf[i].y << 32) | pf[i].x;
             cur[w * FS_ROW + part + 1] = ((uint64_t)pf[i].w << 32) | pf[i].z;
         }
-        if (s + 2 < nstage) load_stage(pf, s + 2);
+        if (s + DEPTH < nstage) load_stage(pf, s + DEPTH);
         wave_sync_lds();
         uint64_t r[FS_W];
 #pragma unroll
@@ -172,9 +174,13 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         }
         wave_sync_lds();
     };
-    for (uint32_t s = 0; s < nstage; s += 2) {
-        stage(pa, s);
-        if (s + 1 < nstage) stage(pb, s + 1);
+    if (DEPTH == 2) {
+        for (uint32_t s = 0; s < nstage; s += 2) {
+            stage(pa, s);
+            if (s + 1 < nstage) stage(pb, s + 1);
+        }
+    } else {
+        for (uint32_t s = 0; s < nstage; ++s) stage(pa, s);
     }
 }
 
@@ -193,9 +199,14 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(fold_stream_kernel, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
-                       (long long)m, (long long)origin, (long long)end, pbase,
-                       (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
+    if (blocks <= 256)  // about one wave per CU: latency-bound, prefetch deeper
+        hipLaunchKernelGGL(fold_stream_kernel<2>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
+                           (long long)m, (long long)origin, (long long)end, pbase,
+                           (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
+    else
+        hipLaunchKernelGGL(fold_stream_kernel<1>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
+                           (long long)m, (long long)origin, (long long)end, pbase,
+                           (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
     return hipGetLastError();
 }
 
