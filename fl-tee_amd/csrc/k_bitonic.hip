@@ -70,6 +70,7 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 
 // Raw buffer access: byte offset = soffset (wave-uniform, SGPR) + voffset (per lane).
 typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int bt_u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBufNT = 2;  // cache policy: nontemporal (streaming, each byte used once)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t bt_rsrc(uint64_t *data) {
@@ -212,6 +213,70 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
+        tile = next;
+    }
+}
+
+// Contiguous merge (the steps j < T of stage ilog) with its first and last LDS round
+// in registers.  Lane t prefetches records t + r*NT (r < E = 2^R1): exactly the group
+// the first round needs (steps T/2 .. NT, distance log2 NT = tlog - R1), so that round
+// runs on the prefetch registers before they are written to LDS.  The last round
+// (steps 2^(RL-1) .. 1, groups of 2^RL consecutive records) stores its groups straight
+// to HBM (16-B stores) instead of writing LDS back for a separate store loop.  Saves
+// one LDS write + read of the tile and two barriers per tile; same network.
+template <int MODE, int E, int NT, int RL>
+__global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
+                                                           uint32_t tlog, uint32_t ilog,
+                                                           uint32_t seed, uint32_t ntiles,
+                                                           uint32_t pbase) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    static_assert((1 << R1) == E, "E must be a power of two <= 32");
+    static_assert(RL >= 1 && RL <= R1, "last round");
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    const uint32_t t = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
+    const uint32_t voff = t * 8u;
+    constexpr uint32_t rstride = (uint32_t)NT * 8u;
+    const uint32_t dlog1 = tlog - (uint32_t)R1;  // == log2 NT
+    uint64_t pf[E];
+    {
+        const uint32_t sb = (tile << tlog) * 8u;
+#pragma unroll
+        for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+    }
+    for (;;) {
+        const uint32_t base = tile << tlog;
+        group_steps<MODE, R1>(pf, base + pbase + t, dlog1, ilog, seed);
+#pragma unroll
+        for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        {
+            const uint32_t sb = ((next < ntiles ? next : tile) << tlog) * 8u;
+#pragma unroll
+            for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+        }
+        lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, ilog, (int)dlog1 - 1, RL, seed);
+        constexpr int G = E >> RL;
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const uint32_t b = (t + (uint32_t)h * NT) << RL;
+            uint64_t v[1 << RL];
+#pragma unroll
+            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + (uint32_t)q)];
+            group_steps<MODE, RL>(v, base + pbase + b, 0u, ilog, seed);
+#pragma unroll
+            for (int q = 0; q < (1 << RL); q += 2) {
+                const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
+                                    (uint32_t)(v[q + 1] >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
+                                                       (int)(base * 8u), kTileCP);
+            }
+        }
+        if (next >= ntiles) break;
+        __syncthreads();  // the last round's LDS reads retire before the next tile lands
         tile = next;
     }
 }
@@ -397,9 +462,53 @@ struct TileCfg {
     size_t lds;
 };
 
+static bool direct_merge() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+template <int MODE, int E, int NT>
+static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
+                                uint32_t seed, uint32_t pbase) {
+    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    const int rest = (int)c.tlog - R1;         // steps after the register round
+    const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
+    if (rl == 0) return hipErrorInvalidValue;
+#define BD_GO(RL_)                                                                                 \
+    do {                                                                                           \
+        static bool attr = false;                                                                  \
+        if (!attr) {                                                                               \
+            (void)hipFuncSetAttribute((const void *)bitonic_merge_direct<MODE, E, NT, RL_>,        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
+            attr = true;                                                                           \
+        }                                                                                          \
+        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_>), dim3(c.grid), dim3(NT), c.lds, \
+                           s, data, c.tlog, ilog, seed, c.tiles, pbase);                           \
+    } while (0)
+    switch (rl) {
+    case 1: BD_GO(1); break;
+    case 2: if constexpr (R1 >= 2) BD_GO(2); break;
+    case 3: if constexpr (R1 >= 3) BD_GO(3); break;
+    case 4: if constexpr (R1 >= 4) BD_GO(4); break;
+    default: if constexpr (R1 >= 5) BD_GO(5); break;
+    }
+#undef BD_GO
+    return hipGetLastError();
+}
+
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
+    if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge() && !pf2()) {
+        if (c.NT == 1024) return launch_direct<MODE, 16, 1024>(c, s, data, ilog, seed, pbase);
+        if (c.E == 32) return launch_direct<MODE, 32, 512>(c, s, data, ilog, seed, pbase);
+        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512>(c, s, data, ilog, seed, pbase);
+        if (c.NT == 512 && c.E == 8) return launch_direct<MODE, 8, 512>(c, s, data, ilog, seed, pbase);
+        if (c.NT == 512 && c.E == 4) return launch_direct<MODE, 4, 512>(c, s, data, ilog, seed, pbase);
+    }
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
     if (c.NT == 1024) BT_GO(16, 1024);
