@@ -222,7 +222,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // the first round needs (steps T/2 .. NT, distance log2 NT = tlog - R1), so that round
 // runs on the prefetch registers before they are written to LDS.  The last round
 // (steps 2^(RL-1) .. 1, groups of 2^RL consecutive records) stores its groups straight
-// to HBM (16-B stores) instead of writing LDS back for a separate store loop.  Saves
+// to HBM instead of writing LDS back for a separate store loop.  Saves
 // one LDS write + read of the tile and two barriers per tile; same network.
 template <int MODE, int E, int NT, int RL>
 __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
@@ -267,12 +267,20 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 #pragma unroll
             for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + (uint32_t)q)];
             group_steps<MODE, RL>(v, base + pbase + b, 0u, ilog, seed);
+            // 16-B stores.  hipcc (ROCm 7.2) may let the next group's VALU overwrite a
+            // dwordx4 store's data registers one instruction after the store, before the
+            // store has read them (measured: nondeterministic output); the explicit
+            // "s_nop 1" fenced by sched_barriers gives the two wait states the hazard needs
+            // (cdna_hip_programming.md §5.7: dwordx3/x4 stores end with s_nop 1).
 #pragma unroll
             for (int q = 0; q < (1 << RL); q += 2) {
                 const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
                                     (uint32_t)(v[q + 1] >> 32)};
                 __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
                                                        (int)(base * 8u), kTileCP);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 1" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         if (next >= ntiles) break;
@@ -502,13 +510,13 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
+    // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
+    // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
     if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge() && !pf2()) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024>(c, s, data, ilog, seed, pbase);
         if (c.E == 32) return launch_direct<MODE, 32, 512>(c, s, data, ilog, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512>(c, s, data, ilog, seed, pbase);
-        if (c.NT == 512 && c.E == 8) return launch_direct<MODE, 8, 512>(c, s, data, ilog, seed, pbase);
-        if (c.NT == 512 && c.E == 4) return launch_direct<MODE, 4, 512>(c, s, data, ilog, seed, pbase);
-    }
+    }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
     if (c.NT == 1024) BT_GO(16, 1024);

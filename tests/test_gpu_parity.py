@@ -144,6 +144,24 @@ def test_keyed_shuffle_bit_exact(dev, oracle, m):
     assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
 
 
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("m", [1 << 22, 1 << 24])
+def test_bitonic_repeatable(dev, mode, m):
+    """The same input through the network three times gives the same bytes (a store
+    whose data registers are overwritten too early shows up here as run-to-run noise)."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(m + mode)
+    base = torch.randint(0, 1 << 20, (m,), generator=g, device="cuda", dtype=torch.int64)
+    base = base | (torch.arange(m, device="cuda", dtype=torch.int64) << 32)
+    outs = []
+    for _ in range(3):
+        x = base.clone()
+        dev.bitonic(x, mode, seed=11)
+        outs.append(x)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 def test_composite_key_sort(dev):
     import torch
     rng = np.random.default_rng(9)
