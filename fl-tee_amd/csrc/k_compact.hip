@@ -52,8 +52,8 @@ typedef unsigned int cp_u32x2 __attribute__((ext_vector_type(2)));
 // Persistent: block b walks tiles b, b + grid, ...; the next tile's records are
 // prefetched into registers (raw buffer loads, out-of-range lanes selected to the
 // dummy afterwards: no per-load branch) while the current tile runs its levels.
-template <int NT, int PER, bool FIRST, int FINAL>
-__global__ __launch_bounds__(NT) void compact_pass(const uint64_t *__restrict__ src,
+template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1>
+__global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restrict__ src,
                                                    uint64_t *__restrict__ dst, uint32_t L,
                                                    uint32_t d, uint32_t j0, uint32_t G,
                                                    uint32_t logW, uint32_t S, uint32_t rows,
@@ -153,16 +153,25 @@ __global__ __launch_bounds__(NT) void compact_pass(const uint64_t *__restrict__ 
     }
 }
 
+// resident 512-lane blocks per CU (FLTEE_COMPACT_BLOCKS=3 asks hipcc for 6 waves per SIMD (launch_bounds 2nd arg = min waves per EU), i.e. <= 80 VGPRs,
+// so three fit; A/B knob)
+static int compact_blocks() {
+    static int b = [] {
+        const char *e = getenv("FLTEE_COMPACT_BLOCKS");
+        return e && e[0] == '3' ? 3 : 2;
+    }();
+    return b;
+}
 static int g_compact_variant = 1;  // fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB
 void set_compact_variant(int v) { g_compact_variant = v; }
 
-template <int NT, int PER>
+template <int NT, int PER, int MINB = 1>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
                               uint64_t *dst, uint32_t L, uint32_t d, uint32_t j0, uint32_t G,
                               uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
                               float coef, float *out, uint32_t ntiles) {
 #define CP_GO(F, X)                                                                              \
-    hipLaunchKernelGGL((compact_pass<NT, PER, F, X>), dim3(grid), dim3(NT), 0, s, src, dst, L, d, \
+    hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB>), dim3(grid), dim3(NT), 0, s, src, dst, L, d, \
                        j0, G, logW, S, rows, ngroups, coef, out, ntiles)
     if (first) {
         if (fin == 0) CP_GO(true, 0); else if (fin == 1) CP_GO(true, 1); else CP_GO(true, 2);
@@ -219,10 +228,16 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
-        const unsigned grid = (unsigned)(ntiles < (small ? 512u : 256u) ? ntiles : (small ? 512u : 256u));
+        const unsigned res = small ? 256u * (unsigned)compact_blocks() : 256u;
+        const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =
-            small ? launch_pass<512, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
-                                        G, logW, S, rows, ngroups, coef, out, (uint32_t)ntiles)
+            small ? (compact_blocks() == 3
+                         ? launch_pass<512, 8, 6>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                                                  (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
+                                                  out, (uint32_t)ntiles)
+                         : launch_pass<512, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                                               (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out,
+                                               (uint32_t)ntiles))
                   : launch_pass<1024, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
                                          G, logW, S, rows, ngroups, coef, out, (uint32_t)ntiles);
         if (e != hipSuccess) return e;
