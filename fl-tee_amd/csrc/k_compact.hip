@@ -153,12 +153,15 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
     }
 }
 
-// resident 512-lane blocks per CU (FLTEE_COMPACT_BLOCKS=3 asks hipcc for 6 waves per SIMD (launch_bounds 2nd arg = min waves per EU), i.e. <= 80 VGPRs,
-// so three fit; A/B knob)
+// Resident 512-lane blocks per CU for the passes after the first: 3 (default) asks hipcc
+// for 6 waves per SIMD (launch_bounds' 2nd argument = min waves per EU: <= 80 VGPRs).
+// A/B at C5: 497 vs 534 us per middle pass, 499 vs 570 us for the last; the first pass
+// (more live state) spills at that bound (868 vs 751 us), so it keeps 2.
+// FLTEE_COMPACT_BLOCKS=2: two for every pass.
 static int compact_blocks() {
     static int b = [] {
         const char *e = getenv("FLTEE_COMPACT_BLOCKS");
-        return e && e[0] == '3' ? 3 : 2;
+        return e && e[0] == '2' ? 2 : 3;
     }();
     return b;
 }
@@ -228,10 +231,11 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
-        const unsigned res = small ? 256u * (unsigned)compact_blocks() : 256u;
+        const int blk = j0 == 0 ? 2 : compact_blocks();
+        const unsigned res = small ? 256u * (unsigned)blk : 256u;
         const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =
-            small ? (compact_blocks() == 3
+            small ? (blk == 3
                          ? launch_pass<512, 8, 6>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
                                                   out, (uint32_t)ntiles)
