@@ -289,6 +289,97 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
     }
 }
 
+// Stage IL (< log2 E) on a lane's E consecutive records at positions p0..p0+E-1: the
+// records form E / 2^IL whole stage blocks, each with its own direction.
+template <int MODE, int IL, int E>
+__device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32_t seed) {
+    constexpr int B = 1 << IL;
+#pragma unroll
+    for (int lv = IL - 1; lv >= 0; --lv) {
+        const uint32_t key = MODE == 2 ? shuffle_step_key(seed, IL, (uint32_t)lv) : 0u;
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            if (q & (1 << lv)) continue;
+            const int qm = q | (1 << lv);
+            const bool asc = ((p0 + (uint32_t)(q & ~(B - 1))) & (1u << IL)) == 0;
+            const uint64_t a = v[q], c = v[qm];
+            const bool sw = asc ^ cond2<MODE>(a, c, p0 + (uint32_t)q, key);
+            v[q] = sw ? c : a;
+            v[qm] = sw ? a : c;
+        }
+    }
+}
+
+// The first pass of a sort (stages 1..T of every contiguous tile) with its first and
+// last work in registers: lane t loads records tE .. tE+E-1 (16-B loads), runs stages
+// 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
+// log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
+// stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
+template <int MODE, int E, int NT, int RL>
+__global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
+                                                          uint32_t tlog, uint32_t seed,
+                                                          uint32_t ntiles, uint32_t pbase) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    static_assert((1 << R1) == E && RL >= 1 && RL <= R1, "tile shape");
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    const uint32_t t = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
+    const uint32_t voff = t * (uint32_t)E * 8u;
+    uint64_t pf[E];
+    auto load = [&](uint32_t tl) {
+        const uint32_t sb = (tl << tlog) * 8u;
+#pragma unroll
+        for (int r = 0; r < E; r += 2) {
+            const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + (uint32_t)r * 8u),
+                                                                      (int)sb, kTileCP);
+            pf[r] = ((uint64_t)x.y << 32) | x.x;
+            pf[r + 1] = ((uint64_t)x.w << 32) | x.z;
+        }
+    };
+    load(tile);
+    for (;;) {
+        const uint32_t base = tile << tlog;
+        const uint32_t p0 = base + pbase + t * (uint32_t)E;
+        lane_stage<MODE, 1, E>(pf, p0, seed);
+        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, seed);
+        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, seed);
+        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, seed);
+        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, seed);
+#pragma unroll
+        for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        load(next < ntiles ? next : tile);
+        for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
+            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
+        lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
+        constexpr int G = E >> RL;
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+            const uint32_t b = (t + (uint32_t)h * NT) << RL;
+            uint64_t v[1 << RL];
+#pragma unroll
+            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + (uint32_t)q)];
+            group_steps<MODE, RL>(v, base + pbase + b, 0u, tlog, seed);
+#pragma unroll
+            for (int q = 0; q < (1 << RL); q += 2) {
+                const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
+                                    (uint32_t)(v[q + 1] >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
+                                                       (int)(base * 8u), kTileCP);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 1" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (next >= ntiles) break;
+        __syncthreads();  // the last round's LDS reads retire before the next tile lands
+        tile = next;
+    }
+}
+
 // The same persistent tile walk with the prefetch TWO tiles deep (pa / pb alternate):
 // the loads of tile i+2 are in flight while tile i runs its rounds and tile i+1 waits
 // in registers.  Needs 2E prefetch registers, so it is used with 512-lane blocks
@@ -507,9 +598,49 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     return hipGetLastError();
 }
 
+template <int MODE, int E, int NT>
+static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
+                                     uint32_t seed, uint32_t pbase) {
+    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
+#define BS_GO(RL_)                                                                                 \
+    do {                                                                                           \
+        static bool attr = false;                                                                  \
+        if (!attr) {                                                                               \
+            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_>,         \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
+            attr = true;                                                                           \
+        }                                                                                          \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_>), dim3(c.grid), dim3(NT), c.lds,  \
+                           s, data, c.tlog, seed, c.tiles, pbase);                                 \
+    } while (0)
+    switch (rl) {
+    case 1: BS_GO(1); break;
+    case 2: if constexpr (R1 >= 2) BS_GO(2); break;
+    case 3: if constexpr (R1 >= 3) BS_GO(3); break;
+    case 4: if constexpr (R1 >= 4) BS_GO(4); break;
+    default: if constexpr (R1 >= 5) BS_GO(5); break;
+    }
+#undef BS_GO
+    return hipGetLastError();
+}
+
+static bool direct_sort() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_DIRECT_SORT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
+    if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort() && !pf2()) {
+        if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
+        if (c.E == 32) return launch_sort_direct<MODE, 32, 512>(c, s, data, seed, pbase);
+        if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
+    }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
     if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge() && !pf2()) {
