@@ -380,58 +380,6 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
     }
 }
 
-// The same persistent tile walk with the prefetch TWO tiles deep (pa / pb alternate):
-// the loads of tile i+2 are in flight while tile i runs its rounds and tile i+1 waits
-// in registers.  Needs 2E prefetch registers, so it is used with 512-lane blocks
-// (2 waves per SIMD, 256 VGPRs); FLTEE_BITONIC_PF2=1 selects it (A/B).
-template <int MODE, bool SORT, int E, int NT>
-__global__ __launch_bounds__(NT) void bitonic_tiles2(uint64_t *__restrict__ data, uint32_t tlog,
-                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    uint32_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    const uint32_t voff = tile_pos(0u, threadIdx.x, wlog, dtile) * 8u;
-    const uint32_t rstride = ((uint32_t)NT << (dtile - wlog)) * 8u;
-    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
-    uint64_t pa[E], pb[E];
-    auto load = [&](uint64_t (&p)[E], uint32_t t) {
-        const uint32_t sb = tile_base(t, tlog, wlog, dtile) * 8u;
-#pragma unroll
-        for (int r = 0; r < E; ++r) p[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
-    };
-    load(pa, tile);
-    load(pb, tile + gridDim.x < ntiles ? tile + gridDim.x : tile);
-    // one tile from p; p then prefetches the tile two steps ahead.  false: last tile done
-    auto body = [&](uint64_t (&p)[E]) -> bool {
-        const uint32_t base = tile_base(tile, tlog, wlog, dtile);
-#pragma unroll
-        for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = p[r];
-        __syncthreads();
-        const uint32_t ahead = tile + 2 * gridDim.x;
-        load(p, ahead < ntiles ? ahead : tile);  // always load: no branch around the loads
-        if (SORT) {
-            for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
-        } else {
-            lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
-                                   wlog < tlog ? (int)wlog : 0, seed);
-        }
-        const uint32_t sb = base * 8u;
-#pragma unroll
-        for (int r = 0; r < E; ++r) bt_store<kTileCP>(rs, voff, sb + (uint32_t)r * rstride, sm[lpad(threadIdx.x + r * NT)]);
-        const uint32_t next = tile + gridDim.x;
-        if (next >= ntiles) return false;
-        __syncthreads();  // this tile's LDS reads retire before the next tile lands
-        tile = next;
-        return true;
-    };
-    for (;;) {
-        if (!body(pa)) break;
-        if (!body(pb)) break;
-    }
-}
-
 // --------------------------------------------------------- global pass -----
 // Steps jtop..jtop-R+1 of stage ilog straight from HBM: lane t owns group t.
 // Record q of a group sits at byte (q << dlog) * 8 + b * 8: a wave-uniform part and
@@ -526,14 +474,6 @@ static bool strided_passes() {
     return on;
 }
 
-static bool pf2() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_PF2");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 template <int MODE, bool SORT, int E, int NT>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
@@ -542,16 +482,10 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles2<MODE, SORT, E, NT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    if (NT <= 512 && E >= 8 && pf2())
-        hipLaunchKernelGGL((bitonic_tiles2<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
-                           tlog, ilog, wlog, dtile, seed, tiles, pbase);
-    else
-        hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
-                           tlog, ilog, wlog, dtile, seed, tiles, pbase);
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
+                       tlog, ilog, wlog, dtile, seed, tiles, pbase);
     return hipGetLastError();
 }
 
@@ -636,14 +570,14 @@ static bool direct_sort() {
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
-    if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort() && !pf2()) {
+    if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
         if (c.E == 32) return launch_sort_direct<MODE, 32, 512>(c, s, data, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
-    if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge() && !pf2()) {
+    if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024>(c, s, data, ilog, seed, pbase);
         if (c.E == 32) return launch_direct<MODE, 32, 512>(c, s, data, ilog, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512>(c, s, data, ilog, seed, pbase);
