@@ -129,6 +129,9 @@ hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, 
                                size_t tf, size_t m, uint64_t *dst, hipStream_t s);
 hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float *out,
                                  hipStream_t s);
+hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_t *r, size_t d,
+                                     size_t tf, size_t pbase, size_t m, uint64_t *dst,
+                                     hipStream_t s);
 
 // k_dp.hip
 hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,

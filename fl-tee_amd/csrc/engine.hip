@@ -459,6 +459,26 @@ extern "C" fltee_status_t fltee_compact_range_device(const void *d_chunk, size_t
                : FLTEE_ERROR_UNEXPECTED;
 }
 
+extern "C" fltee_status_t fltee_nips19_build_range_device(const void *d_records, size_t nrec,
+                                                          const uint32_t *d_r, size_t d,
+                                                          size_t tf, size_t pos_base, size_t m,
+                                                          void *d_dst, void *stream) {
+    if (nrec + d * tf >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_nips19_build_range(d_records, nrec, d_r, d, tf, pos_base, m, (uint64_t *)d_dst,
+                                     (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t m, size_t d,
+                                                      float *d_out, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (d && hipMemsetAsync(d_out, 0, d * 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    return launch_safe_aggregate((const uint64_t *)d_src, m, d, d_out, s) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
 
 extern "C" fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d,

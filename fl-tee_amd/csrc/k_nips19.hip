@@ -45,14 +45,17 @@ hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t
     return hipGetLastError();
 }
 
+// dst[x] = entry pbase + x of the padded array; rec[x] is the record at position
+// pbase + x (read only where pbase + x < nrec).  pbase = 0: the whole array.
 __global__ void nips19_build_kernel(const uint64_t *__restrict__ rec, size_t nrec,
-                                    const uint32_t *__restrict__ r, size_t d, size_t tf, size_t m,
-                                    uint64_t *__restrict__ dst) {
+                                    const uint32_t *__restrict__ r, size_t d, size_t tf,
+                                    size_t pbase, size_t m, uint64_t *__restrict__ dst) {
     const size_t npad = d * tf;
-    for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (size_t)gridDim.x * 256) {
+    for (size_t x = (size_t)blockIdx.x * 256 + threadIdx.x; x < m; x += (size_t)gridDim.x * 256) {
+        const size_t p = pbase + x;
         uint64_t v;
         if (p < nrec) {
-            v = rec[p];
+            v = rec[x];
         } else if (p < nrec + npad) {
             const size_t e = p - nrec;
             const size_t i = e / tf, j = e - i * tf;
@@ -61,17 +64,24 @@ __global__ void nips19_build_kernel(const uint64_t *__restrict__ rec, size_t nre
         } else {
             v = (uint64_t)0xFFFFFFFFu;
         }
-        dst[p] = v;
+        dst[x] = v;
     }
+}
+
+hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_t *r, size_t d,
+                                     size_t tf, size_t pbase, size_t m, uint64_t *dst,
+                                     hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    size_t blocks = (m + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(nips19_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint64_t *)rec, nrec, r, d, tf, pbase, m, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, size_t d,
                                size_t tf, size_t m, uint64_t *dst, hipStream_t s) {
-    size_t blocks = (m + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(nips19_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const uint64_t *)rec, nrec, r, d, tf, m, dst);
-    return hipGetLastError();
+    return launch_nips19_build_range(rec, nrec, r, d, tf, 0, m, dst, s);
 }
 
 constexpr uint32_t SA_SEG = 32768;  // floats per LDS segment (128 KB)

@@ -83,6 +83,8 @@ SIGNATURES = {
     "fltee_fold_context": (_S, [_S]),
     "fltee_fold_range_device": (_U32, [_P, _P, _S, _S, _S, ctypes.c_int64, _S, _S, _P, _P]),
     "fltee_compact_range_device": (_U32, [_P, _S, _S, _P, _P, _F, _P, _P]),
+    "fltee_nips19_build_range_device": (_U32, [_P, _S, _P, _S, _S, _S, _S, _P, _P]),
+    "fltee_safe_aggregate_device": (_U32, [_P, _S, _S, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_version": (ctypes.c_char_p, []),
 }

@@ -197,3 +197,24 @@ def compact_range(chunk, d, coef, buf, tmp, out=None, stream=None):
                                               _ptr(out), _stream(stream)),
            "fltee_compact_range_device")
     return out
+
+
+def nips19_build_range(records, nrec, r, d, tf, pos_base, m, out=None, stream=None):
+    """Entries pos_base..pos_base+m-1 of nips19's padded array (records ++ Laplace dummies
+    ++ pads, common.rs:164-197); r = laplace_r(...)[0], tf = int(T)."""
+    if out is None:
+        out = torch.empty(m, dtype=torch.int64, device=records.device)
+    _check(L.lib().fltee_nips19_build_range_device(_ptr(records), nrec, _ptr(r), d, tf, pos_base, m,
+                                                   _ptr(out), _stream(stream)),
+           "fltee_nips19_build_range_device")
+    return out
+
+
+def safe_aggregate(entries, d, out=None, stream=None):
+    """common.rs:25-35 on a range of shuffled entries: un-averaged f32[d] partial sums."""
+    if out is None:
+        out = torch.empty(d, dtype=torch.float32, device=entries.device)
+    _check(L.lib().fltee_safe_aggregate_device(_ptr(entries), entries.numel(), d, _ptr(out),
+                                               _stream(stream)),
+           "fltee_safe_aggregate_device")
+    return out

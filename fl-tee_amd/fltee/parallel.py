@@ -141,14 +141,17 @@ class DeviceRangeOps:
     def fold_context(self, halo):
         return self.D.fold_context(halo)
 
-    def sort(self, x, pos):
-        self.D.bitonic_range_sort(x, pos)
+    def sort(self, x, pos, mode=0, seed=0):
+        self.D.bitonic_range_sort(x, pos, mode=mode, seed=seed)
 
-    def merge(self, x, pos, stage_log):
-        self.D.bitonic_range_merge(x, pos, stage_log)
+    def merge(self, x, pos, stage_log, mode=0, seed=0):
+        self.D.bitonic_range_merge(x, pos, stage_log, mode=mode, seed=seed)
 
-    def exchange(self, x, theirs, pos, pos_theirs, stage_log):
-        self.D.bitonic_range_exchange(x, theirs, pos, pos_theirs, stage_log)
+    def exchange(self, x, theirs, pos, pos_theirs, stage_log, mode=0, seed=0):
+        self.D.bitonic_range_exchange(x, theirs, pos, pos_theirs, stage_log, mode=mode, seed=seed)
+
+    def safe_aggregate(self, x, d):
+        return self.D.safe_aggregate(x, d)
 
     def steps(self, x, pos, stage_log, step_top, step_bot):
         self.D.bitonic_range_steps(x, pos, stage_log, step_top, step_bot)
@@ -279,6 +282,70 @@ class DistRanks:
         return out if self.rank == root else None
 
 
+def distributed_network(chunks, world, M, ops, comm, mode=0, seed=0, exchange="transpose",
+                        spare=None):
+    """The reference network (advanced.rs:147-176; mode 2: the keyed shuffle of
+    nips19.rs:66-105) over M positions split into `world` ranges of C = M / world:
+    every range runs stages up to C on its own, then each later stage does its steps
+    j >= C across ranges (see index_sharded_advanced for the two exchanges; the
+    transposed one needs only directions, so mode 2 always swaps pairwise) and its
+    steps j < C inside each range.  Returns the chunks dict (ranges may have moved to
+    the `spare` buffers)."""
+    C = M // world
+    clog, mlog = C.bit_length() - 1, M.bit_length() - 1
+    assert 1 << clog == C and 1 << mlog == M
+    for r, x in chunks.items():
+        ops.sort(x, r * C, mode=mode, seed=seed)
+    wlog = world.bit_length() - 1
+    transpose = exchange == "transpose" and world > 1 and mode == 0
+    if transpose:
+        assert clog >= wlog
+        spare = spare if spare is not None else {r: torch.empty_like(x) for r, x in chunks.items()}
+        chunks = dict(chunks)
+    for stage in range(clog + 1, mlog + 1):
+        if transpose:
+            comm.transpose(chunks, spare)
+            chunks, spare = spare, chunks
+            for r, x in chunks.items():  # transposed: global bits clog.. are local bits clog-wlog..
+                ops.steps(x, 0, stage - wlog, stage - 1 - wlog, clog - wlog)
+            comm.transpose(chunks, spare)
+            chunks, spare = spare, chunks
+        else:
+            for j in range(stage - 1, clog - 1, -1):
+                bit = 1 << (j - clog)
+                theirs = comm.swap(chunks, lambda q: q ^ bit)
+                for r, x in chunks.items():
+                    ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage, mode=mode, seed=seed)
+                del theirs
+        for r, x in chunks.items():
+            ops.merge(x, r * C, stage, mode=mode, seed=seed)
+    return chunks
+
+
+def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None, root=0,
+                         dp=None):
+    """nips19 (nips19.rs:18-63) by position range: `chunks` = the ranges of the padded
+    array (records ++ Laplace dummies ++ pads, fltee_nips19_build_range with the same
+    Laplace counts on every rank: counter-based, no exchange); the keyed shuffle runs
+    as a distributed network (pairwise exchanges, mode 2), every rank runs
+    safe_aggregate on its range and one reduce adds the partial sums on the root,
+    x 1f32/n, then DP noise.  The shuffle permutation is bit-identical to one GPU's;
+    the per-index sums are float atomics, as on one GPU (fp32 tolerance)."""
+    assert world & (world - 1) == 0 and M % world == 0
+    ops = ops if ops is not None else DeviceRangeOps()
+    comm = comm if comm is not None else VirtualRanks(world)
+    key = (seed ^ (seed >> 32)) & 0xFFFFFFFF  # the shuffle key of fltee_aggregate_device
+    chunks = distributed_network(chunks, world, M, ops, comm, mode=2, seed=key, exchange="pairwise")
+    outs = {r: ops.safe_aggregate(x, d) for r, x in chunks.items()}
+    out = comm.reduce(outs, root)
+    if out is None:
+        return None
+    out = ops.finish(out, float(np.float32(1.0) / np.float32(n_total)))
+    if dp is not None:
+        ops.dp(out, dp["sigma"], dp["clipping"], n_total, dp.get("seed", 0))
+    return out
+
+
 def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None, halo=None,
                            root=0, dp=None, exchange="transpose", spare=None):
     """Option B: `advanced` over the padded array of M = next_pow2(n_total*k + d)
@@ -308,32 +375,7 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     ops = ops if ops is not None else DeviceRangeOps()
     comm = comm if comm is not None else VirtualRanks(world)
     C = M // world
-    clog, mlog = C.bit_length() - 1, M.bit_length() - 1
-    assert 1 << clog == C and 1 << mlog == M
-    for r, x in chunks.items():
-        ops.sort(x, r * C)
-    wlog = world.bit_length() - 1
-    if exchange == "transpose" and world > 1:
-        assert clog >= wlog
-        spare = spare if spare is not None else {r: torch.empty_like(x) for r, x in chunks.items()}
-        chunks = dict(chunks)
-    for stage in range(clog + 1, mlog + 1):
-        if exchange == "transpose":
-            comm.transpose(chunks, spare)
-            chunks, spare = spare, chunks
-            for r, x in chunks.items():  # transposed: global bits clog.. are local bits clog-wlog..
-                ops.steps(x, 0, stage - wlog, stage - 1 - wlog, clog - wlog)
-            comm.transpose(chunks, spare)
-            chunks, spare = spare, chunks
-        else:
-            for j in range(stage - 1, clog - 1, -1):
-                bit = 1 << (j - clog)
-                theirs = comm.swap(chunks, lambda q: q ^ bit)
-                for r, x in chunks.items():
-                    ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
-                del theirs
-        for r, x in chunks.items():
-            ops.merge(x, r * C, stage)
+    chunks = distributed_network(chunks, world, M, ops, comm, exchange=exchange, spare=spare)
     fold_len = n_total * k + d
     h = n_total if halo is None else halo
     while True:

@@ -268,6 +268,18 @@ fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m,
 fltee_status_t fltee_compact_range_device(const void *d_chunk, size_t c, size_t d, void *d_buf,
                                           void *d_tmp, float coef, float *d_out, void *stream);
 
+/* nips19 by position range (the shuffle is the same kind of network): entries
+ * pos_base .. pos_base+m-1 of records ++ d*tf Laplace dummies (common.rs:189-197;
+ * d_r from fltee_laplace_r_device, tf = (usize)T) ++ (u32::MAX, 0.0) pads; and
+ * safe_aggregate (common.rs:25-35) of m entries into d_out[d] (zeroed first,
+ * un-averaged: the ranges' partial sums are added by the caller's reduce). */
+fltee_status_t fltee_nips19_build_range_device(const void *d_records, size_t nrec,
+                                               const uint32_t *d_r, size_t d, size_t tf,
+                                               size_t pos_base, size_t m, void *d_dst,
+                                               void *stream);
+fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t m, size_t d, float *d_out,
+                                           void *stream);
+
 /* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
 void fltee_debug_set_seed(uint64_t seed);
 /* Library build/version string. */

@@ -14,15 +14,39 @@ def _u(x):
     return x.numpy().view(np.uint64)
 
 
-def _step(a, pbase, ilog, jlog):
-    """One step (stage 2^ilog, distance 2^jlog < len(a)) of advanced.rs:155-175."""
+def _mix32(x):
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def step_key(seed, ilog, jlog):
+    """shuffle_step_key of fl-tee_amd/csrc/common.h (the keyed comparator's per-step key)."""
+    return _mix32(_mix32(seed) + ((ilog << 8) | jlog) * 0x9E3779B9)
+
+
+def _cond2(lo, hi, l, mode, key):
+    if mode == 0:
+        return (lo & MASK) < (hi & MASK)
+    h = ((l.astype(np.uint64) ^ np.uint64(key)) * np.uint64(0x9E3779B1)) & MASK
+    return (h >> np.uint64(31)) != 0
+
+
+def _step(a, pbase, ilog, jlog, mode=0, seed=0):
+    """One step (stage 2^ilog, distance 2^jlog < len(a)) of advanced.rs:155-175 (mode 0)
+    or of the keyed shuffle (mode 2)."""
     j = 1 << jlog
     x = np.arange(len(a) // 2, dtype=np.int64)
     l = ((x & ~(j - 1)) << 1) | (x & (j - 1))
     m = l + j
     asc = ((pbase + l) & (1 << ilog)) == 0
     al, am = a[l].copy(), a[m].copy()
-    sw = asc ^ ((al & MASK) < (am & MASK))
+    key = step_key(seed, ilog, jlog) if mode == 2 else 0
+    sw = asc ^ _cond2(al, am, pbase + l, mode, key)
     a[l] = np.where(sw, am, al)
     a[m] = np.where(sw, al, am)
 
@@ -34,25 +58,37 @@ class NumpyRangeOps:
     def fold_context(self, halo):
         return (halo + 15) // 16 * 16
 
-    def sort(self, x, pos):
+    def sort(self, x, pos, mode=0, seed=0):
         a = _u(x)
         for ilog in range(1, len(a).bit_length()):
             for jlog in range(ilog - 1, -1, -1):
-                _step(a, pos, ilog, jlog)
+                _step(a, pos, ilog, jlog, mode, seed)
 
-    def merge(self, x, pos, stage_log):
+    def merge(self, x, pos, stage_log, mode=0, seed=0):
         a = _u(x)
         for jlog in range(len(a).bit_length() - 2, -1, -1):
-            _step(a, pos, stage_log, jlog)
+            _step(a, pos, stage_log, jlog, mode, seed)
 
-    def exchange(self, x, theirs, pos, pos_theirs, stage_log):
+    def exchange(self, x, theirs, pos, pos_theirs, stage_log, mode=0, seed=0):
         a, b = _u(x), _u(theirs)
         lower = pos < pos_theirs
         lo, hi = (a, b) if lower else (b, a)
         p = min(pos, pos_theirs) + np.arange(len(a), dtype=np.int64)
         asc = (p & (1 << stage_log)) == 0
-        sw = asc ^ ((lo & MASK) < (hi & MASK))
+        jlog = (abs(pos - pos_theirs)).bit_length() - 1
+        key = step_key(seed, stage_log, jlog) if mode == 2 else 0
+        sw = asc ^ _cond2(lo, hi, p, mode, key)
         a[:] = np.where(sw, b, a)
+
+    def safe_aggregate(self, x, d):
+        """common.rs:25-35 on one range: g[idx] += val for idx < d, in position order."""
+        a = _u(x)
+        idx = (a & MASK).astype(np.int64)
+        val = (a >> np.uint64(32)).astype(np.uint32).view(np.float32)
+        out = np.zeros(d, np.float32)
+        sel = idx < d
+        np.add.at(out, idx[sel], val[sel])
+        return torch.from_numpy(out)
 
     def steps(self, x, pos, stage_log, step_top, step_bot):
         a = _u(x)

@@ -36,34 +36,51 @@ def init_chunks(dev, rec, nrec, d, world, M):
             for r in range(world)}
 
 
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("world,m", [(2, 1 << 10), (4, 1 << 15), (8, 1 << 20), (8, 512), (2, 1 << 22)])
-def test_distributed_network_equals_single_sort(dev, oracle, world, m):
-    """Range sorts + exchanges + range merges == the reference network on all M."""
+def test_distributed_network_equals_single_sort(dev, oracle, world, m, mode):
+    """Range sorts + exchanges + range merges == the reference network on all M (mode 0:
+    advanced's sort; mode 2: nips19's keyed shuffle, pairwise exchanges)."""
     import torch
 
-    from fltee.parallel import DeviceRangeOps, VirtualRanks
+    from fltee.parallel import DeviceRangeOps, VirtualRanks, distributed_network
     rng = np.random.default_rng(m + world)
     idx = rng.integers(0, max(2, m // 8), m).astype(np.uint32)   # heavy ties
     val = np.arange(m, dtype=np.float32)                          # identity tracking
     full = torch.from_numpy(dev.pack_records(idx, val)).cuda()
     C = m // world
     chunks = {r: full[r * C:(r + 1) * C].clone() for r in range(world)}
-    ops, comm = DeviceRangeOps(), VirtualRanks(world)
-    clog, mlog = C.bit_length() - 1, m.bit_length() - 1
-    for r, x in chunks.items():
-        ops.sort(x, r * C)
-    for stage in range(clog + 1, mlog + 1):
-        for j in range(stage - 1, clog - 1, -1):
-            bit = 1 << (j - clog)
-            theirs = comm.swap(chunks, lambda q: q ^ bit)
-            for r, x in chunks.items():
-                ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage)
-        for r, x in chunks.items():
-            ops.merge(x, r * C, stage)
-    got = torch.cat([chunks[r] for r in range(world)]).cpu().numpy()
+    out = distributed_network(chunks, world, m, DeviceRangeOps(), VirtualRanks(world), mode=mode,
+                              seed=0xC0FFEE, exchange="pairwise")
+    got = torch.cat([out[r] for r in range(world)]).cpu().numpy()
     gi, gv = dev.unpack_records(got)
-    ref = oracle.bitonic_sort(oracle.as_weights(idx, val))
+    w = oracle.as_weights(idx, val)
+    ref = oracle.bitonic_sort(w) if mode == 0 else oracle.shuffle_keyed(w, 0xC0FFEE)
     assert np.array_equal(gi, ref["idx"]) and np.array_equal(gv.view(np.uint32), ref["val"].view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_index_sharded_nips19_matches_single_gpu(dev, world):
+    """nips19 by position range == fltee_aggregate_device(nips19) with the same seed:
+    same Laplace counts, same shuffle; the sums are float atomics on both (tolerance)."""
+    import torch
+
+    from fltee.parallel import VirtualRanks, index_sharded_nips19
+    n, d, k, seed = 30, 4000, 400, 1234
+    idx, val = case(7 + world, n, d, k)
+    rec = torch.from_numpy(dev.pack_records(idx, val)).cuda()
+    single = dev.aggregate(2, rec, n, k, d, seed=seed).cpu().numpy()
+    assert dev.status() == 0
+    r, T = dev.laplace_r(d, k, n, seed)
+    tf = int(T)
+    nrec = n * k
+    M = 1 << (nrec + d * tf - 1).bit_length()
+    C = M // world
+    chunks = {q: dev.nips19_build_range(rec[q * C:] if q * C < nrec else rec, nrec, r, d, tf,
+                                        q * C, C) for q in range(world)}
+    out = index_sharded_nips19(chunks, world, M, n, d, seed, comm=VirtualRanks(world)).cpu().numpy()
+    tol = 1e-6 * np.abs(val).max() * (n + 1)
+    assert np.abs(out - single).max() <= tol
 
 
 @pytest.mark.parametrize("exchange", ["transpose", "pairwise"])

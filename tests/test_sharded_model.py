@@ -3,6 +3,7 @@ fltee.parallel with numpy stand-ins for the range pieces, every range in one pro
 (VirtualRanks) — must equal the oracle's single-process `advanced` bit for bit."""
 import numpy as np
 import pytest
+import torch
 
 from range_ops_np import NumpyRangeOps, init_range
 
@@ -32,3 +33,23 @@ def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi, exchange):
     ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
     assert st == 0
     assert np.array_equal(out.numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_virtual_keyed_shuffle_network(oracle, world):
+    """The distributed network in mode 2 (nips19's keyed shuffle) == the oracle's
+    single-array shuffle, bit for bit."""
+    from fltee.parallel import VirtualRanks, distributed_network
+    rng = np.random.default_rng(world)
+    m = 1024
+    idx = rng.integers(0, 50, m).astype(np.uint32)
+    val = np.arange(m, dtype=np.float32)
+    w = oracle.as_weights(idx, val)
+    full = torch.from_numpy(w.view(np.int64).copy())
+    C = m // world
+    chunks = {r: full[r * C:(r + 1) * C].clone() for r in range(world)}
+    out = distributed_network(chunks, world, m, NumpyRangeOps(), VirtualRanks(world), mode=2,
+                              seed=0xC0FFEE)
+    got = torch.cat([out[r] for r in range(world)]).numpy()
+    ref = oracle.shuffle_keyed(w, 0xC0FFEE)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
