@@ -211,6 +211,60 @@ def bench_c5_index_sharded(torch, D, dist, world, rank, device, steps, warmup,
                 value=n * k / wall, unit="client-params/s", scaling="strong")
 
 
+def bench_c4_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
+    """configs[3] (nips19 + DP) by position range ("the same as advanced, the
+    shuffle is a bitonic network"; strong scaling): every rank draws the same Laplace
+    counts (counter-based Philox, no exchange), builds its range of the padded array,
+    the keyed shuffle runs as a distributed network with pairwise RCCL range
+    exchanges, each rank runs safe_aggregate on its range and one RCCL reduce adds the
+    partial sums on rank 0, x 1f32/n, + DP noise (fltee/parallel.py)."""
+    from fltee import parallel as P
+    w = WORKLOADS["c4"]
+    n, d, k, seed = w["n"], w["d"], w["k"], 7
+    nrec = n * k
+    r, T = D.laplace_r(d, k, n, seed, device=device)
+    tf = int(T)
+    M = 1 << (nrec + d * tf - 1).bit_length()
+    C = M // world
+    lo = rank * C
+    cnt = max(1, min(C, nrec - lo))
+    g = torch.Generator(device=device).manual_seed(7000 + rank)
+    p = lo + torch.arange(cnt, device=device, dtype=torch.int64)
+    off = torch.randint(0, d, (n,), generator=g, device=device)
+    idx = (off[torch.clamp(p // k, max=n - 1)] + p % k) % d
+    vals = torch.randn(cnt, generator=g, device=device) * 0.01
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).contiguous()
+    del p, idx, vals
+    chunk = torch.empty(C, dtype=torch.int64, device=device)
+    ops, comm = P.DeviceRangeOps(), P.DistRanks(rank, world)
+    dp = dict(sigma=1.12, clipping=1.0, seed=7)
+
+    def step():
+        D.laplace_r(d, k, n, seed, device=device)  # each call draws its counts (same seed here)
+        D.nips19_build_range(rec, nrec, r, d, tf, lo, C, out=chunk)
+        P.index_sharded_nips19({rank: chunk}, world, M, n, d, seed, ops=ops, comm=comm, dp=dp)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    del rec, chunk, ops
+    wall = float(t[0]) / steps
+    return dict(desc=w["desc"] + f", position-range sharded x{world}: distributed keyed shuffle "
+                "(RCCL pairwise range exchanges) + per-range safe_aggregate + one RCCL reduce",
+                alg="nips19", n=n, d=d, k=k, M=M, range_records=C, ms_per_step=wall * 1e3,
+                value=n * k / wall, unit="client-params/s", scaling="strong")
+
+
 # The reference's own published bench files for one configuration (SURVEY §6,
 # secure_aggregation/results/*-50890-5089-10000-*.txt: d = 50890, k = 5089, 10000 users
 # sampled at 0.3 -> n = 3000; "Aggregation" column, seconds, single-threaded SGX enclave).
@@ -489,6 +543,8 @@ def main():
             sharded["c5_index_sharded_pairwise"] = bench_c5_index_sharded(
                 torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1,
                 exchange="pairwise")
+            sharded["c4_index_sharded"] = bench_c4_index_sharded(
+                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
 
     if rank == 0:
         line = {
