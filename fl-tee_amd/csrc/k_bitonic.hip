@@ -224,9 +224,10 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // (steps 2^(RL-1) .. 1, groups of 2^RL consecutive records) stores its groups straight
 // to HBM instead of writing LDS back for a separate store loop.  Saves
 // one LDS write + read of the tile and two barriers per tile; same network.
-template <int MODE, int E, int NT, int RL>
+template <int MODE, int E, int NT, int RL, bool STRIDED>
 __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
                                                            uint32_t tlog, uint32_t ilog,
+                                                           uint32_t wlog, uint32_t dtile,
                                                            uint32_t seed, uint32_t ntiles,
                                                            uint32_t pbase) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
@@ -237,50 +238,62 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
     if (tile >= ntiles) return;
     const uint32_t t = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
-    const uint32_t voff = t * 8u;
-    constexpr uint32_t rstride = (uint32_t)NT * 8u;
-    const uint32_t dlog1 = tlog - (uint32_t)R1;  // == log2 NT
+    // contiguous: wlog = dtile = tlog.  strided: W = 2^wlog consecutive positions x T/W
+    // rows at stride 2^dtile (W <= NT), as in bitonic_tiles
+    const uint32_t voff = tile_pos(0u, t, wlog, dtile) * 8u;
+    const uint32_t rstride = ((uint32_t)NT << (dtile - wlog)) * 8u;
+    const uint32_t dlog1 = tlog - (uint32_t)R1;  // == log2 NT: the first round's tile-local distance
+    const uint32_t dlog1_g = STRIDED ? dlog1 - wlog + dtile : dlog1;
+    const uint32_t jbot = STRIDED ? wlog : 0u;  // the tile's lowest step
     uint64_t pf[E];
     {
-        const uint32_t sb = (tile << tlog) * 8u;
+        const uint32_t sb = tile_base(tile, tlog, wlog, dtile) * 8u;
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
     for (;;) {
-        const uint32_t base = tile << tlog;
-        group_steps<MODE, R1>(pf, base + pbase + t, dlog1, ilog, seed);
+        const uint32_t base = tile_base(tile, tlog, wlog, dtile);
+        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         {
-            const uint32_t sb = ((next < ntiles ? next : tile) << tlog) * 8u;
+            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) * 8u;
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         }
-        lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, ilog, (int)dlog1 - 1, RL, seed);
+        lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
+                               (int)(jbot + RL), seed);
         constexpr int G = E >> RL;
 #pragma unroll
         for (int h = 0; h < G; ++h) {
-            const uint32_t b = (t + (uint32_t)h * NT) << RL;
+            const uint32_t b = spread(t + (uint32_t)h * NT, jbot, RL);
             uint64_t v[1 << RL];
 #pragma unroll
-            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + (uint32_t)q)];
-            group_steps<MODE, RL>(v, base + pbase + b, 0u, ilog, seed);
-            // 16-B stores.  hipcc (ROCm 7.2) may let the next group's VALU overwrite a
-            // dwordx4 store's data registers one instruction after the store, before the
-            // store has read them (measured: nondeterministic output); the explicit
-            // "s_nop 1" fenced by sched_barriers gives the two wait states the hazard needs
-            // (cdna_hip_programming.md §5.7: dwordx3/x4 stores end with s_nop 1).
+            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + ((uint32_t)q << jbot))];
+            const uint32_t pb = tile_pos(0u, b, wlog, dtile);  // tile-relative position of v[0]
+            group_steps<MODE, RL>(v, base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
+            if (STRIDED) {  // v[q] sits 2^dtile positions after v[q-1]: 8-B stores
 #pragma unroll
-            for (int q = 0; q < (1 << RL); q += 2) {
-                const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
-                                    (uint32_t)(v[q + 1] >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
-                                                       (int)(base * 8u), kTileCP);
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_nop 1" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < (1 << RL); ++q)
+                    bt_store<kTileCP>(rs, (pb + ((uint32_t)q << dtile)) * 8u, base * 8u, v[q]);
+            } else {
+                // 16-B stores.  hipcc (ROCm 7.2) may let the next group's VALU overwrite a
+                // dwordx4 store's data registers one instruction after the store, before the
+                // store has read them (measured: nondeterministic output); the explicit
+                // "s_nop 1" fenced by sched_barriers gives the two wait states the hazard needs
+                // (cdna_hip_programming.md §5.7: dwordx3/x4 stores end with s_nop 1).
+#pragma unroll
+                for (int q = 0; q < (1 << RL); q += 2) {
+                    const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
+                                        (uint32_t)(v[q + 1] >> 32)};
+                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((pb + (uint32_t)q) * 8u),
+                                                           (int)(base * 8u), kTileCP);
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_nop 1" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
         if (next >= ntiles) break;
@@ -495,6 +508,13 @@ struct TileCfg {
     size_t lds;
 };
 
+static bool direct_strided() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_DIRECT_STRIDED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static bool direct_merge() {
     static bool on = [] {
         const char *e = getenv("FLTEE_BITONIC_DIRECT");
@@ -503,23 +523,23 @@ static bool direct_merge() {
     return on;
 }
 
-template <int MODE, int E, int NT>
+template <int MODE, int E, int NT, bool STRIDED>
 static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
-                                uint32_t seed, uint32_t pbase) {
+                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
-    const int rest = (int)c.tlog - R1;         // steps after the register round
+    const int rest = (int)c.tlog - (int)(STRIDED ? wlog : 0u) - R1;  // steps after the register round
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
 #define BD_GO(RL_)                                                                                 \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_merge_direct<MODE, E, NT, RL_>,        \
+            (void)hipFuncSetAttribute((const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_>), dim3(c.grid), dim3(NT), c.lds, \
-                           s, data, c.tlog, ilog, seed, c.tiles, pbase);                           \
+        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED>), dim3(c.grid), dim3(NT), \
+                           c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase);       \
     } while (0)
     switch (rl) {
     case 1: BD_GO(1); break;
@@ -578,10 +598,17 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
     if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
-        if (c.NT == 1024) return launch_direct<MODE, 16, 1024>(c, s, data, ilog, seed, pbase);
-        if (c.E == 32) return launch_direct<MODE, 32, 512>(c, s, data, ilog, seed, pbase);
-        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512>(c, s, data, ilog, seed, pbase);
+        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
+        if (c.E == 32) return launch_direct<MODE, 32, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
+        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
     }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
+    // strided tiles (W consecutive x 2^R rows), the same first / last round in registers
+    if (!SORT && wlog < c.tlog && c.tlog > 6 && direct_strided() &&
+        (int)(c.tlog - wlog) > (c.E >= 32 ? 5 : 4)) {
+        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
+        if (c.E == 32) return launch_direct<MODE, 32, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
+        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
+    }
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
     if (c.NT == 1024) BT_GO(16, 1024);
