@@ -508,10 +508,13 @@ struct TileCfg {
     size_t lds;
 };
 
+// Strided LDS passes with the direct first / last round: measured slower (A/B at 2^27:
+// 14.64 vs 14.03 ms mode 0; the last round's 8-B stores land 2^dtile apart), so off
+// unless FLTEE_BITONIC_DIRECT_STRIDED=1.
 static bool direct_strided() {
     static bool on = [] {
         const char *e = getenv("FLTEE_BITONIC_DIRECT_STRIDED");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
