@@ -477,6 +477,16 @@ static uint32_t min_tiles_log() {
     }();
     return t;
 }
+// Narrowest strided-tile row, log2 (FLTEE_BITONIC_MINW_LOG, default 4 = 16 records =
+// 128-B row segments; smaller allows more steps per strided pass; A/B knob).
+static int min_w_log() {
+    static int w = [] {
+        const char *e = getenv("FLTEE_BITONIC_MINW_LOG");
+        int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : (v > 6 ? 6 : v);
+    }();
+    return w;
+}
 // Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
 // disables them, for A/B runs).
 static bool strided_passes() {
@@ -670,7 +680,7 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, u
                               int jtop, uint32_t seed, uint32_t pbase, hipStream_t s) {
     const int kMaxGlobalR = max_global_r();
     const uint32_t tlog = c.tlog, T = 1u << tlog;
-    const int rs = (int)tlog - 4;  // global steps per strided LDS pass (W >= 16)
+    const int rs = (int)tlog - min_w_log();  // global steps per strided LDS pass (W >= 2^min_w_log)
     const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
     hipError_t e;
     if (nglobal > 0) {
