@@ -85,6 +85,14 @@ hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, 
 // ascending (even segments) / descending (odd segments)
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
                                  hipStream_t s);
+// the sort (mode 0) of advanced's padded array / the keyed shuffle (mode 2) of nips19's,
+// with advanced_init / nips19_build fused into the first pass's loads: data[0, m) gets
+// the result.  hipErrorNotSupported: not fusable at this m (build, then sort).
+hipError_t bitonic_sort_advanced(uint64_t *data, size_t m, const void *rec, size_t nrec, size_t d,
+                                 hipStream_t s);
+hipError_t bitonic_sort_nips19(uint64_t *data, size_t m, uint32_t seed, const void *rec, size_t nrec,
+                               const uint32_t *r, size_t d, size_t tf, hipStream_t s);
+void set_fused_init(int on);
 // one range [pbase, pbase + m) of a larger network (pbase a multiple of m): stages
 // 1..log2 m; the steps j < m of stage ilog; the step 2^jlog >= m of stage ilog
 // between this range and the partner range pos_theirs = pos_mine ^ 2^jlog

@@ -154,8 +154,11 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     const size_t L = n * k + d, M = next_pow2_sz(L);
     const size_t fold_len = n * k_req + d;
     uint64_t *A = (uint64_t *)c->ws_a.ptr, *B = (uint64_t *)c->ws_b.ptr;
-    hipError_t e = launch_advanced_init(rec, n * k, d, M, A, s);
-    if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
+    hipError_t e = bitonic_sort_advanced(A, M, rec, n * k, d, s);  // init fused into the sort
+    if (e == hipErrorNotSupported) {
+        e = launch_advanced_init(rec, n * k, d, M, A, s);
+        if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
+    }
     if (e == hipSuccess) e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
     if (e != hipSuccess) return e;
     // Second sort (advanced.rs:106-111): with fold_len == L its [0, d) prefix is the
@@ -251,8 +254,14 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         uint32_t *r = (uint32_t *)c->ws_r.ptr;
         uint64_t *A = (uint64_t *)c->ws_a.ptr;
         e = launch_laplace_r(d, k, T, seed, r, s);
-        if (e == hipSuccess) e = launch_nips19_build(rec, n * k, r, d, tf, M, A, s);
-        if (e == hipSuccess) e = bitonic_sort(A, M, 2, (uint32_t)(seed ^ (seed >> 32)), s);
+        const uint32_t key = (uint32_t)(seed ^ (seed >> 32));
+        if (e == hipSuccess) {  // build fused into the shuffle's first pass where it can be
+            e = bitonic_sort_nips19(A, M, key, rec, n * k, r, d, tf, s);
+            if (e == hipErrorNotSupported) {
+                e = launch_nips19_build(rec, n * k, r, d, tf, M, A, s);
+                if (e == hipSuccess) e = bitonic_sort(A, M, 2, key, s);
+            }
+        }
         if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
         if (e == hipSuccess) e = launch_safe_aggregate(A, M, d, out, s);
         if (e == hipSuccess && !acc && coef != 1.0f) e = launch_scale(out, d, coef, s);
@@ -506,3 +515,17 @@ extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(
 // A/B hook: 0 runs advanced's second bitonic sort instead of the compaction network
 extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_compaction = on != 0; }
 extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_variant(v); }
+extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
+// test hook: the fused-producer sort alone (gen 1: advanced, 2: nips19 with key seed),
+// into d_data[0, m); INVALID_PARAMETER when m is too small to fuse
+extern "C" fltee_status_t fltee_debug_sort_fused(uint32_t gen, void *d_data, size_t m,
+                                                 const void *d_rec, size_t nrec, const uint32_t *d_r,
+                                                 size_t d, size_t tf, uint32_t seed, void *stream) {
+    hipError_t e;
+    if (gen == 1) e = fltee::bitonic_sort_advanced((uint64_t *)d_data, m, d_rec, nrec, d, (hipStream_t)stream);
+    else if (gen == 2)
+        e = fltee::bitonic_sort_nips19((uint64_t *)d_data, m, seed, d_rec, nrec, d_r, d, tf, (hipStream_t)stream);
+    else return FLTEE_ERROR_INVALID_PARAMETER;
+    if (e == hipErrorNotSupported || e == hipErrorInvalidValue) return FLTEE_ERROR_INVALID_PARAMETER;
+    return e == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+}

@@ -323,15 +323,40 @@ __device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32
     }
 }
 
+// Producers fused into a sort's first pass (GEN != 0): the tile loads read the client
+// records from `rec` and synthesize the padded entries in registers, so the padded
+// array is never written by a separate init kernel and read back (one HBM pass less).
+//   GEN 1: advanced_init (advanced.rs:116-142): records ++ (i, +0.0) for i < d ++
+//          (u32::MAX, +0.0) pads
+//   GEN 2: nips19_build (nips19.rs:18-63, common.rs:189-197): records ++ entry e =
+//          i*tf + j of the d*tf dummies ((r_i < j) ? i : u32::MAX, +0.0) ++ pads
+// Same entries as advanced_init_kernel / nips19_build_kernel, position for position.
+struct SortGen {
+    const uint64_t *rec;  // the record at global position p is rec[p - pbase] (p < nrec)
+    const uint32_t *r;    // GEN 2: Laplace counts r_i
+    uint32_t nrec, d, tf;
+};
+template <int GEN>
+__device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint64_t v) {
+    if (p < g.nrec) return v;
+    const uint32_t e = p - g.nrec;
+    if (GEN == 1) return e < g.d ? (uint64_t)e : 0xFFFFFFFFull;
+    if (g.tf == 0) return 0xFFFFFFFFull;
+    const uint32_t i = e / g.tf, j = e - i * g.tf;
+    if (i >= g.d) return 0xFFFFFFFFull;
+    return g.r[i] < j ? (uint64_t)i : 0xFFFFFFFFull;  // o_setb / o_mov, as in the build kernel
+}
+
 // The first pass of a sort (stages 1..T of every contiguous tile) with its first and
 // last work in registers: lane t loads records tE .. tE+E-1 (16-B loads), runs stages
 // 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
 // log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
 // stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
-template <int MODE, int E, int NT, int RL>
+template <int MODE, int E, int NT, int RL, int GEN = 0>
 __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t seed,
-                                                          uint32_t ntiles, uint32_t pbase) {
+                                                          uint32_t ntiles, uint32_t pbase,
+                                                          SortGen g) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     static_assert((1 << R1) == E && RL >= 1 && RL <= R1, "tile shape");
@@ -339,16 +364,37 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
     if (tile >= ntiles) return;
     const uint32_t t = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
+    // GEN: loads come from rec, range-checked to its nloc records from pbase (beyond:
+    // zeros, replaced by gen_entry)
+    uint32_t nloc = 0;
+    if (GEN) {
+        nloc = g.nrec > pbase ? g.nrec - pbase : 0u;
+        const uint32_t m = ntiles << tlog;
+        if (nloc > m) nloc = m;
+    }
+    const uint64_t lbytes = (uint64_t)nloc * 8u;
+    const __amdgpu_buffer_rsrc_t ls =
+        GEN ? __builtin_amdgcn_make_buffer_rsrc((void *)g.rec, (short)0,
+                                                (int)(lbytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)lbytes),
+                                                0x00020000)
+            : rs;
     const uint32_t voff = t * (uint32_t)E * 8u;
     uint64_t pf[E];
     auto load = [&](uint32_t tl) {
         const uint32_t sb = (tl << tlog) * 8u;
 #pragma unroll
         for (int r = 0; r < E; r += 2) {
-            const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + (uint32_t)r * 8u),
+            const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ls, (int)(voff + (uint32_t)r * 8u),
                                                                       (int)sb, kTileCP);
             pf[r] = ((uint64_t)x.y << 32) | x.x;
             pf[r + 1] = ((uint64_t)x.w << 32) | x.z;
+            if (GEN) {
+                const uint32_t xl = (tl << tlog) + t * (uint32_t)E + (uint32_t)r;  // local index of pf[r]
+                if (xl + 1u == nloc)  // the 16-B load straddles the end of rec: reload 8 B
+                    pf[r] = bt_load<kTileCP>(ls, voff + (uint32_t)r * 8u, sb);
+                pf[r] = gen_entry<GEN>(g, pbase + xl, pf[r]);
+                pf[r + 1] = gen_entry<GEN>(g, pbase + xl + 1u, pf[r + 1]);
+            }
         }
     };
     load(tile);
@@ -565,21 +611,21 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     return hipGetLastError();
 }
 
-template <int MODE, int E, int NT>
+template <int MODE, int E, int NT, int GEN = 0>
 static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
-                                     uint32_t seed, uint32_t pbase) {
+                                     uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{}) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
 #define BS_GO(RL_)                                                                                 \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_>,         \
+            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN>,    \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_>), dim3(c.grid), dim3(NT), c.lds,  \
-                           s, data, c.tlog, seed, c.tiles, pbase);                                 \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN>), dim3(c.grid), dim3(NT),   \
+                           c.lds, s, data, c.tlog, seed, c.tiles, pbase, g);                       \
     } while (0)
     switch (rl) {
     case 1: BS_GO(1); break;
@@ -793,6 +839,48 @@ hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t 
     case 1: return sort_impl<1>(data, m, 0, s, slog, 0u);
     default: return sort_impl<2>(data, m, 0, s, slog, 0u);
     }
+}
+
+// ------------------------------------------- sorts with a fused producer ---
+// The sort of the padded array that `g` describes (GEN 1: advanced's, 2: nips19's),
+// written into data[0, m): the producer runs inside the first pass's loads.
+// hipErrorNotSupported when that pass is not the direct tile sort (small m, knob
+// off): the caller then builds the array and sorts it.
+static bool g_fused_init = true;  // fltee_debug_set_fused_init (A/B)
+void set_fused_init(int on) { g_fused_init = on != 0; }
+
+template <int MODE, int GEN>
+static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const SortGen &g,
+                                hipStream_t s) {
+    if (!g_fused_init || m < 2 || m > ((size_t)1 << 29)) return hipErrorNotSupported;
+    const uint32_t mlog = log2_pow2(m);
+    const TileCfg c = make_cfg(mlog, mlog);
+    if (c.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
+    hipError_t e;
+    if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
+    else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, g);
+    else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, g);
+    else return hipErrorNotSupported;
+    if (e != hipSuccess) return e;
+    for (uint32_t ilog = c.tlog + 1; ilog <= mlog; ++ilog) {
+        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, 0u, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t bitonic_sort_advanced(uint64_t *data, size_t m, const void *rec, size_t nrec, size_t d,
+                                 hipStream_t s) {
+    if (nrec + d > m) return hipErrorInvalidValue;
+    const SortGen g{(const uint64_t *)rec, nullptr, (uint32_t)nrec, (uint32_t)d, 0u};
+    return sort_gen_impl<0, 1>(data, m, 0u, g, s);
+}
+
+hipError_t bitonic_sort_nips19(uint64_t *data, size_t m, uint32_t seed, const void *rec, size_t nrec,
+                               const uint32_t *r, size_t d, size_t tf, hipStream_t s) {
+    if (nrec + d * tf > m) return hipErrorInvalidValue;
+    const SortGen g{(const uint64_t *)rec, r, (uint32_t)nrec, (uint32_t)d, (uint32_t)tf};
+    return sort_gen_impl<2, 2>(data, m, seed, g, s);
 }
 
 // ---------------------------------------------- position-range pieces -----

@@ -100,10 +100,10 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 
     // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
     const uint32_t part = (l & 7) * 2;
-    // prefetch DEPTH stages ahead (DEPTH 2: pa / pb alternate).  Two help when there are
-    // few waves (small m: the load latency sets the time); one is faster at full chip
-    // occupancy (C5: 692 vs 741 us).
-    fs_u32x4 pa[8], pb[8];
+    // prefetch DEPTH stages ahead (pf[s % DEPTH] holds stage s).  Deeper prefetch helps
+    // when there are few waves (small m, or long chunks: the load latency sets the time);
+    // one is faster at full chip occupancy (C5 at C = 1024: 692 vs 741 us for two).
+    fs_u32x4 pf[DEPTH][8];
     auto load_stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -116,8 +116,9 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             }
         }
     };
-    load_stage(pa, 0);
-    if (DEPTH == 2 && 1 < nstage) load_stage(pb, 1);
+#pragma unroll
+    for (int q = 0; q < DEPTH; ++q)
+        if ((uint32_t)q < nstage) load_stage(pf[q], (uint32_t)q);
 
     uint32_t pre_idx = 0;
     float pre_val = 0.0f;
@@ -174,17 +175,20 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         }
         wave_sync_lds();
     };
-    if (DEPTH == 2) {
-        for (uint32_t s = 0; s < nstage; s += 2) {
-            stage(pa, s);
-            if (s + 1 < nstage) stage(pb, s + 1);
-        }
-    } else {
-        for (uint32_t s = 0; s < nstage; ++s) stage(pa, s);
+    for (uint32_t s = 0; s < nstage; s += DEPTH) {
+#pragma unroll
+        for (int q = 0; q < DEPTH; ++q)
+            if (s + (uint32_t)q < nstage) stage(pf[q], s + (uint32_t)q);
     }
 }
 
 size_t fold_context(size_t halo) { return (halo + FS_W - 1) / FS_W * FS_W; }
+
+// A/B knobs (read once per process; 0 = the measured default)
+static int fold_knob(const char *name) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : 0;
+}
 
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
@@ -196,17 +200,25 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     size_t C = 64;
     while (C < Hr) C <<= 1;
     while (C > 64 && span / (64 * C) < 1024) C >>= 1;  // keep >= ~1024 waves when halo allows
+    // one doubling more while >= 1024 waves remain: less halo re-read (C5: 2048 instead
+    // of 1024, 620 vs 643 us; 4096: 700 us, 8192: 1220 us — too few waves in flight)
+    if (C >= Hr && span / (64 * 2 * C) >= 1024) C <<= 1;
+    static const int clog = fold_knob("FLTEE_FOLD_CLOG");  // A/B: chunks of 2^clog records
+    if (clog >= 6 && clog <= 20) C = (size_t)1 << clog;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    if (blocks <= 256)  // about one wave per CU: latency-bound, prefetch deeper
-        hipLaunchKernelGGL(fold_stream_kernel<2>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
-                           (long long)m, (long long)origin, (long long)end, pbase,
-                           (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
-    else
-        hipLaunchKernelGGL(fold_stream_kernel<1>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,
-                           (long long)m, (long long)origin, (long long)end, pbase,
-                           (long long)fold_len, (uint32_t)Hr, (uint32_t)C, status);
+    int depth = blocks <= 256 ? 2 : 1;  // about one wave per CU: latency-bound, prefetch deeper
+    static const int dk = fold_knob("FLTEE_FOLD_DEPTH");
+    if (dk == 1 || dk == 2 || dk == 4) depth = dk;
+#define FS_GO(D_)                                                                                  \
+    hipLaunchKernelGGL(fold_stream_kernel<D_>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,   \
+                       (long long)m, (long long)origin, (long long)end, pbase, (long long)fold_len, \
+                       (uint32_t)Hr, (uint32_t)C, status)
+    if (depth == 4) FS_GO(4);
+    else if (depth == 2) FS_GO(2);
+    else FS_GO(1);
+#undef FS_GO
     return hipGetLastError();
 }
 

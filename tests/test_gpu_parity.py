@@ -172,6 +172,39 @@ def test_composite_key_sort(dev):
     assert np.array_equal(t.cpu().numpy(), np.sort(keys))
 
 
+# ------------------------------------------------- fused producers ---------
+@pytest.mark.parametrize("gen", [1, 2])
+@pytest.mark.parametrize("nrec,d", [(1_500_001, 200_000), (999_999, 1_200_000), (3_000_000, 100)])
+def test_sort_fused_producer_equals_build_then_sort(dev, gen, nrec, d):
+    """advanced_init (gen 1) / nips19_build (gen 2) fused into the sort's first pass ==
+    the build kernel, then the sort, bit for bit (M >= 2^21, where the fusion applies;
+    odd record counts exercise the 16-B load straddling the end of the records)."""
+    import torch
+
+    from fltee import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(nrec + d)
+    idx = torch.randint(0, d + 10, (nrec,), generator=g, device="cuda")
+    vbits = torch.randint(0, 1 << 31, (nrec,), generator=g, device="cuda")
+    rec = (idx | (vbits << 32)).contiguous()
+    if gen == 1:
+        tf, key, r = 0, 0, None
+        M = 1 << (nrec + d - 1).bit_length()
+        ref = dev.advanced_init_range(rec, nrec, d, 0, M)
+        dev.bitonic(ref, 0, 0)
+    else:
+        r, T = dev.laplace_r(d, 50, 100, seed=nrec)
+        tf, key = int(T), 0x5EED ^ nrec
+        M = 1 << (nrec + d * tf - 1).bit_length()
+        ref = dev.nips19_build_range(rec, nrec, r, d, tf, 0, M)
+        dev.bitonic(ref, 2, key)
+    out = torch.empty(M, dtype=torch.int64, device="cuda")
+    st = L.lib().fltee_debug_sort_fused(gen, out.data_ptr(), M, rec.data_ptr(), nrec,
+                                        r.data_ptr() if r is not None else None, d, tf, key, None)
+    torch.cuda.synchronize()
+    assert st == 0
+    assert torch.equal(out, ref)
+
+
 # -------------------------------------------------------------- fold -------
 @pytest.mark.parametrize("n,d,k", [(3, 200, 50), (100, 5000, 500), (40, 70000, 7000)])
 def test_fold_bit_exact(dev, oracle, n, d, k):
