@@ -21,7 +21,8 @@
 // with a larger halo.  Every lane performs the same Hr+C+16 steps whatever the
 // data (oblivious).
 //
-// Layout: C >= Hr (halo work <= 2x), so a lane walks a long chunk; the 64
+// Layout: C >= Hr on large arrays (halo work <= 2x; small arrays take shorter
+// chunks, down to 16, to keep ~1024 waves in flight), so a lane walks a long chunk; the 64
 // lanes of a wave walk 64 chunks in lockstep, 16 records per stage.  A stage's
 // 64 windows of 16 records (128 B each) are loaded coalesced (8 lanes per
 // window) one stage ahead into registers, transposed through LDS (row stride
@@ -199,12 +200,14 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     const size_t span = end - origin;
     size_t C = 64;
     while (C < Hr) C <<= 1;
-    while (C > 64 && span / (64 * C) < 1024) C >>= 1;  // keep >= ~1024 waves when halo allows
+    // keep >= ~1024 waves: shorter chunks re-read more halo but put more loads in flight
+    // (C3, M = 2^20, Hr = 112: C = 16 gives 19.7 us against 25.5 us at C = 64)
+    while (C > FS_W && span / (64 * C) < 1024) C >>= 1;
     // one doubling more while >= 1024 waves remain: less halo re-read (C5: 2048 instead
     // of 1024, 620 vs 643 us; 4096: 700 us, 8192: 1220 us — too few waves in flight)
     if (C >= Hr && span / (64 * 2 * C) >= 1024) C <<= 1;
     static const int clog = fold_knob("FLTEE_FOLD_CLOG");  // A/B: chunks of 2^clog records
-    if (clog >= 6 && clog <= 20) C = (size_t)1 << clog;
+    if (clog >= 4 && clog <= 20) C = (size_t)1 << clog;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
