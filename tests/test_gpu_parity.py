@@ -174,7 +174,8 @@ def test_composite_key_sort(dev):
 
 # ------------------------------------------------- fused producers ---------
 @pytest.mark.parametrize("gen", [1, 2])
-@pytest.mark.parametrize("nrec,d", [(1_500_001, 200_000), (999_999, 1_200_000), (3_000_000, 100)])
+@pytest.mark.parametrize("nrec,d", [(1_500_001, 200_000), (999_999, 1_200_000), (3_000_000, 100),
+                                    (0, 1_500_000)])
 def test_sort_fused_producer_equals_build_then_sort(dev, gen, nrec, d):
     """advanced_init (gen 1) / nips19_build (gen 2) fused into the sort's first pass ==
     the build kernel, then the sort, bit for bit (M >= 2^21, where the fusion applies;
@@ -203,6 +204,29 @@ def test_sort_fused_producer_equals_build_then_sort(dev, gen, nrec, d):
     torch.cuda.synchronize()
     assert st == 0
     assert torch.equal(out, ref)
+
+
+def test_optimized_fused_producer_unaligned_batches(dev):
+    """alg 6 batches start at rec + c0*k*8: with k odd every other batch is only 8-B
+    aligned, and the fused first pass reads it with 16-B loads (M = 2^21 per batch).
+    Same bits as the separate init kernel."""
+    import torch
+
+    from fltee import _lib as L
+    n, d, k = 2, 2_000_000, 1_500_001
+    g = torch.Generator(device="cuda").manual_seed(61)
+    idx = torch.cat([torch.randperm(d, generator=g, device="cuda")[:k] for _ in range(n)])
+    vals = torch.randn(n * k, generator=g, device="cuda")
+    rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).contiguous()
+    try:
+        a = dev.aggregate(6, rec, n, k, d, batch=1).cpu().numpy()
+        assert dev.status() == 0
+        L.lib().fltee_debug_set_fused_init(0)
+        b = dev.aggregate(6, rec, n, k, d, batch=1).cpu().numpy()
+        assert dev.status() == 0
+    finally:
+        L.lib().fltee_debug_set_fused_init(1)
+    assert bits_equal(a, b)
 
 
 # -------------------------------------------------------------- fold -------
