@@ -84,7 +84,8 @@ hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, 
     return launch_nips19_build_range(rec, nrec, r, d, tf, 0, m, dst, s);
 }
 
-constexpr uint32_t SA_SEG = 32768;  // floats per LDS segment (128 KB)
+constexpr uint32_t SA_SEG = 32768;      // floats per LDS segment (128 KB)
+constexpr uint32_t SA_SEG_MAX = 40960;  // the whole 160 KB of LDS
 constexpr uint32_t SA_CHUNKS = 256;
 
 // VEC: src 16-B aligned, chunks read as record pairs, SA_U pair loads in flight per
@@ -92,17 +93,20 @@ constexpr uint32_t SA_CHUNKS = 256;
 // 0.69 ms for C4's 1 GB).
 constexpr int SA_U = 4;
 typedef unsigned int sa_u32x4 __attribute__((ext_vector_type(4)));
-template <bool VEC>
+// TAILG: one LDS segment [0, segsz) and the few indices in [segsz, d) go straight to
+// global atomics, so the array is read once (C4, d = 44,964: two 32K segments read it
+// twice from HBM, both blocks of a chunk running at the same time).
+template <bool VEC, bool TAILG>
 __global__ __launch_bounds__(1024) void safe_aggregate_kernel(const uint2 *__restrict__ src,
-                                                              size_t m, size_t d,
+                                                              size_t m, size_t d, uint32_t segsz,
                                                               float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float acc[];
     // 1-D grid, segment fastest: the blocks of every segment of one chunk are dispatched
     // back to back, so all but the first read that chunk from the Infinity Cache
-    const uint32_t nseg = (uint32_t)((d + SA_SEG - 1) / SA_SEG);
+    const uint32_t nseg = TAILG ? 1u : (uint32_t)((d + segsz - 1) / segsz);
     const uint32_t seg = blockIdx.x % nseg, chunk = blockIdx.x / nseg, nchunks = gridDim.x / nseg;
-    const size_t seg_lo = (size_t)seg * SA_SEG;
-    const uint32_t seg_n = (uint32_t)((d - seg_lo) < SA_SEG ? (d - seg_lo) : SA_SEG);
+    const size_t seg_lo = (size_t)seg * segsz;
+    const uint32_t seg_n = (uint32_t)((d - seg_lo) < segsz ? (d - seg_lo) : segsz);
     for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) acc[e] = 0.0f;
     __syncthreads();
     const size_t per = ((m + nchunks - 1) / nchunks + 1) & ~(size_t)1;  // even: pairs
@@ -111,6 +115,7 @@ __global__ __launch_bounds__(1024) void safe_aggregate_kernel(const uint2 *__res
     auto add = [&](uint32_t idx, uint32_t val) {
         const uint32_t rel = idx - (uint32_t)seg_lo;
         if (idx < d && rel < seg_n) atomicAdd(&acc[rel], __uint_as_float(val));
+        else if (TAILG && idx < d) atomicAdd(&out[idx], __uint_as_float(val));
     };
     size_t p = lo + threadIdx.x;
     if (VEC) {
@@ -147,23 +152,28 @@ hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float 
     if (d == 0 || m == 0) return hipSuccess;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)safe_aggregate_kernel<true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, SA_SEG * 4);
-        (void)hipFuncSetAttribute((const void *)safe_aggregate_kernel<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, SA_SEG * 4);
+        const void *k[4] = {(const void *)safe_aggregate_kernel<true, false>,
+                            (const void *)safe_aggregate_kernel<false, false>,
+                            (const void *)safe_aggregate_kernel<true, true>,
+                            (const void *)safe_aggregate_kernel<false, true>};
+        for (const void *f : k)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, SA_SEG_MAX * 4);
         attr = true;
     }
-    const unsigned segs = (unsigned)((d + SA_SEG - 1) / SA_SEG);
+    // d a little above one 32K segment: one 40K segment + global atomics for the rest
+    const bool tailg = d > SA_SEG && d <= SA_SEG_MAX + SA_SEG_MAX / 8;
+    const uint32_t segsz = tailg ? SA_SEG_MAX : SA_SEG;
+    const unsigned segs = tailg ? 1u : (unsigned)((d + segsz - 1) / segsz);
     size_t chunks = (m + 8191) / 8192;
     if (chunks > SA_CHUNKS) chunks = SA_CHUNKS;
-    const size_t lds = (d < SA_SEG ? d : SA_SEG) * 4;
+    const size_t lds = (d < segsz ? d : segsz) * 4;
     const bool vec = ((uintptr_t)src & 15) == 0;
-    if (vec)
-        hipLaunchKernelGGL(safe_aggregate_kernel<true>, dim3((unsigned)(chunks * segs)), dim3(1024),
-                           lds, s, (const uint2 *)src, m, d, out);
-    else
-        hipLaunchKernelGGL(safe_aggregate_kernel<false>, dim3((unsigned)(chunks * segs)), dim3(1024),
-                           lds, s, (const uint2 *)src, m, d, out);
+    const dim3 grid((unsigned)(chunks * segs));
+    const uint2 *s2 = (const uint2 *)src;
+    if (vec && tailg) hipLaunchKernelGGL((safe_aggregate_kernel<true, true>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
+    else if (vec) hipLaunchKernelGGL((safe_aggregate_kernel<true, false>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
+    else if (tailg) hipLaunchKernelGGL((safe_aggregate_kernel<false, true>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
+    else hipLaunchKernelGGL((safe_aggregate_kernel<false, false>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
     return hipGetLastError();
 }
 

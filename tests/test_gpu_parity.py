@@ -391,6 +391,27 @@ def test_nips19_close_to_oracle(dev, oracle):
     assert np.abs(out - ref).max() <= tol and np.abs(out - inorder).max() <= tol
 
 
+@pytest.mark.parametrize("d", [1000, 32768, 40000, 44964, 46080, 46081, 100000])
+@pytest.mark.parametrize("odd", [False, True])
+def test_safe_aggregate_matches_numpy(dev, d, odd):
+    """safe_aggregate (common.rs:25-35) on a shuffled-like array: g[idx] += val for idx < d,
+    every segment layout (one LDS segment, one 40K segment + global-atomic tail, several
+    segments) and an unaligned start (8-B aligned: the 8-B load path); fp32 tolerance."""
+    import torch
+    m = (1 << 20) + (1 if odd else 0)
+    g = torch.Generator(device="cuda").manual_seed(d)
+    idx = torch.randint(0, d + 100, (m,), generator=g, device="cuda")
+    vals = torch.randn(m, generator=g, device="cuda")
+    buf = (idx | (vals.view(torch.int32).to(torch.int64) << 32))
+    src = torch.cat([torch.zeros(1, dtype=torch.int64, device="cuda"), buf])[1:] if odd else buf
+    out = dev.safe_aggregate(src, d).cpu().numpy()
+    i, v = idx.cpu().numpy(), vals.cpu().numpy().astype(np.float64)
+    ref = np.zeros(d, np.float64)
+    sel = i < d
+    np.add.at(ref, i[sel], v[sel])
+    assert np.abs(out - ref).max() <= 1e-3
+
+
 # --------------------------------------------------------------- DP --------
 def test_dp_noise_statistics(dev):
     import torch
