@@ -165,7 +165,10 @@ static int compact_blocks() {
     }();
     return b;
 }
-static int g_compact_variant = 1;  // fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB
+// fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB tiles
+// (1024 lanes x 8), 2 = 32 KiB first pass + 64 KiB strided passes (1024 lanes x 8, one
+// block per CU: 6 levels per pass, 4 passes instead of 5 at C5; 512 x 16 spills)
+static int g_compact_variant = 1;
 void set_compact_variant(int v) { g_compact_variant = v; }
 
 template <int NT, int PER, int MINB = 1>
@@ -202,10 +205,10 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
     const uint32_t nlev = bitlen(max_shift);
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
     if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets
-    const bool small = g_compact_variant == 1;
-    const uint32_t CAP = small ? 4096 : 8192;
     uint64_t *cur = src, *oth = tmp;
     for (uint32_t j0 = 0; j0 < nlev;) {
+        const bool small = g_compact_variant == 1 || (g_compact_variant == 2 && j0 == 0);
+        const uint32_t CAP = small ? 4096 : 8192;
         const uint32_t gmax = j0 == 0 ? (small ? 9 : 10) : (small ? 5 : 6);
         const uint32_t G = min(gmax, nlev - j0), H = (1u << G) - 1;
         const uint64_t rows64 = (L + ((uint64_t)1 << j0) - 1) >> j0;

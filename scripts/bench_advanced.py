@@ -32,7 +32,7 @@ def main():
     rec = bench.make_records(torch, n, d, k, 11, "cuda")
     out = torch.empty(d, dtype=torch.float32, device="cuda")
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
-    variants = {"compact64k": (1, 0), "compact32k": (1, 1), "sort": (0, 0)}
+    variants = {"compact64k": (1, 0), "compact32k": (1, 1), "compact32k_64k": (1, 2), "sort": (0, 0)}
     times = {v: [] for v in variants}
     ref = None
     try:
