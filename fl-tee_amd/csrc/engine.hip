@@ -521,6 +521,7 @@ extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); 
 extern "C" fltee_status_t fltee_debug_sort_fused(uint32_t gen, void *d_data, size_t m,
                                                  const void *d_rec, size_t nrec, const uint32_t *d_r,
                                                  size_t d, size_t tf, uint32_t seed, void *stream) {
+    if (!d_data || (nrec && !d_rec) || (gen == 2 && d && tf && !d_r)) return FLTEE_ERROR_INVALID_PARAMETER;
     hipError_t e;
     if (gen == 1) e = fltee::bitonic_sort_advanced((uint64_t *)d_data, m, d_rec, nrec, d, (hipStream_t)stream);
     else if (gen == 2)
