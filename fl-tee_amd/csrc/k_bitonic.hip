@@ -513,6 +513,15 @@ static bool tile32() {
     }();
     return on;
 }
+// First pass only: 512 lanes x 32 records for the 2^14 tiles (5 stages in registers,
+// 5 steps per LDS round) while the merges keep 1024 x 16 (FLTEE_BITONIC_SORT32=1, A/B).
+static bool sort32() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_SORT32");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 // Smaller tiles until there are at least 2^mt of them (FLTEE_BITONIC_MINTILES_LOG,
 // default 8 = 256 tiles, one per CU; for A/B runs).
 static uint32_t min_tiles_log() {
@@ -563,6 +572,11 @@ struct TileCfg {
     unsigned tiles, grid;
     size_t lds;
 };
+static TileCfg as_e32(TileCfg c) {
+    c.E = 32;
+    c.NT = 512;
+    return c;
+}
 
 // Strided LDS passes with the direct first / last round: measured slower (A/B at 2^27:
 // 14.64 vs 14.03 ms mode 0; the last round's 8-B stores land 2^dtile apart), so off
@@ -650,6 +664,7 @@ template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
     if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
+        if (c.NT == 1024 && sort32()) return launch_sort_direct<MODE, 32, 512>(as_e32(c), s, data, seed, pbase);
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
         if (c.E == 32) return launch_sort_direct<MODE, 32, 512>(c, s, data, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
@@ -857,7 +872,8 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     const TileCfg c = make_cfg(mlog, mlog);
     if (c.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
     hipError_t e;
-    if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
+    if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, g);
+    else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
     else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, g);
     else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, g);
     else return hipErrorNotSupported;
