@@ -179,6 +179,84 @@ __global__ __launch_bounds__(256) void dense_accumulate_r(const uint2 *__restric
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
 
+// Small d (MLP-MNIST, d = 50,890): one lane per output pair leaves most CUs idle and
+// each lane's U-client batches run back to back (latency-bound, 19 us for 100 clients).
+// Here a block of 256 lanes owns DS_OB outputs and stages DS_CC clients of them at a
+// time through LDS: every lane issues its share of the chunk's loads at once (next chunk
+// in flight while the current one is summed), then lanes < DS_OB sum their output over
+// the chunk's clients in client order from LDS.  Same adds in the same order as
+// dense_accumulate_v: bit-identical.
+constexpr int DS_NT = 256;
+
+template <bool VEC, bool CLIP, bool ACC, int DS_OB = 128, int DS_CC = 32>
+__global__ __launch_bounds__(DS_NT) void dense_accumulate_lds(const uint2 *__restrict__ rec, size_t d,
+                                                              uint32_t n, float coef,
+                                                              float *__restrict__ out,
+                                                              const float *__restrict__ ccoef,
+                                                              uint32_t *status) {
+    constexpr int DS_LD = DS_OB * DS_CC / 2 / DS_NT;  // 16-B loads per lane per chunk
+    static_assert(DS_LD >= 1 && DS_LD * 2 * DS_NT == DS_OB * DS_CC && DS_OB <= DS_NT, "shape");
+    __shared__ uint4 buf[2][DS_CC][DS_OB / 2];  // record pairs (conflict-free 16-B writes)
+    const uint32_t t = threadIdx.x;
+    const size_t j0 = (size_t)blockIdx.x * DS_OB;
+    const uint32_t nch = (n + DS_CC - 1) / DS_CC;
+    // lane t, load i: client cl = q / (DS_OB/2), pair pr = q % (DS_OB/2), q = t + i*DS_NT
+    uint4 r[DS_LD];
+    auto load = [&](uint32_t ch) {
+#pragma unroll
+        for (int i = 0; i < DS_LD; ++i) {
+            const uint32_t q = t + (uint32_t)i * DS_NT;
+            const uint32_t cl = q / (DS_OB / 2), pr = q % (DS_OB / 2);
+            const uint32_t c = ch * DS_CC + cl;
+            const size_t j = j0 + 2 * pr;
+            uint4 x = make_uint4(0u, 0u, 0u, 0u);
+            if (c < n) {
+                const uint2 *p = rec + (size_t)c * d + j;
+                if (VEC) {
+                    if (j < d) x = ld_nt(reinterpret_cast<const uint4 *>(p));  // d even: j+1 < d too
+                } else {
+                    if (j < d) { const uint2 a = ld_nt(p); x.x = a.x; x.y = a.y; }
+                    if (j + 1 < d) { const uint2 b = ld_nt(p + 1); x.z = b.x; x.w = b.y; }
+                }
+            }
+            r[i] = x;
+        }
+    };
+    auto stash = [&](int b) {
+#pragma unroll
+        for (int i = 0; i < DS_LD; ++i) {
+            const uint32_t q = t + (uint32_t)i * DS_NT;
+            const uint32_t cl = q / (DS_OB / 2), pr = q % (DS_OB / 2);
+            buf[b][cl][pr] = r[i];
+        }
+    };
+    float acc = 0.0f;
+    uint32_t bad = 0;
+    const size_t j = j0 + t;
+    load(0);
+    stash(0);
+    __syncthreads();
+    for (uint32_t ch = 0; ch < nch; ++ch) {
+        if (ch + 1 < nch) load(ch + 1);
+        if (t < DS_OB && j < d) {
+            const uint32_t cend = n - ch * DS_CC < DS_CC ? n - ch * DS_CC : DS_CC;
+            for (uint32_t cl = 0; cl < cend; ++cl) {
+                const uint2 x = reinterpret_cast<const uint2 *>(buf[ch & 1][cl])[t];
+                float a = __uint_as_float(x.y);
+                if (CLIP) a = __fmul_rn(a, ccoef[ch * DS_CC + cl]);
+                acc = __fadd_rn(acc, a);
+                bad |= x.x ^ (uint32_t)j;
+            }
+        }
+        if (ch + 1 < nch) stash((ch + 1) & 1);
+        __syncthreads();
+    }
+    if (t < DS_OB && j < d) {
+        out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+        if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+    }
+}
+
 // Tuning hook (fltee_debug_set_dense_variant): 0 is the shipped configuration.
 static int g_dense_variant = 0;
 
@@ -196,10 +274,34 @@ static void launch_r(const void *rec, size_t n, size_t d, float coef, float *out
                        0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
 }
 
+template <bool CLIP, bool ACC, int OB, int CC>
+static void launch_lds(bool vec, const void *rec, size_t n, size_t d, float coef, float *out,
+                       const float *ccoef, uint32_t *status, hipStream_t s) {
+    const unsigned blocks = (unsigned)((d + OB - 1) / OB);
+    if (vec)
+        hipLaunchKernelGGL((dense_accumulate_lds<true, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0, s,
+                           (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
+    else
+        hipLaunchKernelGGL((dense_accumulate_lds<false, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0,
+                           s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
+}
+
 template <bool CLIP, bool ACC>
 static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef, float *out,
                                  const float *ccoef, uint32_t *status, hipStream_t s) {
     const bool aligned = ((uintptr_t)rec % 16 == 0) && ((uintptr_t)out % 8 == 0) && (d % 2 == 0);
+    if (d < ((size_t)1 << 18) && n > 1 && (g_dense_variant == 0 || g_dense_variant >= 20)) {
+        // small d: LDS-staged chunks (variants 20-23: other block shapes, A/B)
+        const bool vec = ((uintptr_t)rec % 16 == 0) && (d % 2 == 0);
+        switch (g_dense_variant) {
+        case 20: launch_lds<CLIP, ACC, 64, 32>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        case 21: launch_lds<CLIP, ACC, 128, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        case 22: launch_lds<CLIP, ACC, 256, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        case 23: launch_lds<CLIP, ACC, 64, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        default: launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        }
+        return hipGetLastError();
+    }
     if (aligned) {
         const size_t d2 = d / 2;
         switch (g_dense_variant) {

@@ -15,7 +15,9 @@ sys.path.insert(0, ROOT)
 VARIANTS = {0: "V1 U16 nt 512 lanes (shipped)", 1: "V1 U8 nt", 2: "V1 U32 nt", 3: "V2 U8 nt", 4: "V2 U16 nt",
             5: "V1 U16 plain", 6: "V4 U4 nt", 7: "V4 U8 nt", 8: "= variant 0",
             9: "V1 U16 nt 128 lanes", 10: "8 B/lane U16", 11: "8 B/lane U32", 12: "V1 U16 nt 64 lanes",
-            13: "V1 U16 nt 256 lanes (round-1 default)"}
+            13: "V1 U16 nt 256 lanes (round-1 default)",
+            20: "small d: LDS 64 outputs x 32 clients", 21: "small d: LDS 128 x 16",
+            22: "small d: LDS 256 x 16", 23: "small d: LDS 64 x 16"}
 
 
 def main():

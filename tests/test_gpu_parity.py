@@ -45,7 +45,8 @@ def bits_equal(a, b):
 
 
 # ------------------------------------------------------- flat algorithms ----
-@pytest.mark.parametrize("n,d", [(1, 2), (3, 7), (5, 1000), (30, 50890), (2, 65537), (17, 4099)])
+@pytest.mark.parametrize("n,d", [(1, 2), (3, 7), (5, 1000), (30, 50890), (2, 65537), (17, 4099),
+                                 (100, 50890), (70, 50891), (33, 300000)])
 @pytest.mark.parametrize("alg", [3, 4, 5])
 def test_dense_bit_exact(dev, oracle, n, d, alg):
     rng = np.random.default_rng(n * 1000 + d)
@@ -56,6 +57,33 @@ def test_dense_bit_exact(dev, oracle, n, d, alg):
     assert dev.status() == 0
     ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
     assert st == 0 and bits_equal(out, ref)
+
+
+@pytest.mark.parametrize("n,d", [(100, 50890), (45, 1001)])
+@pytest.mark.parametrize("clip,acc", [(True, False), (False, True), (True, True)])
+def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
+    """The LDS-staged small-d kernel == the one-lane-per-pair streaming kernel (tuning
+    variant 13), bit for bit, with the per-client clip and accumulate fused."""
+    import torch
+
+    from fltee import _lib as L
+    rng = np.random.default_rng(n + d)
+    idx = np.tile(np.arange(d, dtype=np.uint32), n)
+    val = rng.normal(0, 0.01, n * d).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    prev = torch.from_numpy(rng.normal(0, 1, d).astype(np.float32)).cuda()
+    outs = []
+    try:
+        for variant in (0, 13):
+            L.lib().fltee_debug_set_dense_variant(variant)
+            out = prev.clone()
+            dev.aggregate(3, rec, n, d, d, out=out, dense=True, clip=clip, clipping=0.5,
+                          accumulate=acc)
+            assert dev.status() == 0
+            outs.append(out.cpu().numpy())
+    finally:
+        L.lib().fltee_debug_set_dense_variant(0)
+    assert bits_equal(outs[0], outs[1])
 
 
 def test_dense_order_violation_is_reported(dev):
