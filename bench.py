@@ -72,16 +72,17 @@ def time_steps(torch, fn, steps, warmup, stream):
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+    # one event pair around the back-to-back launches (per-step pairs would add their own
+    # gaps, a large share of a 5-10 us kernel)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    a.record(stream)
     for i in range(steps):
-        ev[i][0].record(stream)
         fn(warmup + i)
-        ev[i][1].record(stream)
+    b.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern = sum(a.elapsed_time(b) for a, b in ev) / steps / 1e3
+    kern = a.elapsed_time(b) / steps / 1e3
     return wall, kern
 
 
@@ -570,10 +571,13 @@ def main():
         if world == 1 and not args.no_extra:
             extra = {}
             for name in [x for x in args.extra.split(",") if x]:
-                r = bench_workload(torch, D, name, steps=max(5, args.steps // 5), warmup=2,
+                wl = WORKLOADS[name]
+                small = wl["n"] * (wl["k"] or wl["d"]) * 8 < 100e6  # < 100 MB: more launches
+                ksteps = max(10, args.steps * 2) if small else max(5, args.steps // 5)
+                r = bench_workload(torch, D, name, steps=ksteps, warmup=2 + ksteps // 10,
                                    device=device)
                 extra[name] = dict(desc=WORKLOADS[name]["desc"], alg=r["alg"], n=r["n"], d=r["d"],
-                                   k=r["k"], ms_per_step=r["wall_s"] * 1e3 / max(5, args.steps // 5),
+                                   k=r["k"], ms_per_step=r["wall_s"] * 1e3 / ksteps,
                                    kernel_ms=r["kernel_s"] * 1e3, value=r["rate"],
                                    unit="client-params/s")
             line["extra"] = extra
