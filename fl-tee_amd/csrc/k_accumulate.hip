@@ -20,6 +20,8 @@
 //   while a client's indices are distinct (top-k, utils.py:327-354); a client
 //   with a repeated index sets FLTEE_DEV_ERR_FOLD_OVERFLOW and the host reruns
 //   sweep_sequential (one output per lane, all records in order).
+#include <atomic>
+
 #include "common.h"
 
 namespace fltee {
@@ -515,7 +517,8 @@ constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restrict__ rec, size_t n,
                                                            size_t k, size_t d,
                                                            uint32_t *__restrict__ mat,
-                                                           uint32_t *dup, uint32_t *status) {
+                                                           uint32_t *dup, uint32_t epoch,
+                                                           uint32_t *status) {
     uint32_t bad = 0, rep = 0;
     for (size_t c = blockIdx.y; c < n; c += gridDim.y) {
         for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < k; e += (size_t)gridDim.x * 256) {
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restri
         }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(status, FLTEE_DEV_ERR_INDEX_RANGE);
-    if (__any(rep) && (threadIdx.x & 63) == 0) atomicOr(dup, 1u);
+    if (__any(rep) && (threadIdx.x & 63) == 0) atomicMax(dup, epoch);  // this call's mark
 }
 
 // One lane per output j: the n rows' slots j are read U at a time (wave-coalesced
@@ -535,11 +538,12 @@ template <bool ACC, int U>
 __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restrict__ mat, size_t d,
                                                         uint32_t n, const uint2 *__restrict__ rec,
                                                         size_t nrec, const uint32_t *dup,
-                                                        float coef, float *__restrict__ out) {
+                                                        uint32_t epoch, float coef,
+                                                        float *__restrict__ out) {
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     float acc = 0.0f;
     bool hit = false;
-    if (*dup == 0) {
+    if (*dup != epoch) {
         if (j >= d) return;
         const uint32_t *col = mat + j;
         uint32_t c = 0;
@@ -554,11 +558,19 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
                 hit |= h;
             }
         }
-        for (; c < n; ++c) {
-            const uint32_t x = col[(size_t)c * d];
-            const bool h = x != kEmptySlot;
-            acc = __fadd_rn(acc, h ? __uint_as_float(x) : 0.0f);
-            hit |= h;
+        if (c < n) {  // the last n % U rows as one predicated batch (all loads in flight)
+            uint32_t x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[u] = c + u < n ? __builtin_nontemporal_load(col + (size_t)(c + u) * d) : kEmptySlot;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (c + u < n) {
+                    const bool h = x[u] != kEmptySlot;
+                    acc = __fadd_rn(acc, h ? __uint_as_float(x[u]) : 0.0f);
+                    hit |= h;
+                }
+            }
         }
     } else {  // a client repeated an index: every record, in upload order
         __shared__ uint2 tile[SW_CHUNK];
@@ -587,23 +599,27 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
                               uint32_t *dup, float coef, float *out, bool accumulate,
                               uint32_t *status, hipStream_t s) {
     if (d == 0) return hipSuccess;
+    // *dup holds the epoch of the last call that saw a repeated index: a fresh epoch per
+    // call replaces a memset of the flag (one launch less)
+    static std::atomic<uint32_t> epochs{0};
+    uint32_t epoch = ++epochs;
+    if (epoch == 0) epoch = ++epochs;
     hipError_t e = hipMemsetAsync(mat, 0xFF, n * d * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(dup, 0, 4, s);
     if (e != hipSuccess) return e;
     if (k) {
         const size_t bx = (k + 255) / 256 < 1024 ? (k + 255) / 256 : 1024;
         const size_t by = n < 65535 ? n : 65535;
         hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, s,
-                           (const uint2 *)rec, n, k, d, mat, dup, status);
+                           (const uint2 *)rec, n, k, d, mat, dup, epoch, status);
     }
     const unsigned blocks = (unsigned)((d + 255) / 256);
     const size_t nrec = n * k;
     if (accumulate)
-        hipLaunchKernelGGL((scatter_rows_sum<true, 16>), dim3(blocks), dim3(256), 0, s, mat, d,
-                           (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out);
+        hipLaunchKernelGGL((scatter_rows_sum<true, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
+                           (uint32_t)n, (const uint2 *)rec, nrec, dup, epoch, coef, out);
     else
-        hipLaunchKernelGGL((scatter_rows_sum<false, 16>), dim3(blocks), dim3(256), 0, s, mat, d,
-                           (uint32_t)n, (const uint2 *)rec, nrec, dup, coef, out);
+        hipLaunchKernelGGL((scatter_rows_sum<false, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
+                           (uint32_t)n, (const uint2 *)rec, nrec, dup, epoch, coef, out);
     return hipGetLastError();
 }
 

@@ -120,6 +120,22 @@ def test_sparse_repeated_index_flagged(dev):
     assert out.tolist() == [0, 1.0, 0.5, 0.5, 0, 0, 0, 0]
 
 
+def test_non_oblivious_scatter_repeat_flag_is_per_call(dev, oracle):
+    """The scatter's repeated-index mark is tagged with the call's epoch: a call with a
+    repeated index, then calls without, then with again, each exact (no stale flag)."""
+    rng = np.random.default_rng(3)
+    n, d, k = 6, 700, 90
+    good_i, good_v = rand_sparse(rng, n, d, k)
+    bad_i = good_i.copy()
+    bad_i[k + 1] = bad_i[k]                       # client 1 repeats an index
+    for idx in (bad_i, good_i, good_i, bad_i, good_i):
+        rec = cuda_records(dev, idx, good_v)
+        out = dev.aggregate(4, rec, n, k, d).cpu().numpy()
+        assert dev.status() == 0
+        ref, st = oracle.non_oblivious(oracle.as_weights(idx, good_v), d, n)
+        assert st == 0 and bits_equal(out, ref)
+
+
 def test_non_oblivious_scatter_sentinel_value(dev, oracle):
     # a value whose bits equal the scatter's empty-slot sentinel (a NaN) takes the
     # in-order sweep, like a repeated index; every other output stays bit-exact
