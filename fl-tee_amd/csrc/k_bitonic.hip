@@ -652,6 +652,15 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     return hipGetLastError();
 }
 
+// the direct first pass (and fused producers) for 2^12-record tiles too (512 lanes x 8;
+// FLTEE_BITONIC_DIRECT_SORT8=0 turns it off, A/B)
+static bool direct_sort8() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_DIRECT_SORT8");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static bool direct_sort() {
     static bool on = [] {
         const char *e = getenv("FLTEE_BITONIC_DIRECT_SORT");
@@ -668,6 +677,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
         if (c.E == 32) return launch_sort_direct<MODE, 32, 512>(c, s, data, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
+        if (c.NT == 512 && c.E == 8 && direct_sort8()) return launch_sort_direct<MODE, 8, 512>(c, s, data, seed, pbase);
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
@@ -876,6 +886,7 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
     else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, g);
     else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, g);
+    else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, g);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
     for (uint32_t ilog = c.tlog + 1; ilog <= mlog; ++ilog) {

@@ -159,8 +159,9 @@ def test_non_oblivious_index_out_of_range(dev):
 
 
 # ---------------------------------------------------------- bitonic ---------
-# 2^18: 2^11 tiles + one strided LDS pass; 2^22: 2^14 tiles + strided passes
-@pytest.mark.parametrize("m", [2, 4, 64, 128, 1024, 8192, 1 << 15, 1 << 18, 1 << 22])
+# 2^18: 2^11 tiles + one strided LDS pass; 2^20: 2^12 tiles (512 x 8, direct first pass);
+# 2^22: 2^14 tiles + strided passes
+@pytest.mark.parametrize("m", [2, 4, 64, 128, 1024, 8192, 1 << 15, 1 << 18, 1 << 20, 1 << 22])
 def test_bitonic_idx_network_bit_exact(dev, oracle, m):
     import torch
     rng = np.random.default_rng(m)
@@ -174,7 +175,7 @@ def test_bitonic_idx_network_bit_exact(dev, oracle, m):
     assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
 
 
-@pytest.mark.parametrize("m", [2, 256, 8192, 1 << 16, 1 << 22])
+@pytest.mark.parametrize("m", [2, 256, 8192, 1 << 16, 1 << 20, 1 << 22])
 def test_keyed_shuffle_bit_exact(dev, oracle, m):
     import torch
     rng = np.random.default_rng(m + 1)
@@ -189,7 +190,7 @@ def test_keyed_shuffle_bit_exact(dev, oracle, m):
 
 
 @pytest.mark.parametrize("mode", [0, 2])
-@pytest.mark.parametrize("m", [1 << 22, 1 << 24])
+@pytest.mark.parametrize("m", [1 << 20, 1 << 22, 1 << 24])
 def test_bitonic_repeatable(dev, mode, m):
     """The same input through the network three times gives the same bytes (a store
     whose data registers are overwritten too early shows up here as run-to-run noise)."""
@@ -219,7 +220,7 @@ def test_composite_key_sort(dev):
 # ------------------------------------------------- fused producers ---------
 @pytest.mark.parametrize("gen", [1, 2])
 @pytest.mark.parametrize("nrec,d", [(1_500_001, 200_000), (999_999, 1_200_000), (3_000_000, 100),
-                                    (0, 1_500_000)])
+                                    (0, 1_500_000), (700_001, 100_000)])
 def test_sort_fused_producer_equals_build_then_sort(dev, gen, nrec, d):
     """advanced_init (gen 1) / nips19_build (gen 2) fused into the sort's first pass ==
     the build kernel, then the sort, bit for bit (M >= 2^21, where the fusion applies;
