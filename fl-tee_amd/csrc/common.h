@@ -135,8 +135,13 @@ hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t
                             hipStream_t s);
 hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, size_t d,
                                size_t tf, size_t m, uint64_t *dst, hipStream_t s);
-hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float *out,
-                                 hipStream_t s);
+// safe_aggregate pieces: tile counts + exclusive scan (base[nb] = total selected),
+// then the order-preserving write of the idx < d entries (engine.hip drives them)
+size_t select_tiles(size_t m);
+hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t *cnt,
+                               uint32_t *base, hipStream_t s);
+hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const uint32_t *base,
+                               uint64_t *dst, hipStream_t s);
 hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_t *r, size_t d,
                                      size_t tf, size_t pbase, size_t m, uint64_t *dst,
                                      hipStream_t s);

@@ -174,8 +174,15 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
                       alg == FLTEE_ALG_NON_OBLIVIOUS;
     if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
     if (alg == FLTEE_ALG_NIPS19) o.seed = next_seed();
+    // advanced's fold (advanced.rs:66-101) is exact for runs up to the halo; halo = n
+    // covers every run of clients with distinct indices (n records + the initial
+    // entry).  A longer run (a client repeating an index) is detected and the fold
+    // reruns with a wider halo; the last attempt uses the longest run the fold can
+    // see (n * k_req + d positions: every record plus the initial entry in one run),
+    // so the loop always ends with the enclave's exact sums.
+    const size_t max_run = n * std::max(k_req, rpc) + d;
     size_t halo = n;
-    for (int attempt = 0; attempt < 6; ++attempt) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
         if (hipMemsetAsync(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         o.fold_halo = halo;
         uint32_t st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, c->stream, c->status);
@@ -198,7 +205,9 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
                     return FLTEE_ERROR_UNEXPECTED;
                 return hipStreamSynchronize(c->stream) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
             }
-            halo = halo * 4 + 16;  // a run longer than the halo: widen it
+            if (halo >= max_run) return FLTEE_ERROR_UNEXPECTED;  // cannot happen
+            // a run longer than the halo: widen it (x16), then the bound itself
+            halo = (attempt >= 2 || halo * 16 + 16 >= max_run) ? max_run : halo * 16 + 16;
             continue;
         }
         return FLTEE_ERROR_UNEXPECTED;

@@ -21,6 +21,8 @@ struct DeviceCtx {
     Buffer ws_a, ws_b, ws_mat, ws_r, ws_coef, ws_rec;  // aggregation scratch
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
+    Buffer ws_cnt, ws_sel, ws_keys;                      // nips19 ordered safe_aggregate
+    uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)
     static constexpr int kCopyEvents = 64;
@@ -38,6 +40,12 @@ float nips19_threshold(size_t d, size_t k, size_t n);
 
 fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,
                          const fltee_device_opts &o, hipStream_t s, uint32_t *status);
+// common.rs:25-35 on m entries of src (the shuffled array), bit-exact: out[i] = coef *
+// (+0 + v1 + v2 ...) over the entries with idx == i in position order (accumulate:
+// out[i] += the un-scaled sum).  Synchronises `s` once to read the selected count.
+hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, size_t d,
+                                  float coef, float *out, bool accumulate, uint32_t *status,
+                                  hipStream_t s);
 fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
                                            float *out, bool acc, hipStream_t s);
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);

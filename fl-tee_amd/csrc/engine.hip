@@ -129,7 +129,8 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         break;
     }
     case FLTEE_ALG_NIPS19: {
-        const float T = nips19_threshold(d, k, n);
+        const size_t kq = (o.flags & FLTEE_OPT_K_REQ) ? o.k_req : k;  // nips19.rs:38
+        const float T = nips19_threshold(d, kq, n);
         p.a_bytes = next_pow2_sz(n * k + d * f32_to_usize_sat(T)) * 8;
         p.r_bytes = d * 4;
         break;
@@ -143,6 +144,35 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
     return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
            c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
            c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes);
+}
+
+hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, size_t d,
+                                  float coef, float *out, bool acc, uint32_t *status,
+                                  hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (!acc && d) e = hipMemsetAsync(out, 0, d * 4, s);
+    if (e != hipSuccess || m == 0 || d == 0) return e;
+    const size_t nb = select_tiles(m);
+    if (!c->ws_cnt.reserve((2 * nb + 2) * 4)) return hipErrorOutOfMemory;
+    if (!c->host_word && hipHostMalloc((void **)&c->host_word, 64, hipHostMallocDefault) != hipSuccess) {
+        c->host_word = nullptr;
+        return hipErrorOutOfMemory;
+    }
+    uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
+    e = launch_select_count(src, m, d, cnt, base, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->host_word, base + nb, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    const size_t lc = *c->host_word;  // entries with idx < d (the DP-noised histogram total)
+    if (lc == 0) return hipSuccess;
+    const size_t mc = next_pow2_sz(lc);
+    if (!c->ws_sel.reserve(lc * 8) || !c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
+    uint64_t *sel = (uint64_t *)c->ws_sel.ptr, *keys = (uint64_t *)c->ws_keys.ptr;
+    e = launch_select_write(src, m, d, base, sel, s);
+    if (e == hipSuccess) e = launch_composite_init(sel, lc, d, mc, keys, status, s);
+    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s);
+    if (e == hipSuccess) e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, s);
+    return e;
 }
 
 // `advanced` over n clients' records into out (coef or accumulate).
@@ -178,6 +208,21 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
     if (!c) return FLTEE_ERROR_UNEXPECTED;
     if (n == 0) return FLTEE_ERROR_INVALID_PARAMETER;
     if (n * k + d >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;  // 32-bit positions
+    // the networks address records with 32-bit byte offsets: arrays of <= 2^29 records
+    // (k_bitonic.hip, k_compact.hip); refuse larger ones before reserving scratch
+    constexpr size_t kMaxNet = (size_t)1 << 29;
+    if ((alg == FLTEE_ALG_ADVANCED && next_pow2_sz(n * k + d) > kMaxNet) ||
+        (alg == FLTEE_ALG_OPTIMIZED &&
+         next_pow2_sz((o.batch && o.batch < n ? o.batch : n) * k + d) > kMaxNet) ||
+        (alg == FLTEE_ALG_NON_OBLIVIOUS && !(o.flags & FLTEE_OPT_DENSE) &&
+         !use_scatter_rows(n, k, d) && next_pow2_sz(n * k) > kMaxNet))
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    if (alg == FLTEE_ALG_NIPS19) {
+        const size_t kq = (o.flags & FLTEE_OPT_K_REQ) ? o.k_req : k;
+        const size_t tf = f32_to_usize_sat(nips19_threshold(d, kq, n));
+        if (tf > ((size_t)1 << 31) / (d ? d : 1) || next_pow2_sz(n * k + d * tf) > kMaxNet)
+            return FLTEE_ERROR_INVALID_PARAMETER;
+    }
     const bool dense = (o.flags & FLTEE_OPT_DENSE) != 0;
     if (dense && k != d) return FLTEE_ERROR_INVALID_PARAMETER;
     const bool acc = (o.flags & FLTEE_OPT_ACCUMULATE) != 0;
@@ -246,14 +291,17 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         break;
     }
     case FLTEE_ALG_NIPS19: {
-        const float T = nips19_threshold(d, k, n);
+        // nips19.rs:38 takes T and the Laplace scale from the REQUEST's
+        // num_of_sparse_parameters (0 for fl_main.py's dense uploads), not the payload
+        const size_t kq = (o.flags & FLTEE_OPT_K_REQ) ? o.k_req : k;
+        const float T = nips19_threshold(d, kq, n);
         const size_t tf = f32_to_usize_sat(T);
         const size_t L = n * k + d * tf, M = next_pow2_sz(L);
-        if (L >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+        if (L >= ((size_t)1 << 31) || M > kMaxNet) return FLTEE_ERROR_INVALID_PARAMETER;
         const uint64_t seed = o.seed ? o.seed : next_seed();
         uint32_t *r = (uint32_t *)c->ws_r.ptr;
         uint64_t *A = (uint64_t *)c->ws_a.ptr;
-        e = launch_laplace_r(d, k, T, seed, r, s);
+        e = launch_laplace_r(d, kq, T, seed, r, s);
         const uint32_t key = (uint32_t)(seed ^ (seed >> 32));
         if (e == hipSuccess) {  // build fused into the shuffle's first pass where it can be
             e = bitonic_sort_nips19(A, M, key, rec, n * k, r, d, tf, s);
@@ -262,9 +310,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
                 if (e == hipSuccess) e = bitonic_sort(A, M, 2, key, s);
             }
         }
-        if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
-        if (e == hipSuccess) e = launch_safe_aggregate(A, M, d, out, s);
-        if (e == hipSuccess && !acc && coef != 1.0f) e = launch_scale(out, d, coef, s);
+        if (e == hipSuccess) e = safe_aggregate_ordered(c, A, M, d, coef, out, acc, status, s);
         break;
     }
     default:
@@ -481,9 +527,12 @@ extern "C" fltee_status_t fltee_nips19_build_range_device(const void *d_records,
 
 extern "C" fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t m, size_t d,
                                                       float *d_out, void *stream) {
-    hipStream_t s = (hipStream_t)stream;
-    if (d && hipMemsetAsync(d_out, 0, d * 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-    return launch_safe_aggregate((const uint64_t *)d_src, m, d, d_out, s) == hipSuccess
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c) return FLTEE_ERROR_UNEXPECTED;
+    if (m >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+    return safe_aggregate_ordered(c, (const uint64_t *)d_src, m, d, 1.0f, d_out, false, c->status,
+                                  (hipStream_t)stream) == hipSuccess
                ? FLTEE_SUCCESS
                : FLTEE_ERROR_UNEXPECTED;
 }

@@ -8,13 +8,10 @@
 //                    ((r_i < j) ? i : u32::MAX, 0.0) (oblivious_pad, branch-free)
 //                    ++ (u32::MAX, 0.0) pads to 2^m
 //   [bitonic network, mode 2 = keyed shuffle]
-//   safe_aggregate : g[idx] += val for idx < d in shuffled order.  Every entry
-//                    with idx < d is added (dummies add +0.0), exactly the
-//                    access histogram the enclave reveals.  Sums go through
-//                    LDS float atomics per (chunk, d-segment) and one global
-//                    atomic per slot per chunk, so the per-index summation
-//                    order is not the enclave's: parity is within fp32
-//                    tolerance (the enclave's own order is random anyway).
+//   safe_aggregate : g[idx] += val for idx < d in shuffled order, left to right
+//                    per index exactly like the enclave (compaction of the idx < d
+//                    entries + stable composite sort + ordered fold, see below):
+//                    bit-exact with the oracle's nips19 under the same seed.
 #include "common.h"
 
 namespace fltee {
@@ -32,7 +29,10 @@ __global__ void laplace_r_kernel(size_t d, float b, float T, uint32_t k0, uint32
     uint32_t c[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), 0u, FLTEE_STREAM_LAPLACE};
     philox4x32_10(c, k0, k1);
     const float p = (float)(c[0] >> 8) * (1.0f / 16777216.0f);
-    const float noise = p > 0.5f ? -b * logf(2.0f - 2.0f * p) : b * logf(2.0f * p);
+    // f32 ln as (float)ln((double)x): the same bits as the oracle's host math (and
+    // the correctly rounded f32 ln in practice), so the counts match exactly
+    const float noise = p > 0.5f ? -b * (float)log((double)(2.0f - 2.0f * p))
+                                 : b * (float)log((double)(2.0f * p));
     r[i] = fabsf(noise) > T ? f32_to_u32_sat(ceilf(T)) : f32_to_u32_sat(T + ceilf(noise));
 }
 
@@ -84,97 +84,150 @@ hipError_t launch_nips19_build(const void *rec, size_t nrec, const uint32_t *r, 
     return launch_nips19_build_range(rec, nrec, r, d, tf, 0, m, dst, s);
 }
 
-constexpr uint32_t SA_SEG = 32768;      // floats per LDS segment (128 KB)
-constexpr uint32_t SA_SEG_MAX = 40960;  // the whole 160 KB of LDS
-constexpr uint32_t SA_CHUNKS = 256;
+// ------------------------------------------------------------ safe_aggregate --
+// common.rs:25-35: for w in v { if w.0 < d { g[w.0] += w.1 } } — a left-to-right
+// fp32 sum per index in SHUFFLED order.  Reproduced exactly (bit for bit) as:
+//   1. select_count / select_write: order-preserving stream compaction of the
+//      entries with idx < d (real records and the valid Laplace dummies; the
+//      u32::MAX dummies and pads drop out, as in the reference's branch).  Blocks
+//      own contiguous tiles of SEL_TILE entries; ranks inside a tile come from wave
+//      ballots, tile bases from one exclusive scan of the tile counts.  The selected
+//      count Lc is what the enclave's g[] access pattern reveals anyway (the
+//      DP-noised histogram total).
+//   2. the composite-key stable sort of non_oblivious (k_fold.hip: key = idx << 32 |
+//      compacted position, mode-1 bitonic network over next_pow2(Lc)) and the
+//      ordered fold: each run head sums its run in shuffled order from +0.0.
+constexpr int SEL_NT = 256;
+constexpr size_t SEL_TILE = 8192;  // entries per block
+constexpr uint32_t SEL_ROUNDS = (uint32_t)(SEL_TILE / (2 * SEL_NT));
+typedef unsigned int sel_u32x4 __attribute__((ext_vector_type(4)));
 
-// VEC: src 16-B aligned, chunks read as record pairs, SA_U pair loads in flight per
-// lane (one 8-B load per lane at a time left ~8 KB in flight per CU: latency-bound,
-// 0.69 ms for C4's 1 GB).
-constexpr int SA_U = 4;
-typedef unsigned int sa_u32x4 __attribute__((ext_vector_type(4)));
-// TAILG: one LDS segment [0, segsz) and the few indices in [segsz, d) go straight to
-// global atomics, so the array is read once (C4, d = 44,964: two 32K segments read it
-// twice from HBM, both blocks of a chunk running at the same time).
-template <bool VEC, bool TAILG>
-__global__ __launch_bounds__(1024) void safe_aggregate_kernel(const uint2 *__restrict__ src,
-                                                              size_t m, size_t d, uint32_t segsz,
-                                                              float *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) float acc[];
-    // 1-D grid, segment fastest: the blocks of every segment of one chunk are dispatched
-    // back to back, so all but the first read that chunk from the Infinity Cache
-    const uint32_t nseg = TAILG ? 1u : (uint32_t)((d + segsz - 1) / segsz);
-    const uint32_t seg = blockIdx.x % nseg, chunk = blockIdx.x / nseg, nchunks = gridDim.x / nseg;
-    const size_t seg_lo = (size_t)seg * segsz;
-    const uint32_t seg_n = (uint32_t)((d - seg_lo) < segsz ? (d - seg_lo) : segsz);
-    for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) acc[e] = 0.0f;
-    __syncthreads();
-    const size_t per = ((m + nchunks - 1) / nchunks + 1) & ~(size_t)1;  // even: pairs
-    const size_t lo = (size_t)chunk * per < m ? (size_t)chunk * per : m;
-    const size_t hi = lo + per < m ? lo + per : m;
-    auto add = [&](uint32_t idx, uint32_t val) {
-        const uint32_t rel = idx - (uint32_t)seg_lo;
-        if (idx < d && rel < seg_n) atomicAdd(&acc[rel], __uint_as_float(val));
-        else if (TAILG && idx < d) atomicAdd(&out[idx], __uint_as_float(val));
-    };
-    size_t p = lo + threadIdx.x;
-    if (VEC) {
-        const sa_u32x4 *s4 = (const sa_u32x4 *)src;
-        const size_t plo = lo / 2, phi = hi / 2;
-        size_t q = plo + threadIdx.x;
-        for (; q + (SA_U - 1) * 1024 < phi; q += SA_U * 1024) {
-            sa_u32x4 w[SA_U];
-#pragma unroll
-            for (int u = 0; u < SA_U; ++u) w[u] = __builtin_nontemporal_load(&s4[q + u * 1024]);
-#pragma unroll
-            for (int u = 0; u < SA_U; ++u) {
-                add(w[u].x, w[u].y);
-                add(w[u].z, w[u].w);
-            }
-        }
-        for (; q < phi; q += 1024) {
-            const sa_u32x4 w = __builtin_nontemporal_load(&s4[q]);
-            add(w.x, w.y);
-            add(w.z, w.w);
-        }
-        p = 2 * phi + threadIdx.x;  // an odd record at the end of the array
+// entries p, p + 1 (p even); u32::MAX beyond m
+template <bool VEC>
+__device__ __forceinline__ void sel_load(const uint2 *__restrict__ src, size_t m, size_t p, uint2 &a,
+                                         uint2 &b) {
+    if (VEC && p + 1 < m) {
+        const sel_u32x4 w = __builtin_nontemporal_load((const sel_u32x4 *)(src + p));
+        a = make_uint2(w.x, w.y);
+        b = make_uint2(w.z, w.w);
+    } else {
+        a = p < m ? src[p] : make_uint2(0xFFFFFFFFu, 0u);
+        b = p + 1 < m ? src[p + 1] : make_uint2(0xFFFFFFFFu, 0u);
     }
-    for (; p < hi; p += 1024) {
-        const uint2 w = src[p];
-        add(w.x, w.y);
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < seg_n; e += 1024) atomicAdd(&out[seg_lo + e], acc[e]);
 }
 
-hipError_t launch_safe_aggregate(const uint64_t *src, size_t m, size_t d, float *out,
-                                 hipStream_t s) {
-    if (d == 0 || m == 0) return hipSuccess;
-    static bool attr = false;
-    if (!attr) {
-        const void *k[4] = {(const void *)safe_aggregate_kernel<true, false>,
-                            (const void *)safe_aggregate_kernel<false, false>,
-                            (const void *)safe_aggregate_kernel<true, true>,
-                            (const void *)safe_aggregate_kernel<false, true>};
-        for (const void *f : k)
-            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, SA_SEG_MAX * 4);
-        attr = true;
+template <bool VEC>
+__global__ __launch_bounds__(SEL_NT) void select_count_kernel(const uint2 *__restrict__ src,
+                                                              size_t m, uint32_t d,
+                                                              uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t wsum[SEL_NT / 64];
+    const size_t lo = (size_t)blockIdx.x * SEL_TILE;
+    uint32_t c = 0;
+#pragma unroll 4
+    for (uint32_t r = 0; r < SEL_ROUNDS; ++r) {
+        uint2 a, b;
+        sel_load<VEC>(src, m, lo + 2 * ((size_t)r * SEL_NT + threadIdx.x), a, b);
+        c += (a.x < d) + (b.x < d);
     }
-    // d a little above one 32K segment: one 40K segment + global atomics for the rest
-    const bool tailg = d > SA_SEG && d <= SA_SEG_MAX + SA_SEG_MAX / 8;
-    const uint32_t segsz = tailg ? SA_SEG_MAX : SA_SEG;
-    const unsigned segs = tailg ? 1u : (unsigned)((d + segsz - 1) / segsz);
-    size_t chunks = (m + 8191) / 8192;
-    if (chunks > SA_CHUNKS) chunks = SA_CHUNKS;
-    const size_t lds = (d < segsz ? d : segsz) * 4;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < SEL_NT / 64; ++w) t += wsum[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of nb tile counts in one block; base[nb] = total
+__global__ __launch_bounds__(1024) void select_scan_kernel(const uint32_t *__restrict__ cnt,
+                                                           uint32_t nb, uint32_t *__restrict__ base) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t lo = threadIdx.x * per < nb ? threadIdx.x * per : nb;
+    const uint32_t hi = lo + per < nb ? lo + per : nb;
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (uint32_t i = lo; i < hi; ++i) {
+        base[i] = run;
+        run += cnt[i];
+    }
+    if (threadIdx.x == 1023) base[nb] = part[1023];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(SEL_NT) void select_write_kernel(const uint2 *__restrict__ src,
+                                                              size_t m, uint32_t d,
+                                                              const uint32_t *__restrict__ base,
+                                                              uint2 *__restrict__ dst) {
+    __shared__ uint32_t wsum[2][SEL_NT / 64];
+    const size_t lo = (size_t)blockIdx.x * SEL_TILE;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t run = base[blockIdx.x];
+    for (uint32_t r = 0; r < SEL_ROUNDS; ++r) {
+        uint2 a, b;
+        sel_load<VEC>(src, m, lo + 2 * ((size_t)r * SEL_NT + threadIdx.x), a, b);
+        const uint32_t f0 = a.x < d, f1 = b.x < d;
+        const uint64_t b0 = __ballot(f0), b1 = __ballot(f1);
+        // lane l holds entries 2l, 2l+1 of the wave's span: all of lanes < l come first
+        const uint32_t rank = __popcll(b0 & below) + __popcll(b1 & below);
+        if (lane == 0) wsum[r & 1][wv] = __popcll(b0) + __popcll(b1);
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < SEL_NT / 64; ++w) {
+            const uint32_t x = wsum[r & 1][w];
+            pre += w < wv ? x : 0u;
+            tot += x;
+        }
+        const uint32_t o = run + pre + rank;
+        if (f0) dst[o] = a;
+        if (f1) dst[o + f0] = b;
+        run += tot;
+    }
+}
+
+hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t *cnt,
+                               uint32_t *base, hipStream_t s) {
+    const size_t nb = select_tiles(m);
     const bool vec = ((uintptr_t)src & 15) == 0;
-    const dim3 grid((unsigned)(chunks * segs));
-    const uint2 *s2 = (const uint2 *)src;
-    if (vec && tailg) hipLaunchKernelGGL((safe_aggregate_kernel<true, true>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
-    else if (vec) hipLaunchKernelGGL((safe_aggregate_kernel<true, false>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
-    else if (tailg) hipLaunchKernelGGL((safe_aggregate_kernel<false, true>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
-    else hipLaunchKernelGGL((safe_aggregate_kernel<false, false>), grid, dim3(1024), lds, s, s2, m, d, segsz, out);
+    const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+    if (vec)
+        hipLaunchKernelGGL(select_count_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+                           (const uint2 *)src, m, dd, cnt);
+    else
+        hipLaunchKernelGGL(select_count_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+                           (const uint2 *)src, m, dd, cnt);
+    hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
     return hipGetLastError();
 }
+
+hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const uint32_t *base,
+                               uint64_t *dst, hipStream_t s) {
+    const size_t nb = select_tiles(m);
+    const bool vec = ((uintptr_t)src & 15) == 0;
+    const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+    if (vec)
+        hipLaunchKernelGGL(select_write_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+                           (const uint2 *)src, m, dd, base, (uint2 *)dst);
+    else
+        hipLaunchKernelGGL(select_write_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+                           (const uint2 *)src, m, dd, base, (uint2 *)dst);
+    return hipGetLastError();
+}
+
+size_t select_tiles(size_t m) { return m ? (m + SEL_TILE - 1) / SEL_TILE : 1; }
 
 }  // namespace fltee

@@ -70,6 +70,12 @@ static inline size_t f32_to_usize_sat(float x) {
     return (size_t)x;
 }
 
+/* Test-only parallelism for the comparator networks (each step's compare-exchanges
+ * are independent, so the result is the same for any thread count).  Default 1: the
+ * CPU baseline (bench.py) stays single-threaded like the 1-TCS enclave. */
+static int g_threads = 1;
+void fo_set_threads(int t) { g_threads = t > 0 ? t : 1; }
+
 size_t fo_next_pow2(size_t x) {
     size_t p = 1;
     while (p < x) p <<= 1;
@@ -253,6 +259,7 @@ void fo_bitonic_sort_by_idx(fo_weight *s, size_t size) {
     for (size_t i = 2; i <= size; i <<= 1) {
         for (size_t j = i >> 1; j > 0; j >>= 1) {
             size_t ml = j - 1, mh = ~ml;
+#pragma omp parallel for if (g_threads > 1 && half >= 65536) num_threads(g_threads) schedule(static)
             for (size_t k = 0; k < half; ++k) {
                 size_t l = ((k & mh) << 1) | (k & ml);
                 size_t m = l + j;
@@ -342,6 +349,8 @@ float fo_nips19_threshold(size_t d, size_t k, size_t n) {
     return l1 / epsilon * logf((float)d / delta); /* common.rs:81 */
 }
 
+static inline float ln_f32(float x) { return (float)log((double)x); }
+
 /* common.rs:77-98 (uniform from Philox instead of sgx_rand StdRng) and
  * common.rs:151-161 transform_to_random_int_vec */
 void fo_laplace_r(size_t d, size_t k, size_t n, uint64_t seed, uint32_t *r, float *T_out) {
@@ -352,7 +361,9 @@ void fo_laplace_r(size_t d, size_t k, size_t n, uint64_t seed, uint32_t *r, floa
         uint32_t ctr[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), 0, STREAM_LAPLACE}, o[4];
         fo_philox4x32_10(ctr, key, o);
         float p = (float)(o[0] >> 8) * (1.0f / 16777216.0f);
-        float noise = p > 0.5f ? -b * logf(2.0f - 2.0f * p) : b * logf(2.0f * p);
+        /* f32 ln as (float)ln((double)x): correctly rounded in practice and the same
+         * bits on the GPU (k_nips19.hip), so the Laplace counts match exactly */
+        float noise = p > 0.5f ? -b * ln_f32(2.0f - 2.0f * p) : b * ln_f32(2.0f * p);
         r[i] = fabsf(noise) > T ? f32_to_u32_sat(ceilf(T)) : f32_to_u32_sat(T + ceilf(noise));
     }
     if (T_out) *T_out = T;
@@ -383,6 +394,7 @@ void fo_shuffle_keyed(fo_weight *s, size_t size, uint32_t seed) {
         for (size_t j = i >> 1; j > 0; j >>= 1, --jlog) {
             size_t ml = j - 1, mh = ~ml;
             uint32_t key = fo_shuffle_step_key(seed, ilog, jlog);
+#pragma omp parallel for if (g_threads > 1 && half >= 65536) num_threads(g_threads) schedule(static)
             for (size_t k = 0; k < half; ++k) {
                 size_t l = ((k & mh) << 1) | (k & ml);
                 size_t m = l + j;

@@ -63,6 +63,7 @@ def lib():
             "fo_sample_client_ids": (None, [P, S, S, U64, P]),
             "fo_reset": (None, []),
             "fo_set_seed": (None, [U64]),
+            "fo_set_threads": (None, [ctypes.c_int]),
             "fo_ecall_fl_init": (U32, [U32, P, S, S, S, F, F, F, F, U32, U8, U8]),
             "fo_ecall_start_round": (U32, [U32, U32, S, P]),
             "fo_ecall_secure_aggregation": (U32, [U32, U32, P, S, P, S, S, S, U32, P, P]),
@@ -264,6 +265,11 @@ def sample_client_ids(ids, amount, seed):
     out = np.zeros(amount, dtype=np.uint32)
     lib().fo_sample_client_ids(_p(ids), len(ids), amount, seed, _p(out))
     return out
+
+
+def set_threads(t):
+    """Tests only: run the comparator networks on t threads (results are identical)."""
+    lib().fo_set_threads(int(t))
 
 
 # ------------------------------------------------------ ECALL mirror ------

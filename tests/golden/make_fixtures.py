@@ -20,9 +20,12 @@ for dataset loaders, which are out of scope).
 
 Outputs (tests/golden/*.npz) hold inputs and the reference-produced bytes
 (plaintext records, ciphertext), plus the oracle's aggregates at generation
-time for regression.  Expected aggregates are from the oracle (the Rust enclave
-cannot run here): the aggregation arithmetic is parity-unpinned beyond the
-invariants in tests/test_oracle.py.
+time for regression.  ref_aggregate.npz pins the aggregation arithmetic itself:
+its expected aggregates are the output of the reference's own in-order
+aggregator, src/update.py:173-184 update_global_weights (the fl_main.py:251-253
+path), run here on the same client updates whose payloads it stores (the Rust
+enclave cannot run here; this is the reference code that computes the same
+per-index in-order fp32 sum).
 """
 import os
 
@@ -154,6 +157,76 @@ def client_fixtures(utils, update, models):
     print("client_producer d", d, "k", k)
 
 
+REF_AGG_CASES = [  # (name, model, dense, n): n power of two -> torch.div == x * (1/n)
+    ("sparse_n4", "mnist", False, 4),
+    ("sparse_n32", "mnist", False, 32),
+    ("sparse_n30", "mnist", False, 30),
+    ("sparse_n100", "mnist", False, 100),
+    ("dense_n4", "small", True, 4),
+    ("dense_n30", "small", True, 30),
+    ("dense_n32", "small", True, 32),
+]
+
+
+def reference_aggregate_fixtures(utils, update, models):
+    """The reference's OWN aggregate on the same client updates.
+
+    src/update.py:173-184 update_global_weights is the fl_main.py:251-253 in-order
+    aggregator: w_avg = diffs[0]; w_avg += diffs[i] for i = 1..n-1 (client order);
+    torch.div(w_avg, n); global += w_avg.  Run here on a zero global model it returns
+    the averaged update.  The sparse cases feed it the top-k-zeroed state dicts that
+    zero_except_top_k_weights returns (utils.py:327-354), the dense cases the full
+    diffs; the payload of each client is serialize_sparse / serialize_dense of the
+    same state (fl_main.py:221-238), in the same client order.
+
+    The enclave sums the same values per index in the same order from +0.0 and
+    multiplies by 1f32/n (common.rs:14-19); torch.div divides.  For a power-of-two n
+    the two are the same IEEE operation (bit-exact); otherwise they differ by at most
+    one ulp.  Stored per case: client_ids, plaintext records (the reference's bytes),
+    d, k, ref_avg (update_global_weights' output, flattened) and abs_sum (sum of
+    |client values| per index, f64, for the reassociation bound of advanced/nips19).
+    Ciphertexts are not stored: tests encrypt with the oracle's AES, which is pinned to
+    the reference's encryption.cpp (test_oracle.py)."""
+    from collections import OrderedDict
+    out = {}
+    for name, which, dense, n in REF_AGG_CASES:
+        if which == "mnist":
+            model = models.MLP(dim_in=784, dim_hidden=64, dim_out=10)  # d = 50,890
+        else:  # a small MLP for the dense payloads (d = 3,562) to keep fixtures small
+            model = models.MLP(dim_in=100, dim_hidden=32, dim_out=10)
+        bn = utils.get_buffer_names(model)
+        d = utils.count_parameters(model)
+        k = d if dense else int(0.1 * d)
+        ids = (np.arange(n, dtype=np.uint32) * 7 + 11).astype(np.uint32)
+        states, plain = [], []
+        for cid in ids:
+            diff = perturbed_diff(model, seed=5000 + int(cid) + 100000 * n)
+            if dense:
+                st = diff
+                b = utils.serialize_dense(st, bn, d)
+            else:
+                st, idxs = utils.zero_except_top_k_weights(diff, bn, k)
+                b = utils.serialize_sparse(st, bn, idxs)
+            states.append(OrderedDict((key, v.clone()) for key, v in st.items()))
+            plain.append(np.frombuffer(b, np.uint8))
+        flats = [utils.flatten_params(utils.get_learnable_parameters(s, bn)).numpy().astype(np.float64)
+                 for s in states]
+        abs_sum = np.sum(np.abs(np.stack(flats)), axis=0)
+        glob = OrderedDict((key, torch.zeros_like(v)) for key, v in model.state_dict().items())
+        update.update_global_weights(glob, states)   # the reference's aggregator
+        ref_avg = utils.flatten_params(utils.get_learnable_parameters(glob, bn)).numpy()
+        out[name] = dict(client_ids=ids, plaintext=np.concatenate(plain), d=d, k=k, n=n,
+                         dense=dense, ref_avg=ref_avg.astype(np.float32),
+                         abs_sum=abs_sum.astype(np.float32))
+        print("ref_aggregate", name, "d", d, "k", k, "n", n)
+    flat = {}
+    for name, fx in out.items():
+        for key, v in fx.items():
+            flat[name + "__" + key] = np.asarray(v)
+    flat["cases"] = np.array([c[0] for c in REF_AGG_CASES])
+    np.savez_compressed(os.path.join(OUT, "ref_aggregate.npz"), **flat)
+
+
 def main():
     if "--wire-only" in sys.argv:
         wire_fixtures()
@@ -161,6 +234,9 @@ def main():
     utils, update, models = import_reference()
     if "--client-only" in sys.argv:
         client_fixtures(utils, update, models)
+        return
+    if "--ref-aggregate-only" in sys.argv:
+        reference_aggregate_fixtures(utils, update, models)
         return
     torch.manual_seed(1)
 
@@ -245,6 +321,7 @@ def main():
                         ciphertext=np.frombuffer(ct, np.uint8))
     print("ffi kat ok")
     client_fixtures(utils, update, models)
+    reference_aggregate_fixtures(utils, update, models)
     wire_fixtures()
 
 

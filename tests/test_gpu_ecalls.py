@@ -64,10 +64,7 @@ def test_secure_aggregation_matches_oracle(enclave, oracle, alg, name):
     assert np.isfinite(times).all() and (times >= 0).all()
     ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, k, alg)
     assert ost == 0
-    if alg == 2:  # nips19: atomics-based scatter, fp32 tolerance
-        assert np.abs(out - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()) * 5
-    else:
-        assert bits_equal(out, ref)
+    assert bits_equal(out, ref)
     # round advanced: the same round is now rejected (lib.rs:241-243,421)
     st, rv, out2, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k, alg)
     assert (st, rv) == (0, 2) and not out2.any()
@@ -144,3 +141,70 @@ def test_error_paths(enclave):
     assert bogus.ecall_secure_aggregation(400, 1, ids, enc, d, k, 4)[0] == L.ERROR_INVALID_ENCLAVE_ID
     run_round(enclave, ids, d, k, 7, enc, 401)
     assert enclave.ecall_secure_aggregation(401, 0, ids, enc, d, k, 7)[1] == L.ERROR_INVALID_PARAMETER
+
+
+def _encrypt(oracle, ids, recs):
+    return oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
+
+
+def test_advanced_long_run_ends_exact(enclave, oracle):
+    """a client repeating one index k times makes a run of ~k records, far
+    longer than the fold's n-record halo.  The ECALL widens the halo and, at the
+    latest, folds with the longest possible run (n*k + d): always the exact sums."""
+    from fltee.ecalls import set_debug_seed
+    n, k = 30, 4000
+    d = k
+    rng = np.random.default_rng(5)
+    ids = np.arange(500, 500 + n, dtype=np.uint32)
+    recs = []
+    for c in range(n):
+        w = np.zeros(k, dtype=oracle.WEIGHT)
+        w["idx"] = 7 if c == 3 else rng.permutation(d)[:k]
+        w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        recs.append(w)
+    enc = _encrypt(oracle, ids, recs)
+    for alg, fl in ((1, 610), (6, 611)):
+        set_debug_seed(SEED)
+        O = oracle.OracleEnclave(seed=SEED)
+        run_round(enclave, ids, d, k, alg, enc, fl)
+        O.fl_init(fl, ids, d, k, 1.12, 1.0, 0.1, 1.0, alg)
+        O.start_round(fl, 0, n)
+        if alg == 1:
+            st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k, alg)
+            ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, k, alg)
+        else:
+            st, rv, out, _ = enclave.ecall_client_size_optimized_secure_aggregation(
+                fl, 0, 7, ids, enc, d, k, alg)
+            ost, ref, _ = O.client_size_optimized_secure_aggregation(fl, 0, 7, ids, enc, d, k, alg)
+        assert (st, rv, ost) == (0, 0, 0)
+        assert bits_equal(out, ref)
+    set_debug_seed(0)
+
+
+@pytest.mark.parametrize("k_req", [0, 1, 50, 300])
+def test_nips19_uses_request_k(enclave, oracle, k_req):
+    """nips19.rs:38 takes T (and the Laplace scale) from the request's
+    num_of_sparse_parameters, not from the payload's record count; fl_main.py sends
+    dense uploads with k = 0 (no --alpha), where T = 0 and no dummies are added."""
+    from fltee.ecalls import set_debug_seed
+    n, d, rpc = 6, 2000, 300
+    rng = np.random.default_rng(k_req)
+    ids = np.arange(40, 40 + n, dtype=np.uint32)
+    recs = []
+    for _ in range(n):
+        w = np.zeros(rpc, dtype=oracle.WEIGHT)
+        w["idx"] = rng.permutation(d)[:rpc]
+        w["val"] = rng.normal(0, 0.01, rpc).astype(np.float32)
+        recs.append(w)
+    enc = _encrypt(oracle, ids, recs)
+    fl = 700 + k_req
+    set_debug_seed(SEED)
+    O = oracle.OracleEnclave(seed=SEED)
+    run_round(enclave, ids, d, k_req, 2, enc, fl)
+    O.fl_init(fl, ids, d, k_req, 1.12, 1.0, 0.1, 1.0, 2)
+    O.start_round(fl, 0, n)
+    st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k_req, 2)
+    ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, k_req, 2)
+    assert (st, rv, ost) == (0, 0, 0)
+    assert bits_equal(out, ref)
+    set_debug_seed(0)
