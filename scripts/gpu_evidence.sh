@@ -1,0 +1,36 @@
+#!/bin/bash
+# One gpurun job that regenerates the round's GPU evidence (run under gpurun from the
+# repo root):  TAG=r02 [TESTS=1] [BENCH=1] [PROFILE="ns c1 c3 c4 mnist100"] [PMC="ns"] \
+#              bash scripts/gpu_evidence.sh
+# Every GPU step has its own time limit and the steps stop at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}" || exit 2
+TAG=${TAG:-rxx}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+if [ "${TESTS:-1}" = 1 ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+      --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || exit 11
+  tail -3 "$OUT/pytest_gpu.log"
+fi
+if [ "${BENCH:-1}" = 1 ]; then
+  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 12
+  tail -c 600 "$OUT/bench.json"; echo
+fi
+for w in ${PROFILE}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 20 --warmup 3 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/prof_$w.log" 2>&1 || exit 13
+  echo "profiled $w"
+done
+for w in ${PMC}; do
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/pmc_fetch_$w.log" 2>&1 || exit 14
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
+  echo "pmc $w"
+done
+echo done
