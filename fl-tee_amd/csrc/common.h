@@ -92,6 +92,14 @@ hipError_t bitonic_sort_advanced(uint64_t *data, size_t m, const void *rec, size
                                  hipStream_t s);
 hipError_t bitonic_sort_nips19(uint64_t *data, size_t m, uint32_t seed, const void *rec, size_t nrec,
                                const uint32_t *r, size_t d, size_t tf, hipStream_t s);
+// the same shuffle whose last pass keeps only the entries with idx < d: tile t's are
+// left at data[t * (m / tiles), + tile_cnt[t]) in position order (the array itself is not
+// written out).  bitonic_select_tiles(m): the tile count, 0 when the last pass cannot
+// select (then hipErrorNotSupported).
+size_t bitonic_select_tiles(size_t m);
+hipError_t bitonic_sort_nips19_select(uint64_t *data, size_t m, uint32_t seed, const void *rec,
+                                      size_t nrec, const uint32_t *r, size_t d, size_t tf,
+                                      uint32_t *tile_cnt, hipStream_t s);
 void set_fused_init(int on);
 // one range [pbase, pbase + m) of a larger network (pbase a multiple of m): stages
 // 1..log2 m; the steps j < m of stage ilog; the step 2^jlog >= m of stage ilog
@@ -127,8 +135,10 @@ hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint
                                  uint64_t *tmp, float coef, float *out, hipStream_t s);
 hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,
                                  uint32_t *status, hipStream_t s);
+// writes every out[i], i < d (accumulate: adds where index i has records); start: d u32
 hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,
-                               float *out, size_t d, bool accumulate, hipStream_t s);
+                               float *out, size_t d, bool accumulate, uint32_t *start,
+                               hipStream_t s);
 
 // k_nips19.hip
 hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t *r,
@@ -142,6 +152,10 @@ hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t
                                uint32_t *base, hipStream_t s);
 hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const uint32_t *base,
                                uint64_t *dst, hipStream_t s);
+hipError_t launch_select_scan(const uint32_t *cnt, size_t nb, uint32_t *base, hipStream_t s);
+hipError_t launch_select_gather(const uint64_t *data, uint32_t tlog, size_t ntiles,
+                                const uint32_t *cnt, const uint32_t *base, uint64_t *sel,
+                                hipStream_t s);
 hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_t *r, size_t d,
                                      size_t tf, size_t pbase, size_t m, uint64_t *dst,
                                      hipStream_t s);

@@ -21,7 +21,7 @@ struct DeviceCtx {
     Buffer ws_a, ws_b, ws_mat, ws_r, ws_coef, ws_rec;  // aggregation scratch
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
-    Buffer ws_cnt, ws_sel, ws_keys;                      // nips19 ordered safe_aggregate
+    Buffer ws_cnt, ws_sel, ws_keys, ws_start;            // ordered folds (nips19, non_oblivious)
     uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)

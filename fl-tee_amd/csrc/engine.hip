@@ -11,6 +11,7 @@
 
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 
@@ -99,6 +100,7 @@ static size_t f32_to_usize_sat(float x) {
 // scratch plan per algorithm
 struct Plan {
     size_t a_bytes = 0, b_bytes = 0, mat_bytes = 0, r_bytes = 0, coef_bytes = 0, rec_bytes = 0;
+    size_t start_bytes = 0;
 };
 
 static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -117,7 +119,7 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (!dense) {
             if (use_scatter_rows(n, k, d)) p.mat_bytes = n * d * 4;
-            else p.a_bytes = next_pow2_sz(n * k) * 8;
+            else p.a_bytes = next_pow2_sz(n * k) * 8, p.start_bytes = d * 4;
         }
         break;
     case FLTEE_ALG_ADVANCED:
@@ -133,6 +135,7 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         const float T = nips19_threshold(d, kq, n);
         p.a_bytes = next_pow2_sz(n * k + d * f32_to_usize_sat(T)) * 8;
         p.r_bytes = d * 4;
+        p.start_bytes = d * 4;
         break;
     }
     default: break;
@@ -143,40 +146,83 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
 static bool reserve_plan(DeviceCtx *c, const Plan &p) {
     return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
            c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
-           c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes);
+           c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes) &&
+           c->ws_start.reserve(p.start_bytes);
+}
+
+// the selected list sel[0, lc) (entries with idx < d in position order) -> out: stable
+// composite sort by (idx, list position), then the ordered fold
+static hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d,
+                                    float coef, float *out, bool acc, uint32_t *status,
+                                    hipStream_t s) {
+    if (lc == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    const size_t mc = next_pow2_sz(lc);
+    if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
+    uint64_t *keys = (uint64_t *)c->ws_keys.ptr;
+    hipError_t e = launch_composite_init(sel, lc, d, mc, keys, status, s);
+    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s);
+    if (e == hipSuccess)
+        e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
+    return e;
+}
+
+static hipError_t read_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s) {
+    if (!c->host_word && hipHostMalloc((void **)&c->host_word, 64, hipHostMallocDefault) != hipSuccess) {
+        c->host_word = nullptr;
+        return hipErrorOutOfMemory;
+    }
+    hipError_t e = hipMemcpyAsync(c->host_word, dev_word, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) *out = *c->host_word;
+    return e;
 }
 
 hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, size_t d,
                                   float coef, float *out, bool acc, uint32_t *status,
                                   hipStream_t s) {
-    hipError_t e = hipSuccess;
-    if (!acc && d) e = hipMemsetAsync(out, 0, d * 4, s);
-    if (e != hipSuccess || m == 0 || d == 0) return e;
+    if (d == 0) return hipSuccess;
+    if (m == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
     const size_t nb = select_tiles(m);
-    if (!c->ws_cnt.reserve((2 * nb + 2) * 4)) return hipErrorOutOfMemory;
-    if (!c->host_word && hipHostMalloc((void **)&c->host_word, 64, hipHostMallocDefault) != hipSuccess) {
-        c->host_word = nullptr;
-        return hipErrorOutOfMemory;
-    }
+    if (!c->ws_cnt.reserve((2 * nb + 2) * 4) || !c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
-    e = launch_select_count(src, m, d, cnt, base, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(c->host_word, base + nb, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipError_t e = launch_select_count(src, m, d, cnt, base, s);
+    size_t lc = 0;  // entries with idx < d (the DP-noised histogram total)
+    if (e == hipSuccess) e = read_word(c, base + nb, &lc, s);
     if (e != hipSuccess) return e;
-    const size_t lc = *c->host_word;  // entries with idx < d (the DP-noised histogram total)
-    if (lc == 0) return hipSuccess;
-    const size_t mc = next_pow2_sz(lc);
-    if (!c->ws_sel.reserve(lc * 8) || !c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
-    uint64_t *sel = (uint64_t *)c->ws_sel.ptr, *keys = (uint64_t *)c->ws_keys.ptr;
-    e = launch_select_write(src, m, d, base, sel, s);
-    if (e == hipSuccess) e = launch_composite_init(sel, lc, d, mc, keys, status, s);
-    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s);
-    if (e == hipSuccess) e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, s);
-    return e;
+    if (!c->ws_sel.reserve(lc * 8 + 8)) return hipErrorOutOfMemory;
+    uint64_t *sel = (uint64_t *)c->ws_sel.ptr;
+    if (lc) e = launch_select_write(src, m, d, base, sel, s);
+    if (e != hipSuccess) return e;
+    return ordered_from_list(c, sel, lc, d, coef, out, acc, status, s);
+}
+
+// nips19's shuffle + safe_aggregate with the selection fused into the shuffle's last
+// pass (bitonic_sort_nips19_select): the 2^27-entry array is never written out or read
+// back.  hipErrorNotSupported: shape not fusable (the caller shuffles, then selects).
+static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, uint32_t key,
+                                           const void *rec, size_t nrec, const uint32_t *r,
+                                           size_t d, size_t tf, float coef, float *out, bool acc,
+                                           uint32_t *status, hipStream_t s) {
+    const size_t ntl = bitonic_select_tiles(M);
+    if (ntl == 0 || d == 0) return hipErrorNotSupported;
+    if (!c->ws_cnt.reserve((2 * ntl + 2) * 4) || !c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
+    uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + ntl + 1;
+    hipError_t e = bitonic_sort_nips19_select(A, M, key, rec, nrec, r, d, tf, cnt, s);
+    if (e != hipSuccess) return e;
+    e = launch_select_scan(cnt, ntl, base, s);
+    size_t lc = 0;
+    if (e == hipSuccess) e = read_word(c, base + ntl, &lc, s);
+    if (e != hipSuccess) return e;
+    if (!c->ws_sel.reserve(lc * 8 + 8)) return hipErrorOutOfMemory;
+    uint64_t *sel = (uint64_t *)c->ws_sel.ptr;
+    if (lc) e = launch_select_gather(A, log2_pow2(M / ntl), ntl, cnt, base, sel, s);
+    if (e != hipSuccess) return e;
+    return ordered_from_list(c, sel, lc, d, coef, out, acc, status, s);
 }
 
 // `advanced` over n clients' records into out (coef or accumulate).
 static bool g_advanced_compaction = true;  // fltee_debug_set_advanced_compaction
+static bool g_nips19_fused_select = true;  // fltee_debug_set_nips19_fused_select (A/B)
 
 static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k, size_t d,
                                size_t k_req, size_t halo, float coef, float *out, bool acc,
@@ -261,8 +307,8 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             uint64_t *K = (uint64_t *)c->ws_a.ptr;
             e = launch_composite_init(rec, n * k, d, M, K, status, s);
             if (e == hipSuccess) e = bitonic_sort(K, M, 1, 0, s);
-            if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
-            if (e == hipSuccess) e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, s);
+            if (e == hipSuccess)
+                e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
         } else {
             if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
                 e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
@@ -303,14 +349,21 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         uint64_t *A = (uint64_t *)c->ws_a.ptr;
         e = launch_laplace_r(d, kq, T, seed, r, s);
         const uint32_t key = (uint32_t)(seed ^ (seed >> 32));
-        if (e == hipSuccess) {  // build fused into the shuffle's first pass where it can be
+        bool done = false;
+        if (e == hipSuccess && g_nips19_fused_select) {  // build + shuffle + select fused
+            e = nips19_shuffle_aggregate(c, A, M, key, rec, n * k, r, d, tf, coef, out, acc,
+                                         status, s);
+            done = e != hipErrorNotSupported;
+            if (!done) e = hipSuccess;
+        }
+        if (e == hipSuccess && !done) {  // build fused into the shuffle's first pass where it can be
             e = bitonic_sort_nips19(A, M, key, rec, n * k, r, d, tf, s);
             if (e == hipErrorNotSupported) {
                 e = launch_nips19_build(rec, n * k, r, d, tf, M, A, s);
                 if (e == hipSuccess) e = bitonic_sort(A, M, 2, key, s);
             }
+            if (e == hipSuccess) e = safe_aggregate_ordered(c, A, M, d, coef, out, acc, status, s);
         }
-        if (e == hipSuccess) e = safe_aggregate_ordered(c, A, M, d, coef, out, acc, status, s);
         break;
     }
     default:
@@ -320,6 +373,9 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         const uint64_t seed = o.seed ? o.seed : next_seed();
         e = launch_dp_noise(out, d, o.sigma, o.clipping, n_avg, seed, s);
     }
+    if (e != hipSuccess)
+        std::fprintf(stderr, "[fltee] aggregate(alg %u, n %zu, k %zu, d %zu): %s\n", alg, n, k, d,
+                     hipGetErrorString(e));
     return e == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
 }
 
@@ -333,7 +389,8 @@ fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t 
 
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
     const Plan p = plan_for(alg, n, k, d, o);
-    return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes;
+    return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes +
+           p.start_bytes;
 }
 
 bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -565,6 +622,8 @@ extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(
 extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_compaction = on != 0; }
 extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_variant(v); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
+// A/B hook: 0 writes nips19's shuffled array out and selects in separate passes
+extern "C" void fltee_debug_set_nips19_fused_select(int on) { fltee::g_nips19_fused_select = on != 0; }
 // test hook: the fused-producer sort alone (gen 1: advanced, 2: nips19 with key seed),
 // into d_data[0, m); INVALID_PARAMETER when m is too small to fuse
 extern "C" fltee_status_t fltee_debug_sort_fused(uint32_t gen, void *d_data, size_t m,

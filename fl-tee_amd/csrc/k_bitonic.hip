@@ -224,13 +224,23 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // (steps 2^(RL-1) .. 1, groups of 2^RL consecutive records) stores its groups straight
 // to HBM instead of writing LDS back for a separate store loop.  Saves
 // one LDS write + read of the tile and two barriers per tile; same network.
-template <int MODE, int E, int NT, int RL, bool STRIDED>
+//
+// SEL (the LAST pass of nips19's shuffle only): instead of storing the tile, keep the
+// entries with idx < sel_d — the ones safe_aggregate adds (common.rs:25-35) — and write
+// them compacted, in position order, to the front of the tile's own slot of `data`
+// (data[tile * T, + count)), and their count to sel_cnt[tile].  The last round then
+// gives lane t the E consecutive records t*E .. t*E+E-1 (groups t*G .. t*G+G-1), so
+// one block-wide exclusive scan of the lanes' counts orders the tile's entries.  The
+// tile was read into LDS before, so the in-place writes are safe.
+template <int MODE, int E, int NT, int RL, bool STRIDED, bool SEL = false>
 __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
                                                            uint32_t tlog, uint32_t ilog,
                                                            uint32_t wlog, uint32_t dtile,
                                                            uint32_t seed, uint32_t ntiles,
-                                                           uint32_t pbase) {
+                                                           uint32_t pbase, uint32_t sel_d,
+                                                           uint32_t *__restrict__ sel_cnt) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
+    __shared__ uint32_t wtot[SEL ? NT / 64 : 1];
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     static_assert((1 << R1) == E, "E must be a power of two <= 32");
     static_assert(RL >= 1 && RL <= R1, "last round");
@@ -266,6 +276,50 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
                                (int)(jbot + RL), seed);
         constexpr int G = E >> RL;
+        if constexpr (SEL && !STRIDED) {
+            uint64_t v[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) v[q] = sm[lpad(t * (uint32_t)E + (uint32_t)q)];
+            uint32_t c = 0;
+#pragma unroll
+            for (int h = 0; h < G; ++h) {
+                uint64_t (&g)[1 << RL] = *reinterpret_cast<uint64_t (*)[1 << RL]>(&v[h << RL]);
+                group_steps<MODE, RL>(g, base + pbase + t * (uint32_t)E + ((uint32_t)h << RL), 0u,
+                                      ilog, seed);
+            }
+#pragma unroll
+            for (int q = 0; q < E; ++q) c += (uint32_t)v[q] < sel_d;
+            // block-wide exclusive scan of c in lane order
+            const uint32_t lane = t & 63, wv = t / 64;
+            uint32_t inc = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            if (lane == 63) wtot[wv] = inc;
+            __syncthreads();
+            uint32_t pre = 0, tot = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < NT / 64; ++w) {
+                const uint32_t x = wtot[w];
+                pre += w < wv ? x : 0u;
+                tot += x;
+            }
+            uint32_t o = base + pre + inc - c;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                if ((uint32_t)v[q] < sel_d) {
+                    bt_store<kTileCP>(rs, o * 8u, 0u, v[q]);  // per-lane offset: voffset
+                    ++o;
+                }
+            }
+            if (t == NT - 1) sel_cnt[tile] = tot;
+            if (next >= ntiles) break;
+            __syncthreads();  // wtot and the last round's LDS reads retire
+            tile = next;
+            continue;
+        }
 #pragma unroll
         for (int h = 0; h < G; ++h) {
             const uint32_t b = spread(t + (uint32_t)h * NT, jbot, RL);
@@ -596,23 +650,38 @@ static bool direct_merge() {
     return on;
 }
 
+// the selection sink of the last pass (see bitonic_merge_direct SEL)
+struct SelSink {
+    uint32_t d = 0;
+    uint32_t *cnt = nullptr;  // null: no sink
+};
+
 template <int MODE, int E, int NT, bool STRIDED>
 static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
-                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
+                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
+                                const SelSink &sink = SelSink{}) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rest = (int)c.tlog - (int)(STRIDED ? wlog : 0u) - R1;  // steps after the register round
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
-#define BD_GO(RL_)                                                                                 \
+#define BD_GO1(RL_, SEL_)                                                                          \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED>, \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
+            (void)hipFuncSetAttribute(                                                             \
+                (const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_>,               \
+                hipFuncAttributeMaxDynamicSharedMemorySize,                                        \
+                160 * 1024 - (SEL_ ? 256 : 0)); /* static wtot[] counts against the 160 KB */      \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED>), dim3(c.grid), dim3(NT), \
-                           c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase);       \
+        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_>), dim3(c.grid),  \
+                           dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles,     \
+                           pbase, sink.d, sink.cnt);                                               \
+    } while (0)
+#define BD_GO(RL_)                                                                                 \
+    do {                                                                                           \
+        if (!STRIDED && sink.cnt) BD_GO1(RL_, true);                                               \
+        else BD_GO1(RL_, false);                                                                   \
     } while (0)
     switch (rl) {
     case 1: BD_GO(1); break;
@@ -622,6 +691,7 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     default: if constexpr (R1 >= 5) BD_GO(5); break;
     }
 #undef BD_GO
+#undef BD_GO1
     return hipGetLastError();
 }
 
@@ -671,7 +741,8 @@ static bool direct_sort() {
 
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
-                               uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase) {
+                               uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
+                               const SelSink &sink = SelSink{}) {
     if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
         if (c.NT == 1024 && sort32()) return launch_sort_direct<MODE, 32, 512>(as_e32(c), s, data, seed, pbase);
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
@@ -682,10 +753,11 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
     if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
-        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
-        if (c.E == 32) return launch_direct<MODE, 32, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
-        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase);
+        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
+        if (c.E == 32) return launch_direct<MODE, 32, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
+        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
     }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
+    if (sink.cnt) return hipErrorNotSupported;  // only the direct contiguous merge selects
     // strided tiles (W consecutive x 2^R rows), the same first / last round in registers
     if (!SORT && wlog < c.tlog && c.tlog > 6 && direct_strided() &&
         (int)(c.tlog - wlog) > (c.E >= 32 ? 5 : 4)) {
@@ -748,7 +820,8 @@ static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
 // or strided LDS passes (more than 6), then one merge tile pass for the steps j < T.
 template <int MODE>
 static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, uint32_t ilog,
-                              int jtop, uint32_t seed, uint32_t pbase, hipStream_t s) {
+                              int jtop, uint32_t seed, uint32_t pbase, hipStream_t s,
+                              const SelSink &sink = SelSink{}) {
     const int kMaxGlobalR = max_global_r();
     const uint32_t tlog = c.tlog, T = 1u << tlog;
     const int rs = (int)tlog - min_w_log();  // global steps per strided LDS pass (W >= 2^min_w_log)
@@ -770,7 +843,7 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, u
             jtop -= R;
         }
     }
-    return launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed, pbase);
+    return launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed, pbase, sink);
 }
 
 // Stages 1..slog of the network over m records at global positions pbase.. (pbase a
@@ -874,13 +947,23 @@ hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t 
 static bool g_fused_init = true;  // fltee_debug_set_fused_init (A/B)
 void set_fused_init(int on) { g_fused_init = on != 0; }
 
+// whether the last pass of an m-record sort is the direct contiguous merge (the only
+// pass that can carry the selection sink)
+static bool last_pass_is_direct_merge(size_t m) {
+    const uint32_t mlog = log2_pow2(m);
+    const TileCfg c = make_cfg(mlog, mlog);
+    return c.tlog > 6 && mlog > c.tlog && direct_merge() &&
+           (c.NT == 1024 || c.E == 32 || (c.NT == 512 && c.E == 16));
+}
+
 template <int MODE, int GEN>
 static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const SortGen &g,
-                                hipStream_t s) {
+                                hipStream_t s, const SelSink &sink = SelSink{}) {
     if (!g_fused_init || m < 2 || m > ((size_t)1 << 29)) return hipErrorNotSupported;
     const uint32_t mlog = log2_pow2(m);
     const TileCfg c = make_cfg(mlog, mlog);
     if (c.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
+    if (sink.cnt && !last_pass_is_direct_merge(m)) return hipErrorNotSupported;
     hipError_t e;
     if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, g);
     else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
@@ -890,7 +973,8 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
     for (uint32_t ilog = c.tlog + 1; ilog <= mlog; ++ilog) {
-        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, 0u, s);
+        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, 0u, s,
+                              ilog == mlog ? sink : SelSink{});
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -908,6 +992,23 @@ hipError_t bitonic_sort_nips19(uint64_t *data, size_t m, uint32_t seed, const vo
     if (nrec + d * tf > m) return hipErrorInvalidValue;
     const SortGen g{(const uint64_t *)rec, r, (uint32_t)nrec, (uint32_t)d, (uint32_t)tf};
     return sort_gen_impl<2, 2>(data, m, seed, g, s);
+}
+
+size_t bitonic_select_tiles(size_t m) {
+    if (m < 2 || m > ((size_t)1 << 29) || !last_pass_is_direct_merge(m)) return 0;
+    const TileCfg c = make_cfg(log2_pow2(m), log2_pow2(m));
+    return c.tiles;
+}
+
+hipError_t bitonic_sort_nips19_select(uint64_t *data, size_t m, uint32_t seed, const void *rec,
+                                      size_t nrec, const uint32_t *r, size_t d, size_t tf,
+                                      uint32_t *tile_cnt, hipStream_t s) {
+    if (nrec + d * tf > m || d > 0xFFFFFFFFull || !tile_cnt) return hipErrorInvalidValue;
+    const SortGen g{(const uint64_t *)rec, r, (uint32_t)nrec, (uint32_t)d, (uint32_t)tf};
+    SelSink sink;
+    sink.d = (uint32_t)d;
+    sink.cnt = tile_cnt;
+    return sort_gen_impl<2, 2>(data, m, seed, g, s, sink);
 }
 
 // ---------------------------------------------- position-range pieces -----

@@ -230,4 +230,31 @@ hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const ui
 
 size_t select_tiles(size_t m) { return m ? (m + SEL_TILE - 1) / SEL_TILE : 1; }
 
+// The shuffle's last pass left tile t's selected entries at data[t << tlog, + cnt[t])
+// (bitonic_sort_nips19_select): exclusive scan of the counts, then one block per tile
+// copies its entries to sel[base[t], ...) — the whole selected list in position order.
+__global__ __launch_bounds__(256) void select_gather_kernel(const uint64_t *__restrict__ data,
+                                                            uint32_t tlog,
+                                                            const uint32_t *__restrict__ cnt,
+                                                            const uint32_t *__restrict__ base,
+                                                            uint64_t *__restrict__ sel) {
+    const uint32_t t = blockIdx.x, c = cnt[t], b = base[t];
+    const uint64_t *src = data + ((size_t)t << tlog);
+    for (uint32_t i = threadIdx.x; i < c; i += 256) sel[b + i] = src[i];
+}
+
+hipError_t launch_select_scan(const uint32_t *cnt, size_t nb, uint32_t *base, hipStream_t s) {
+    hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_gather(const uint64_t *data, uint32_t tlog, size_t ntiles,
+                                const uint32_t *cnt, const uint32_t *base, uint64_t *sel,
+                                hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(select_gather_kernel, dim3((unsigned)ntiles), dim3(256), 0, s, data, tlog,
+                       cnt, base, sel);
+    return hipGetLastError();
+}
+
 }  // namespace fltee

@@ -473,6 +473,46 @@ def test_nips19_c4_full_size_bit_exact(dev, oracle):
     assert np.allclose(outdp, oracle.dp_noise(ref, 1.12, 1.0, n, seed), rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,d,k", [(10, 4000, 1000), (10, 8000, 1000), (10, 16000, 1000),
+                                   (20, 20000, 2000)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_nips19_fused_selection_bit_exact(dev, oracle, n, d, k, fused):
+    """M = 2^20 (no fusable last pass), 2^21 (2^13 tiles), 2^22 (2^14 tiles), 2^24: the
+    selection fused into the shuffle's last pass (fused) and the separate select passes
+    give the oracle's nips19 bit for bit."""
+    from fltee import _lib as L
+    rng = np.random.default_rng(d + n)
+    idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    L.lib().fltee_debug_set_nips19_fused_select(1 if fused else 0)
+    try:
+        out = dev.aggregate(2, rec, n, k, d, seed=99).cpu().numpy()
+    finally:
+        L.lib().fltee_debug_set_nips19_fused_select(1)
+    assert dev.status() == 0
+    oracle.set_threads(16)
+    try:
+        ref, st = oracle.nips19(k, oracle.as_weights(idx, val), d, n, seed=99)
+    finally:
+        oracle.set_threads(1)
+    assert st == 0 and bits_equal(out, ref)
+
+
+def test_ordered_fold_long_runs(dev, oracle):
+    """non_oblivious's stable-sort path (rows too large for scatter rows) with very
+    long runs: the wave-per-index fold walks runs of thousands of records in order."""
+    rng = np.random.default_rng(8)
+    n, d, k = 4, 1 << 23, 60000  # n*d > 64*next_pow2(n*k): the sort path
+    idx = np.concatenate([np.where(rng.random(k) < 0.5, 3, rng.integers(0, d, k)) for _ in range(n)]
+                         ).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(4, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
 @pytest.mark.parametrize("d", [1000, 32768, 40000, 44964, 46080, 46081, 100000])
 @pytest.mark.parametrize("odd", [False, True])
 def test_safe_aggregate_matches_numpy(dev, d, odd):
