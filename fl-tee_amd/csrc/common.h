@@ -172,5 +172,9 @@ void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
 hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                           size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
                           hipStream_t s);
+// the bytes [16 * block_off, ...) of each client's payload; idx_sub subtracted from each idx
+hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
+                                size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
+                                uint64_t block_off, uint32_t idx_sub, hipStream_t s);
 
 }  // namespace fltee

@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "engine.h"
+#include "group.h"
 
 namespace fltee {
 
@@ -38,7 +39,13 @@ struct FLConfig {  // fl_config.rs:29-44
 static std::map<uint32_t, FLConfig> g_cfg;
 static std::set<uint32_t> g_keys;
 static bool g_have_keys = false;
-static std::vector<int> g_eid_dev;  // eid - 1 -> hip device
+static std::vector<int> g_eid_dev;  // eid - 1 -> hip device (a group's root device)
+static std::map<fltee_eid_t, Group *> g_groups;  // eids from fltee_device_init_multi
+
+static Group *group_of(fltee_eid_t eid) {
+    auto it = g_groups.find(eid);
+    return it == g_groups.end() ? nullptr : it->second;
+}
 
 void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
 
@@ -102,6 +109,19 @@ static uint32_t check_uploaded(const FLConfig &cfg, const uint32_t *ids, size_t 
     return FLTEE_SUCCESS;
 }
 
+// AES-128 round keys of the n clients' session keys (session_key_store.rs:21-22)
+static void client_round_keys(const uint32_t *ids, size_t n, std::vector<uint32_t> &rk) {
+    rk.resize(n * 44);
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t key[16] = {0};
+        key[4] = (uint8_t)(ids[i] >> 24);
+        key[5] = (uint8_t)(ids[i] >> 16);
+        key[6] = (uint8_t)(ids[i] >> 8);
+        key[7] = (uint8_t)ids[i];
+        aes128_expand_key(key, &rk[i * 44]);
+    }
+}
+
 // H2D + GPU AES-CTR decrypt of n slices of bpc bytes -> c->records (n * (bpc/8) records)
 // Loading + decryption (lib.rs:285-343), pipelined: the ciphertext crosses PCIe in
 // client chunks of ~64 MB on the copy stream, and each chunk's AES-CTR kernel runs on
@@ -117,15 +137,8 @@ static uint32_t load_and_decrypt(DeviceCtx *c, const uint32_t *ids, size_t n, co
     if (!c->cipher.reserve(n * bpc) || !c->records.reserve(n * rpc * 8) ||
         !c->round_keys.reserve(n * 44 * 4))
         return FLTEE_ERROR_OUT_OF_MEMORY;
-    std::vector<uint32_t> rk(n * 44);
-    for (size_t i = 0; i < n; ++i) {
-        uint8_t key[16] = {0};  // session_key_store.rs:21-22
-        key[4] = (uint8_t)(ids[i] >> 24);
-        key[5] = (uint8_t)(ids[i] >> 16);
-        key[6] = (uint8_t)(ids[i] >> 8);
-        key[7] = (uint8_t)ids[i];
-        aes128_expand_key(key, &rk[i * 44]);
-    }
+    std::vector<uint32_t> rk;
+    client_round_keys(ids, n, rk);
     if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     size_t per = bpc ? kLoadChunkBytes / bpc : n;
@@ -164,7 +177,7 @@ static uint32_t read_status(DeviceCtx *c, uint32_t *st) {
 // buffer (c->ws_b reused is unsafe: use records tail) and run the exact
 // fallbacks the status word asks for.
 static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t rpc, size_t d,
-                                  size_t k_req, size_t batch, float *d_out) {
+                                  size_t k_req, size_t batch, float *d_out, uint64_t seed = 0) {
     fltee_device_opts o;
     std::memset(&o, 0, sizeof o);
     o.k_req = k_req;
@@ -173,7 +186,7 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
                       alg == FLTEE_ALG_NON_OBLIVIOUS;
     if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
-    if (alg == FLTEE_ALG_NIPS19) o.seed = next_seed();
+    if (alg == FLTEE_ALG_NIPS19) o.seed = seed ? seed : next_seed();
     // advanced's fold (advanced.rs:66-101) is exact for runs up to the halo; halo = n
     // covers every run of clients with distinct indices (n records + the initial
     // entry).  A longer run (a client repeating an index) is detected and the fold
@@ -233,11 +246,35 @@ extern "C" fltee_status_t fltee_device_init(int hip_device, fltee_eid_t *eid) {
     return FLTEE_SUCCESS;
 }
 
+extern "C" fltee_status_t fltee_device_init_multi(const int *hip_devices, int n, fltee_eid_t *eid) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (!eid || !hip_devices) return FLTEE_ERROR_INVALID_PARAMETER;
+    uint32_t st = 0;
+    Group *G = group_create(hip_devices, n, &st);
+    if (!G) return st;
+    if (hipSetDevice(hip_devices[0]) != hipSuccess || !device_ctx(hip_devices[0])) return FLTEE_ERROR_UNEXPECTED;
+    g_eid_dev.push_back(hip_devices[0]);
+    *eid = (fltee_eid_t)g_eid_dev.size();
+    g_groups[*eid] = G;
+    return FLTEE_SUCCESS;
+}
+
+extern "C" int fltee_device_count(fltee_eid_t eid) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return 0;
+    Group *G = group_of(eid);
+    return G ? group_size(G) : 1;
+}
+
 extern "C" fltee_status_t fltee_device_fini(fltee_eid_t eid) {
     std::lock_guard<std::recursive_mutex> lk(api_mutex());
     if (eid == 0 || eid > g_eid_dev.size() || g_eid_dev[eid - 1] < 0) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
     const int dev = g_eid_dev[eid - 1];
     g_eid_dev[eid - 1] = -1;
+    if (Group *G = group_of(eid)) {
+        group_destroy(G);
+        g_groups.erase(eid);
+    }
     if (hipSetDevice(dev) == hipSuccess) (void)hipDeviceSynchronize();
     return FLTEE_SUCCESS;
 }
@@ -333,15 +370,40 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     if (aggregation_alg == FLTEE_ALG_ADVANCED && n * num_of_sparse_parameters > n * rpc)
         return fail(FLTEE_ERROR_INVALID_PARAMETER);  // advanced.rs:72 out-of-bounds panic
 
-    uint32_t st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data, bpc,
-                                   &execution_time_results[0], &execution_time_results[1]);
-    if (st) return fail(st);
-
-    const double t2 = now_s();
-    float *d_out = nullptr;
     if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
-    d_out = (float *)c->outbuf.ptr;
-    st = aggregate_records(c, aggregation_alg, n, rpc, d, num_of_sparse_parameters, 0, d_out);
+    float *d_out = (float *)c->outbuf.ptr;
+    const size_t k_req = num_of_sparse_parameters;
+    const float coef = 1.0f / (float)n;
+    Group *G = group_of(eid);
+    uint32_t st = FLTEE_GROUP_FALLBACK;
+    double t2 = 0;
+    const bool flat = aggregation_alg == FLTEE_ALG_BASELINE || aggregation_alg == FLTEE_ALG_PATH_ORAM ||
+                      aggregation_alg == FLTEE_ALG_NON_OBLIVIOUS;
+    if (G && flat && rpc == d && bpc == d * 8) {
+        // dense uploads over a multi-GPU eid: every GPU loads and decrypts its own
+        // parameter range (group.hip); "Loading" = the parallel H2D, "Decryption" = the
+        // decrypt + aggregate + gather
+        std::vector<uint32_t> rk;
+        client_round_keys(client_ids, n, rk);
+        st = group_dense_ecall(G, rk.data(), n, encrypted_parameters_data, d, coef, d_out,
+                               &execution_time_results[0], &execution_time_results[1]);
+        t2 = now_s();
+        if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
+    }
+    if (st == FLTEE_GROUP_FALLBACK) {
+        st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data, bpc,
+                              &execution_time_results[0], &execution_time_results[1]);
+        if (st) return fail(st);
+        t2 = now_s();
+        st = FLTEE_GROUP_FALLBACK;
+        uint64_t seed = 0;
+        if (G && aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc)
+            st = group_advanced(G, c->records.ptr, n, rpc, d, coef, d_out);
+        else if (G && aggregation_alg == FLTEE_ALG_NIPS19)
+            st = group_nips19(G, c, c->records.ptr, n, rpc, k_req, d, seed = next_seed(), coef, d_out);
+        if (st == FLTEE_GROUP_FALLBACK)  // one device (or a shape the group does not shard)
+            st = aggregate_records(c, aggregation_alg, n, rpc, d, k_req, 0, d_out, seed);
+    }
     if (!st && cfg.dp) {  // lib.rs:399-408
         if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
             st = FLTEE_ERROR_UNEXPECTED;
@@ -394,7 +456,10 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
     float *d_out = nullptr;
     if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
     d_out = (float *)c->outbuf.ptr;
-    st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
+    if (Group *G = group_of(eid))  // the batches split over the eid's GPUs (group.hip)
+        st = group_optimized(G, c->records.ptr, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
+    else
+        st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
     if (!st && cfg.dp) {  // lib.rs:586-588
         if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
             st = FLTEE_ERROR_UNEXPECTED;

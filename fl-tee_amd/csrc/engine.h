@@ -46,6 +46,13 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
 hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, size_t d,
                                   float coef, float *out, bool accumulate, uint32_t *status,
                                   hipStream_t s);
+// the selected list sel[0, lc) (nips19 entries with idx < d, in shuffled order) -> out
+hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d, float coef,
+                             float *out, bool acc, uint32_t *status, hipStream_t s);
+// one alg-6 batch: `advanced` of n clients into out[d], un-averaged (current device)
+hipError_t advanced_batch(const void *rec, size_t n, size_t k, size_t d, size_t halo, float *out,
+                          uint32_t *status, hipStream_t s);
+hipError_t read_device_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s);
 fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
                                            float *out, bool acc, hipStream_t s);
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);

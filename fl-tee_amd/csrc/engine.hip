@@ -152,10 +152,10 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
 
 // the selected list sel[0, lc) (entries with idx < d in position order) -> out: stable
 // composite sort by (idx, list position), then the ordered fold
-static hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d,
-                                    float coef, float *out, bool acc, uint32_t *status,
-                                    hipStream_t s) {
+hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d, float coef,
+                             float *out, bool acc, uint32_t *status, hipStream_t s) {
     if (lc == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    if (!c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
     const size_t mc = next_pow2_sz(lc);
     if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
     uint64_t *keys = (uint64_t *)c->ws_keys.ptr;
@@ -166,7 +166,7 @@ static hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc
     return e;
 }
 
-static hipError_t read_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s) {
+hipError_t read_device_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s) {
     if (!c->host_word && hipHostMalloc((void **)&c->host_word, 64, hipHostMallocDefault) != hipSuccess) {
         c->host_word = nullptr;
         return hipErrorOutOfMemory;
@@ -187,7 +187,7 @@ hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, s
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
     hipError_t e = launch_select_count(src, m, d, cnt, base, s);
     size_t lc = 0;  // entries with idx < d (the DP-noised histogram total)
-    if (e == hipSuccess) e = read_word(c, base + nb, &lc, s);
+    if (e == hipSuccess) e = read_device_word(c, base + nb, &lc, s);
     if (e != hipSuccess) return e;
     if (!c->ws_sel.reserve(lc * 8 + 8)) return hipErrorOutOfMemory;
     uint64_t *sel = (uint64_t *)c->ws_sel.ptr;
@@ -211,7 +211,7 @@ static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, 
     if (e != hipSuccess) return e;
     e = launch_select_scan(cnt, ntl, base, s);
     size_t lc = 0;
-    if (e == hipSuccess) e = read_word(c, base + ntl, &lc, s);
+    if (e == hipSuccess) e = read_device_word(c, base + ntl, &lc, s);
     if (e != hipSuccess) return e;
     if (!c->ws_sel.reserve(lc * 8 + 8)) return hipErrorOutOfMemory;
     uint64_t *sel = (uint64_t *)c->ws_sel.ptr;
@@ -246,6 +246,18 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     e = bitonic_sort(B, M, 0, 0, s);
     if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
     return e;
+}
+
+// `advanced` of n clients' records into out[d] un-averaged (coef 1, overwrite): one
+// batch sum of alg 6 (advanced.rs:10-21), on the current device's scratch
+hipError_t advanced_batch(const void *rec, size_t n, size_t k, size_t d, size_t halo, float *out,
+                          uint32_t *status, hipStream_t s) {
+    DeviceCtx *c = current_ctx();
+    if (!c) return hipErrorInvalidDevice;
+    fltee_device_opts o;
+    std::memset(&o, 0, sizeof o);
+    if (!reserve_plan(c, plan_for(FLTEE_ALG_ADVANCED, n, k, d, o))) return hipErrorOutOfMemory;
+    return run_advanced(c, rec, n, k, d, k, halo, 1.0f, out, false, status, s);
 }
 
 fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,

@@ -1,0 +1,31 @@
+// group.h — an enclave id spanning several GPUs (group.hip).
+#pragma once
+#include "common.h"
+#include "engine.h"
+
+namespace fltee {
+
+struct Group;
+// returned by the group paths when the shape is not sharded there (the caller runs
+// the single-device path on the root)
+constexpr uint32_t FLTEE_GROUP_FALLBACK = 0xFFFFFFFEu;
+
+Group *group_create(const int *devs, int n, uint32_t *status);
+void group_destroy(Group *G);
+int group_size(const Group *G);
+int group_root_device(const Group *G);
+hipStream_t group_root_stream(const Group *G);
+
+// dense uploads straight from the host ciphertext, parameter-range sharded; rk_host =
+// the n clients' AES round keys (44 words each); d_out_root gets the averaged f32[d]
+uint32_t group_dense_ecall(Group *G, const uint32_t *rk_host, size_t n, const uint8_t *enc,
+                           size_t d, float coef, float *d_out_root, float *t_load, float *t_dec);
+// on records decrypted into the root device's HBM (client-major, n x k)
+uint32_t group_advanced(Group *G, const void *root_rec, size_t n, size_t k, size_t d, float coef,
+                        float *d_out_root);
+uint32_t group_nips19(Group *G, DeviceCtx *root, const void *root_rec, size_t n, size_t k,
+                      size_t k_req, size_t d, uint64_t seed, float coef, float *d_out_root);
+uint32_t group_optimized(Group *G, const void *root_rec, size_t n, size_t k, size_t d,
+                         size_t batch, float coef, float *d_out_root);
+
+}  // namespace fltee

@@ -113,12 +113,17 @@ __device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// block_off: the slices are the bytes [16 * block_off, ...) of each client's payload (a
+// column slice of dense uploads, one GPU's parameter range): counter block b + block_off.
+// idx_sub is subtracted from every record's idx (the slice's first parameter), so that
+// the dense kernels' idx == position check runs on slice-local positions.
 template <bool ALIGNED>
 __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict__ cipher,
                                                       size_t n, size_t bpc, size_t rpc,
                                                       const uint32_t *__restrict__ rks,
                                                       const uint32_t *__restrict__ tables,
-                                                      uint8_t *__restrict__ plain) {
+                                                      uint8_t *__restrict__ plain,
+                                                      uint64_t block_off, uint32_t idx_sub) {
     __shared__ uint32_t T[5 * 256];
     for (uint32_t e = threadIdx.x; e < 5 * 256; e += 256) T[e] = tables[e];
     __syncthreads();
@@ -127,9 +132,10 @@ __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict_
     for (size_t g = (size_t)blockIdx.x * 256 + threadIdx.x; g < total;
          g += (size_t)gridDim.x * 256) {
         const size_t c = g / bpcl, b = g - c * bpcl;
+        const uint64_t ctr = (uint64_t)b + block_off;
         uint32_t ks[4];
         aes128_block(T, T + 256, T + 512, T + 768, T + 1024, rks + c * 44, 0u, 0u,
-                     (uint32_t)((uint64_t)b >> 32), (uint32_t)b, ks);
+                     (uint32_t)(ctr >> 32), (uint32_t)ctr, ks);
         uint2 *dst = reinterpret_cast<uint2 *>(plain + c * rpc * 8) + 2 * b;
         const bool two = 2 * b + 1 < rpc;
         uint2 x, y = make_uint2(0, 0);
@@ -142,8 +148,8 @@ __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict_
             x = make_uint2(ld_u32_bytes(src), ld_u32_bytes(src + 4));
             if (two) y = make_uint2(ld_u32_bytes(src + 8), ld_u32_bytes(src + 12));
         }
-        dst[0] = make_uint2(x.x ^ bswap32(ks[0]), x.y ^ bswap32(ks[1]));
-        if (two) dst[1] = make_uint2(y.x ^ bswap32(ks[2]), y.y ^ bswap32(ks[3]));
+        dst[0] = make_uint2((x.x ^ bswap32(ks[0])) - idx_sub, x.y ^ bswap32(ks[1]));
+        if (two) dst[1] = make_uint2((y.x ^ bswap32(ks[2])) - idx_sub, y.y ^ bswap32(ks[3]));
     }
 }
 
@@ -162,9 +168,9 @@ static uint32_t *device_tables(hipStream_t s) {
     return g_dev_tables[dev];
 }
 
-hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
-                          size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
-                          hipStream_t s) {
+hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
+                                size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
+                                uint64_t block_off, uint32_t idx_sub, hipStream_t s) {
     const size_t total = n * ((rec_per_client + 1) / 2);
     if (total == 0) return hipSuccess;
     uint32_t *tables = device_tables(s);
@@ -173,11 +179,20 @@ hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_clie
     if (blocks > 16384) blocks = 16384;
     if (bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0)
         hipLaunchKernelGGL(aes_ctr_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, cipher, n,
-                           bytes_per_client, rec_per_client, round_keys, tables, plain);
+                           bytes_per_client, rec_per_client, round_keys, tables, plain, block_off,
+                           idx_sub);
     else
         hipLaunchKernelGGL(aes_ctr_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, cipher,
-                           n, bytes_per_client, rec_per_client, round_keys, tables, plain);
+                           n, bytes_per_client, rec_per_client, round_keys, tables, plain,
+                           block_off, idx_sub);
     return hipGetLastError();
+}
+
+hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
+                          size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
+                          hipStream_t s) {
+    return launch_aes_ctr_slice(cipher, n, bytes_per_client, rec_per_client, round_keys, plain, 0,
+                                0, s);
 }
 
 // host-side single block, for the CPU self-test (no GPU needed)

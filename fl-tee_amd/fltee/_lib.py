@@ -87,6 +87,8 @@ SIGNATURES = {
     "fltee_safe_aggregate_device": (_U32, [_P, _S, _S, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_version": (ctypes.c_char_p, []),
+    "fltee_device_init_multi": (_U32, [_P, ctypes.c_int, _P]),
+    "fltee_device_count": (ctypes.c_int, [_U64]),
 }
 EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_aes_block": (None, [_P, _P, _P]),

@@ -27,13 +27,24 @@ def _as_u8(buf):
 
 
 class Enclave:
+    """device: one HIP device id, or a list of them for an eid over several GPUs
+    (fltee_device_init_multi: the ECALLs shard internally; the same id repeated gives
+    virtual ranks on one GPU)."""
+
     def __init__(self, device=0):
         self.lib = L.lib()
         eid = ctypes.c_uint64(0)
-        st = self.lib.fltee_device_init(device, ctypes.byref(eid))
+        if isinstance(device, (list, tuple)):
+            devs = (ctypes.c_int * len(device))(*device)
+            st = self.lib.fltee_device_init_multi(devs, len(device), ctypes.byref(eid))
+        else:
+            st = self.lib.fltee_device_init(device, ctypes.byref(eid))
         if st != L.SUCCESS:
             raise RuntimeError(f"fltee_device_init({device}) failed: {st:#x}")
         self.eid = eid.value
+
+    def device_count(self):
+        return self.lib.fltee_device_count(self.eid)
 
     def geteid(self):
         return self.eid

@@ -29,6 +29,10 @@
  *                     server.rs:241-245); the library serialises them with one
  *                     process-wide mutex (the enclave had one TCS,
  *                     Enclave.config.xml:6) and binds the eid's device per call.
+ *                     The device-resident entry points below share per-device
+ *                     scratch: calls for one device must not overlap in time on
+ *                     different streams (the mutex orders the host calls; the
+ *                     kernels of two streams could still interleave).
  */
 #ifndef FLTEE_AGG_H
 #define FLTEE_AGG_H
@@ -65,6 +69,21 @@ typedef uint64_t fltee_eid_t;
 /* ------------------------------------------------------------------------ */
 fltee_status_t fltee_device_init(int hip_device, fltee_eid_t *eid);
 fltee_status_t fltee_device_fini(fltee_eid_t eid);
+
+/* One enclave id over n GPUs of this node (n a power of two): the four ECALLs of that
+ * eid shard the aggregation internally and return the same bits as one
+ * GPU.  Dense uploads (baseline / non_oblivious / path_oram with k = d): parameter-range
+ * shards, each GPU copies and decrypts only its columns of the host ciphertext over its
+ * own PCIe link, RCCL gathers the averaged slices on the root (hip_devices[0]).
+ * advanced: position-range sharded bitonic network (RCCL all-to-alls), halo fold,
+ * compaction and one RCCL reduce.  nips19: the same network (pairwise exchanges), the
+ * ranges' selected entries gathered in order to the root.  alg 6: the batches split
+ * over the GPUs, the batch sums summed in order on the root.  Sparse flat algorithms
+ * run on the root.  Devices all distinct: RCCL over xGMI; the same device repeated n
+ * times: n virtual ranks on that GPU (exchanges are device copies; for tests). */
+fltee_status_t fltee_device_init_multi(const int *hip_devices, int n, fltee_eid_t *eid);
+/* GPUs (ranks) behind an eid: 1 for fltee_device_init, n for _multi, 0 if unknown. */
+int fltee_device_count(fltee_eid_t eid);
 
 /* ------------------------------------------------------------------------ */
 /* The four ECALLs (ecalls.rs:6-64 / Enclave.edl:26-73)                      */

@@ -1,0 +1,129 @@
+"""A multi-GPU enclave id behind the unchanged ECALL ABI (fltee_device_init_multi,
+group.hip): every algorithm returns the same bits as the single-GPU eid.
+
+On the one-GPU test box the ranks are virtual (the same device repeated: every range
+on one GPU, the exchanges device copies) — the sharding, the distributed network,
+the halo fold, the reduce and the gathers all run exactly as on W GPUs; only the
+transport differs.  [0] alone opens a one-rank RCCL communicator, so the RCCL
+calls themselves (ncclCommInitAll, grouped send/recv, ncclReduce) run too.  The
+8-GPU RCCL path is measured by bench.py's multi-GPU run (extra.c_abi_multi_gpu).
+"""
+import numpy as np
+import pytest
+
+import refcheck as R
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+SEED = 0x6A0
+
+
+@pytest.fixture(scope="module")
+def enclaves():
+    import torch
+    torch.cuda.init()
+    from fltee.ecalls import Enclave
+    es = {1: Enclave(0), "rccl1": Enclave([0])}
+    for w in (2, 4, 8):
+        es[w] = Enclave([0] * w)
+    yield es
+    for e in es.values():
+        e.destroy()
+
+
+_fl = [5000]
+
+
+def run(E, c, alg, enc, batch=None, k=None):
+    from fltee.ecalls import set_debug_seed
+    _fl[0] += 1
+    fl = _fl[0]
+    ids = c["client_ids"]
+    k = c["k"] if k is None else k
+    set_debug_seed(SEED)
+    assert E.ecall_fl_init(fl, ids, c["d"], k, 1.12, 1.0, 0.1, 1.0, alg, 0, 0) == (0, 0)
+    assert E.ecall_start_round(fl, 0, len(ids))[:2] == (0, 0)
+    if alg == 6:
+        st, rv, out, times = E.ecall_client_size_optimized_secure_aggregation(
+            fl, 0, batch, ids, enc, c["d"], k, 6)
+    else:
+        st, rv, out, times = E.ecall_secure_aggregation(fl, 0, ids, enc, c["d"], k, alg)
+    set_debug_seed(0)
+    assert (st, rv) == (0, 0)
+    assert np.isfinite(times).all()
+    return out
+
+
+_enc = {}
+
+
+def payload(oracle, c):
+    if c["name"] not in _enc:
+        w = R.records(c).reshape(c["n"], c["k"])
+        _enc[c["name"]] = oracle.encrypt_clients(c["client_ids"], [w[i].tobytes() for i in range(c["n"])])
+    return _enc[c["name"]]
+
+
+def test_device_counts(enclaves):
+    assert enclaves[1].device_count() == 1 and enclaves["rccl1"].device_count() == 1
+    assert [enclaves[w].device_count() for w in (2, 4, 8)] == [2, 4, 8]
+
+
+def test_bad_device_lists_are_refused():
+    from fltee.ecalls import Enclave
+    for devs in ([], [0, 0, 0], [0] * 128):
+        with pytest.raises(RuntimeError):
+            Enclave(devs)
+
+
+CASES = [("dense_n30", 3), ("dense_n30", 4), ("dense_n32", 5), ("sparse_n32", 4), ("sparse_n30", 3),
+         ("sparse_n32", 1), ("sparse_n100", 1), ("sparse_n4", 1), ("sparse_n32", 2), ("sparse_n100", 2),
+         ("dense_n4", 2)]
+
+
+@pytest.mark.parametrize("name,alg", CASES)
+@pytest.mark.parametrize("w", [2, 4, 8, "rccl1"])
+def test_group_ecall_bit_identical_to_one_gpu(enclaves, oracle, name, alg, w):
+    c = R.case(name)
+    enc = payload(oracle, c)
+    one = run(enclaves[1], c, alg, enc)
+    grp = run(enclaves[w], c, alg, enc)
+    assert np.array_equal(one.view(np.uint32), grp.view(np.uint32))
+    if alg in (3, 4, 5):
+        R.assert_in_order_exact(grp, c)
+    else:
+        R.assert_reassociated(grp, c)
+
+
+@pytest.mark.parametrize("name,batch", [("sparse_n32", 5), ("sparse_n30", 30), ("sparse_n100", 7)])
+@pytest.mark.parametrize("w", [2, 8, "rccl1"])
+def test_group_alg6_bit_identical_to_one_gpu(enclaves, oracle, name, batch, w):
+    c = R.case(name)
+    enc = payload(oracle, c)
+    one = run(enclaves[1], c, 6, enc, batch=batch)
+    grp = run(enclaves[w], c, 6, enc, batch=batch)
+    assert np.array_equal(one.view(np.uint32), grp.view(np.uint32))
+    R.assert_reassociated(grp, c)
+
+
+def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
+    """A client repeating one index (fold halo widening on every range) and the k=0
+    dense quirk (advanced.rs:70, the root path): both equal the single-GPU result."""
+    rng = np.random.default_rng(3)
+    n, k, d = 16, 3000, 3000
+    ids = np.arange(900, 900 + n, dtype=np.uint32)
+    recs = []
+    for i in range(n):
+        w = np.zeros(k, dtype=oracle.WEIGHT)
+        w["idx"] = 11 if i == 5 else rng.permutation(d)[:k]
+        w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        recs.append(w)
+    enc = oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
+    c = dict(client_ids=ids, d=d, k=k, n=n, name="long")
+    one = run(enclaves[1], c, 1, enc)
+    for w in (2, 8):
+        assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, 1, enc).view(np.uint32))
+    one0 = run(enclaves[1], c, 1, enc, k=0)
+    assert np.array_equal(one0.view(np.uint32), run(enclaves[4], c, 1, enc, k=0).view(np.uint32))
