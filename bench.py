@@ -527,6 +527,24 @@ def e2e_sample(torch, D, n, d, device, reps=3):
                 "AES left after the last chunk landed, aggregate+D2H}")
 
 
+def c_abi_multi_gpu(world):
+    """The multi-GPU path as the Rust host reaches it: ECALLs on one enclave id over all
+    `world` GPUs (fltee_device_init_multi), host-inclusive, vs a one-GPU eid
+    (scripts/ecall_multi_bench.py).  Run in a child process: it opens its own RCCL
+    communicators over the node's GPUs while this job's ranks wait on a host barrier."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "ecall_multi_bench.py"), "--devices",
+           str(world)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+    except Exception as ex:  # noqa: BLE001 - reported, never fatal for the bench line
+        return {"error": repr(ex)}
+    lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc={r.returncode}", "stderr": r.stderr[-1500:]}
+    return json.loads(lines[-1])
+
+
 def traffic_from_profiles(name):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
@@ -657,6 +675,16 @@ def main():
                 exchange="pairwise")
             sharded["c4_index_sharded"] = bench_c4_index_sharded(
                 torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
+        if os.environ.get("FLTEE_BENCH_NO_CABI") != "1":
+            # the C-ABI multi-GPU eid, in a child of rank 0 while every rank waits on a
+            # host (gloo) barrier with its cached HBM released
+            hostpg = dist.new_group(backend="gloo")
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            dist.barrier(group=hostpg)
+            if rank == 0:
+                sharded["c_abi_multi_gpu"] = c_abi_multi_gpu(world)
+            dist.barrier(group=hostpg)
 
     if rank == 0:
         line = {
