@@ -390,17 +390,40 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         t2 = now_s();
         if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
     }
-    if (st == FLTEE_GROUP_FALLBACK) {
+    const bool sharded = G && ((aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc) ||
+                               aggregation_alg == FLTEE_ALG_NIPS19);
+    if (st == FLTEE_GROUP_FALLBACK && sharded && group_splits_host_copy(G)) {
+        // every GPU copies and decrypts the clients of its own position range
+        std::vector<uint32_t> rk;
+        client_round_keys(client_ids, n, rk);
+        GroupInput in;
+        in.enc = encrypted_parameters_data;
+        in.rk = rk.data();
+        in.bpc = bpc;
+        in.t_load = &execution_time_results[0];
+        in.t_dec = &execution_time_results[1];
+        const double ta = now_s();
+        if (aggregation_alg == FLTEE_ALG_ADVANCED)
+            st = group_advanced(G, in, n, rpc, d, coef, d_out);
+        else
+            st = group_nips19(G, c, in, n, rpc, k_req, d, next_seed(), coef, d_out);
+        if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
+        // "Aggregation" = the call minus its load and decrypt phases
+        t2 = ta + execution_time_results[0] + execution_time_results[1];
+    }
+    if (st == FLTEE_GROUP_FALLBACK) {  // (a shape the per-GPU path declines comes here too)
         st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data, bpc,
                               &execution_time_results[0], &execution_time_results[1]);
         if (st) return fail(st);
         t2 = now_s();
         st = FLTEE_GROUP_FALLBACK;
         uint64_t seed = 0;
+        GroupInput in;
+        in.root_rec = (const uint64_t *)c->records.ptr;
         if (G && aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc)
-            st = group_advanced(G, c->records.ptr, n, rpc, d, coef, d_out);
+            st = group_advanced(G, in, n, rpc, d, coef, d_out);
         else if (G && aggregation_alg == FLTEE_ALG_NIPS19)
-            st = group_nips19(G, c, c->records.ptr, n, rpc, k_req, d, seed = next_seed(), coef, d_out);
+            st = group_nips19(G, c, in, n, rpc, k_req, d, seed = next_seed(), coef, d_out);
         if (st == FLTEE_GROUP_FALLBACK)  // one device (or a shape the group does not shard)
             st = aggregate_records(c, aggregation_alg, n, rpc, d, k_req, 0, d_out, seed);
     }
@@ -450,16 +473,35 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
 
     float t_load = 0, t_dec = 0;
     const double t1 = now_s();
-    uint32_t st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data_ptr, k * 8, &t_load, &t_dec);
-    if (st) return fail(st);
-    execution_time_results[0] = t_load;
     float *d_out = nullptr;
     if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
     d_out = (float *)c->outbuf.ptr;
-    if (Group *G = group_of(eid))  // the batches split over the eid's GPUs (group.hip)
-        st = group_optimized(G, c->records.ptr, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
-    else
-        st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
+    uint32_t st;
+    Group *G = group_of(eid);
+    if (G && group_splits_host_copy(G)) {
+        // the batches split over the eid's GPUs, each loading its own clients (group.hip)
+        std::vector<uint32_t> rk;
+        client_round_keys(client_ids, n, rk);
+        GroupInput in;
+        in.enc = encrypted_parameters_data_ptr;
+        in.rk = rk.data();
+        in.bpc = k * 8;
+        in.t_load = &t_load;
+        in.t_dec = &t_dec;
+        st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
+        execution_time_results[0] = t_load;
+    } else {
+        st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data_ptr, k * 8, &t_load, &t_dec);
+        if (st) return fail(st);
+        execution_time_results[0] = t_load;
+        if (G) {
+            GroupInput in;
+            in.root_rec = (const uint64_t *)c->records.ptr;
+            st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
+        } else {
+            st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
+        }
+    }
     if (!st && cfg.dp) {  // lib.rs:586-588
         if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
             st = FLTEE_ERROR_UNEXPECTED;

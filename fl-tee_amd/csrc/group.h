@@ -20,12 +20,24 @@ hipStream_t group_root_stream(const Group *G);
 // the n clients' AES round keys (44 words each); d_out_root gets the averaged f32[d]
 uint32_t group_dense_ecall(Group *G, const uint32_t *rk_host, size_t n, const uint8_t *enc,
                            size_t d, float coef, float *d_out_root, float *t_load, float *t_dec);
-// on records decrypted into the root device's HBM (client-major, n x k)
-uint32_t group_advanced(Group *G, const void *root_rec, size_t n, size_t k, size_t d, float coef,
+// Where the client-major n x k records come from: decrypted into the root device's HBM
+// (root_rec), or the host ciphertext (enc, bpc bytes per client, rk = the clients' round
+// keys): then every GPU of the eid copies and decrypts the clients covering its own
+// range (t_load / t_dec: the ECALL's "Loading" / "Decryption" times).
+struct GroupInput {
+    const uint64_t *root_rec = nullptr;
+    const uint8_t *enc = nullptr;
+    const uint32_t *rk = nullptr;
+    size_t bpc = 0;
+    float *t_load = nullptr, *t_dec = nullptr;
+};
+uint32_t group_advanced(Group *G, const GroupInput &in, size_t n, size_t k, size_t d, float coef,
                         float *d_out_root);
-uint32_t group_nips19(Group *G, DeviceCtx *root, const void *root_rec, size_t n, size_t k,
+uint32_t group_nips19(Group *G, DeviceCtx *root, const GroupInput &in, size_t n, size_t k,
                       size_t k_req, size_t d, uint64_t seed, float coef, float *d_out_root);
-uint32_t group_optimized(Group *G, const void *root_rec, size_t n, size_t k, size_t d,
+uint32_t group_optimized(Group *G, const GroupInput &in, size_t n, size_t k, size_t d,
                          size_t batch, float coef, float *d_out_root);
+// true when the group loads the host ciphertext per GPU (eids of > 1 rank)
+bool group_splits_host_copy(const Group *G);
 
 }  // namespace fltee

@@ -314,6 +314,66 @@ static hipError_t scatter_records(Group &G, const uint64_t *root_rec, size_t nre
     return p2p(G, ops);
 }
 
+// The records each rank needs: positions [lo[i], hi[i]) of the n*rpc client-major
+// records.  From the host ciphertext (in.enc): every GPU copies the whole
+// clients that cover its range over its own PCIe link (one host thread per GPU) and
+// decrypts them itself; rec_r[i] points at position lo[i].  Otherwise from the root's
+// decrypted records (scatter_records).  Virtual ranks take the per-GPU path too (all
+// on one device), so the one-GPU tests cover its client ranges and offsets.
+static uint32_t group_records(Group &G, const GroupInput &in, size_t n, size_t rpc,
+                              const std::vector<size_t> &lo, const std::vector<size_t> &hi,
+                              std::vector<const uint64_t *> &rec_r) {
+    const size_t nrec = n * rpc;
+    if (!in.enc) {
+        if (!in.root_rec) return FLTEE_ERROR_UNEXPECTED;
+        return scatter_records(G, in.root_rec, nrec, lo, hi, rec_r) == hipSuccess
+                   ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+    }
+    const int W = G.W;
+    rec_r.assign(W, nullptr);
+    std::vector<size_t> c_lo(W), c_hi(W);
+    std::vector<uint32_t> errs(W, 0);
+    for (int i = 0; i < W; ++i) {
+        const size_t a = lo[i] < nrec ? lo[i] : nrec, b = hi[i] < nrec ? hi[i] : nrec;
+        c_lo[i] = rpc ? a / rpc : 0;
+        c_hi[i] = (rpc && b > a) ? (b + rpc - 1) / rpc : c_lo[i];
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    auto load = [&](int i) {
+        Rank &R = G.r[i];
+        const size_t nc = c_hi[i] - c_lo[i];
+        if (hipSetDevice(R.dev) != hipSuccess) { errs[i] = 1; return; }
+        if (!R.cipher.reserve(nc * in.bpc + 16) || !R.rec.reserve(nc * rpc * 8 + 16) ||
+            !R.rk.reserve(nc * 44 * 4 + 16)) { errs[i] = 3; return; }
+        if (nc == 0) return;
+        if (hipMemcpyAsync(R.rk.ptr, in.rk + c_lo[i] * 44, nc * 44 * 4, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+            hipMemcpyAsync(R.cipher.ptr, in.enc + c_lo[i] * in.bpc, nc * in.bpc, hipMemcpyHostToDevice,
+                           R.s) != hipSuccess ||
+            hipStreamSynchronize(R.s) != hipSuccess)
+            errs[i] = 1;
+    };
+    std::vector<std::thread> th;
+    for (int i = 0; i < W; ++i) th.emplace_back(load, i);
+    for (auto &t : th) t.join();
+    for (int i = 0; i < W; ++i)
+        if (errs[i]) return errs[i] == 3 ? FLTEE_ERROR_OUT_OF_MEMORY : FLTEE_ERROR_UNEXPECTED;
+    const auto t1 = std::chrono::steady_clock::now();
+    for (int i = 0; i < W; ++i) {
+        Rank &R = G.r[i];
+        const size_t nc = c_hi[i] - c_lo[i];
+        rec_r[i] = (const uint64_t *)R.rec.ptr + (lo[i] < nrec ? lo[i] - c_lo[i] * rpc : 0);
+        if (nc == 0) continue;
+        if (hipSetDevice(R.dev) != hipSuccess ||
+            launch_aes_ctr((const uint8_t *)R.cipher.ptr, nc, in.bpc, rpc, (const uint32_t *)R.rk.ptr,
+                           (uint8_t *)R.rec.ptr, R.s) != hipSuccess)
+            return FLTEE_ERROR_UNEXPECTED;
+    }
+    if (sync_all(G) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (in.t_load) *in.t_load = std::chrono::duration<float>(t1 - t0).count();
+    if (in.t_dec) *in.t_dec = std::chrono::duration<float>(std::chrono::steady_clock::now() - t1).count();
+    return FLTEE_SUCCESS;
+}
+
 // ================================================================ dense =====
 // Parameter-range shard of dense uploads, straight from the host ciphertext.
 uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const uint8_t *enc,
@@ -456,7 +516,7 @@ static bool reserve_chunks(Group &G, size_t C, std::vector<uint64_t *> &chunk,
 }
 
 // ============================================================= advanced =====
-uint32_t group_advanced(Group *Gp, const void *root_rec, size_t n, size_t k, size_t d,
+uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, size_t d,
                         float coef, float *d_out_root) {
     Group &G = *Gp;
     const int W = G.W;
@@ -467,8 +527,7 @@ uint32_t group_advanced(Group *Gp, const void *root_rec, size_t n, size_t k, siz
     std::vector<size_t> lo(W), hi(W);
     for (int i = 0; i < W; ++i) lo[i] = i * C, hi[i] = (i + 1) * C;
     std::vector<const uint64_t *> rec;
-    if (scatter_records(G, (const uint64_t *)root_rec, nrec, lo, hi, rec) != hipSuccess)
-        return FLTEE_ERROR_UNEXPECTED;
+    if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
     for (int i = 0; i < W; ++i) {  // advanced.rs:116-142 on each range
         if (hipSetDevice(G.r[i].dev) != hipSuccess ||
             launch_advanced_init_range(rec[i], nrec, d, i * C, C, chunk[i], G.r[i].s) != hipSuccess)
@@ -534,7 +593,7 @@ uint32_t group_advanced(Group *Gp, const void *root_rec, size_t n, size_t k, siz
 }
 
 // =============================================================== nips19 =====
-uint32_t group_nips19(Group *Gp, DeviceCtx *root, const void *root_rec, size_t n, size_t k,
+uint32_t group_nips19(Group *Gp, DeviceCtx *root, const GroupInput &in, size_t n, size_t k,
                       size_t k_req, size_t d, uint64_t seed, float coef, float *d_out_root) {
     Group &G = *Gp;
     const int W = G.W;
@@ -548,8 +607,7 @@ uint32_t group_nips19(Group *Gp, DeviceCtx *root, const void *root_rec, size_t n
     std::vector<size_t> lo(W), hi(W);
     for (int i = 0; i < W; ++i) lo[i] = i * C, hi[i] = (i + 1) * C;
     std::vector<const uint64_t *> rec;
-    if (scatter_records(G, (const uint64_t *)root_rec, nrec, lo, hi, rec) != hipSuccess)
-        return FLTEE_ERROR_UNEXPECTED;
+    if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
     for (int i = 0; i < W; ++i) {  // every rank draws the same counts (counter-based Philox)
         Rank &R = G.r[i];
         if (!reserve_on(R, R.lap, d * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
@@ -601,7 +659,7 @@ uint32_t group_nips19(Group *Gp, DeviceCtx *root, const void *root_rec, size_t n
 }
 
 // ========================================================= optimized (alg 6) =
-uint32_t group_optimized(Group *Gp, const void *root_rec, size_t n, size_t k, size_t d,
+uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, size_t d,
                          size_t batch, float coef, float *d_out_root) {
     Group &G = *Gp;
     const int W = G.W;
@@ -616,8 +674,7 @@ uint32_t group_optimized(Group *Gp, const void *root_rec, size_t n, size_t k, si
         hi[i] = (b1[i] * batch < n ? b1[i] * batch : n) * k;
     }
     std::vector<const uint64_t *> rec;
-    if (scatter_records(G, (const uint64_t *)root_rec, n * k, lo, hi, rec) != hipSuccess)
-        return FLTEE_ERROR_UNEXPECTED;
+    if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
     size_t h = n;
     const size_t max_run = n * k + d;
     for (int attempt = 0;; ++attempt) {
@@ -660,4 +717,8 @@ uint32_t group_optimized(Group *Gp, const void *root_rec, size_t n, size_t k, si
     return sync_all(G) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
 }
 
+}  // namespace fltee
+
+namespace fltee {
+bool group_splits_host_copy(const Group *G) { return G && G->W > 1; }
 }  // namespace fltee

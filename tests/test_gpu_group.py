@@ -127,3 +127,24 @@ def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
         assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, 1, enc).view(np.uint32))
     one0 = run(enclaves[1], c, 1, enc, k=0)
     assert np.array_equal(one0.view(np.uint32), run(enclaves[4], c, 1, enc, k=0).view(np.uint32))
+
+
+@pytest.mark.parametrize("alg", [1, 2, 4])
+def test_group_ragged_payload(enclaves, oracle, alg):
+    """Client slices of 8*k + 3 bytes (lib.rs:305-306 floors bytes and records per
+    client): every GPU loads whole clients that cover its range at byte offsets that are
+    not record-aligned; the result equals the single-GPU eid's."""
+    rng = np.random.default_rng(alg)
+    n, k, d = 10, 301, 1000
+    ids = np.arange(70, 70 + n, dtype=np.uint32)
+    slices = []
+    for i in ids:
+        w = np.zeros(k, dtype=oracle.WEIGHT)
+        w["idx"] = rng.permutation(d)[:k]
+        w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        slices.append(oracle.aes128_ctr(oracle.session_key(int(i)), w.tobytes() + b"\x01\x02\x03"))
+    enc = b"".join(slices)
+    c = dict(client_ids=ids, d=d, k=k, n=n, name=f"ragged{alg}")
+    one = run(enclaves[1], c, alg, enc)
+    for w in (2, 8):
+        assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, alg, enc).view(np.uint32))
