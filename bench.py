@@ -110,9 +110,51 @@ def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False):
 
     wall, kern = time_steps(torch, step, steps, warmup, stream)
     assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
+    net = net_stats(torch, lambda: step(0))
     del recs
     return dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
-                rate=n * kk / kern, bytes=n * kk * 8 + d * 4, nbuf=nbuf)
+                rate=n * kk / kern, bytes=n * kk * 8 + d * 4, nbuf=nbuf, net=net)
+
+
+def net_stats(torch, call):
+    """Streaming passes one aggregate launches and the bytes they sweep (the library's
+    launch-side accounting: read + write of the array per pass)."""
+    from fltee import _lib as L
+    lib = L.lib()
+    a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lib.fltee_debug_net_stats(ctypes.byref(a), ctypes.byref(b), 1)
+    call()
+    torch.cuda.synchronize()
+    lib.fltee_debug_net_stats(ctypes.byref(a), ctypes.byref(b), 1)
+    return dict(passes=a.value, bytes=b.value)
+
+
+def dominant_kernel(name):
+    """The kernel with the largest total time in the committed rocprofv3 summary of this
+    config (profiles/r02/<name>_kernel_stats.csv), or None."""
+    import csv
+    path = os.path.join(ROOT, "profiles", "r02", f"{name}_kernel_stats.csv")
+    try:
+        with open(path) as f:
+            rows = [r for r in csv.DictReader(f) if "fltee::" in r["Name"]]
+    except (OSError, KeyError):
+        return None
+    if not rows:
+        return None
+    r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    return dict(kernel=r["Name"].split("(")[0], calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
+                source=os.path.relpath(path, ROOT))
+
+
+def network_records(w):
+    """Entries of the array the oblivious network sorts for workload w (0: none)."""
+    n, d, k = w["n"], w["d"], w["k"] or w["d"]
+    if w["alg"] == 1:
+        return 1 << (n * k + d - 1).bit_length()
+    if w["alg"] == 2:
+        T = np.float32(2 * k) / np.float32(100.0) * np.float32(np.log(np.float32(d) * np.float32(n)))
+        return 1 << (n * k + d * int(T) - 1).bit_length()
+    return 0
 
 
 def bench_c5_sharded(torch, D, dist, world, rank, device, steps, warmup):
@@ -722,6 +764,23 @@ def main():
                                    k=r["k"], ms_per_step=r["wall_s"] * 1e3 / ksteps,
                                    kernel_ms=r["kernel_s"] * 1e3, value=r["rate"],
                                    unit="client-params/s")
+                M = network_records(wl)
+                if M:  # the oblivious paths: their network traffic, not the useful bytes
+                    nb = r["net"]["bytes"]
+                    roof = dict(bound="hbm", network_passes=r["net"]["passes"], network_bytes=nb,
+                                network_records=M,
+                                achieved=nb / r["kernel_s"] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
+                                frac=nb / r["kernel_s"] / 1e9 / HBM_PEAK_GBS,
+                                algorithmic_bytes=r["bytes"],
+                                note="network bytes = read + write of the array per streaming pass "
+                                     "(launch-side accounting); achieved = those bytes / the "
+                                     "aggregate's event time")
+                    dk = dominant_kernel(name)
+                    if dk:
+                        dk["bytes_per_launch"] = 16 * M
+                        dk["achieved_gbs"] = 16 * M / (dk["avg_us"] * 1e-6) / 1e9
+                        roof["dominant_kernel"] = dk
+                    extra[name]["roofline"] = roof
             line["extra"] = extra
             # the metric's literal configuration (100 clients x MLP-MNIST, dense baseline),
             # inputs rotated through > 1.5 x the Infinity Cache so every launch reads HBM

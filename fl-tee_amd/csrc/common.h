@@ -69,6 +69,11 @@ static inline uint32_t log2_pow2(size_t x) {
 // ---- kernel launchers (implemented in the k_*.hip files) ------------------
 namespace fltee {
 
+// Measurement: HBM bytes the streaming passes of the networks move (algorithmic per
+// launch: read + write of the array they sweep), counted at launch on the host
+// (engine.hip; read by bench.py through fltee_debug_net_stats).
+void net_account(uint64_t bytes);
+
 // k_accumulate.hip
 hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,
                                    const float *client_coef, bool accumulate, uint32_t *status,

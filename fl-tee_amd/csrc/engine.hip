@@ -41,6 +41,12 @@ static std::mutex g_ctx_mu;
 static std::atomic<uint64_t> g_debug_seed{0};
 static std::atomic<uint64_t> g_seed_calls{0};
 
+static std::atomic<uint64_t> g_net_launches{0}, g_net_bytes{0};
+void net_account(uint64_t bytes) {
+    g_net_launches.fetch_add(1, std::memory_order_relaxed);
+    g_net_bytes.fetch_add(bytes, std::memory_order_relaxed);
+}
+
 uint64_t next_seed() {
     const uint64_t s = g_debug_seed.load();
     if (s) return s + 0x9E3779B97F4A7C15ull * (++g_seed_calls);
@@ -607,6 +613,16 @@ extern "C" fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t 
 }
 
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
+
+// measurement hook: streaming passes launched and the bytes they sweep since the last reset
+extern "C" void fltee_debug_net_stats(uint64_t *launches, uint64_t *bytes, int reset) {
+    if (launches) *launches = fltee::g_net_launches.load();
+    if (bytes) *bytes = fltee::g_net_bytes.load();
+    if (reset) {
+        fltee::g_net_launches.store(0);
+        fltee::g_net_bytes.store(0);
+    }
+}
 
 extern "C" fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d,
                                                 float coef, float *d_out, void *stream) {

@@ -525,6 +525,7 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
                                 int R, uint32_t seed, hipStream_t s, uint32_t pbase) {
     const uint32_t ngroups = 1u << (mlog - R);
     const unsigned blocks = (ngroups + 255) / 256;
+    net_account((uint64_t)16 << mlog);
     switch (R) {
     case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
     case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
@@ -616,6 +617,7 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
+    net_account((uint64_t)16 * tiles << tlog);
     hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
                        tlog, ilog, wlog, dtile, seed, tiles, pbase);
     return hipGetLastError();
@@ -664,6 +666,7 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     const int rest = (int)c.tlog - (int)(STRIDED ? wlog : 0u) - R1;  // steps after the register round
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
+    net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog);  // the select pass writes ~nothing
 #define BD_GO1(RL_, SEL_)                                                                          \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -700,6 +703,7 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
                                      uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{}) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
+    net_account((uint64_t)16 * c.tiles << c.tlog);
 #define BS_GO(RL_)                                                                                 \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -1074,6 +1078,7 @@ hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, ui
     const uint32_t lower = pos_mine < pos_theirs;
     const uint32_t pos_lo = lower ? pos_mine : pos_theirs;
     const uint32_t key = mode == 2 ? shuffle_step_key(seed, ilog, jlog) : 0u;
+    net_account((uint64_t)24 * m);
 #define BX_GO(MD)                                                                                  \
     hipLaunchKernelGGL((bitonic_exchange_kernel<MD>), dim3((unsigned)blocks), dim3(256), 0, s,     \
                        (uint4 *)mine, (const uint4 *)theirs, m2, pos_lo, lower, ilog, key)

@@ -233,6 +233,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         if (ntiles == 0 || ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
+        net_account((uint64_t)(last ? 8 : 16) * L);
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
         const int blk = j0 == 0 ? 2 : compact_blocks();
         const unsigned res = small ? 256u * (unsigned)blk : 256u;

@@ -210,6 +210,7 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     if (clog >= 4 && clog <= 20) C = (size_t)1 << clog;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
+    net_account((uint64_t)16 * span);
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     int depth = blocks <= 256 ? 2 : 1;  // about one wave per CU: latency-bound, prefetch deeper
     static const int dk = fold_knob("FLTEE_FOLD_DEPTH");
