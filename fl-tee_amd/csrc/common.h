@@ -134,6 +134,10 @@ hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold
 hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
                           hipStream_t s);
 // k_compact.hip
+// fold (fold_len == L) + compaction from the SORTED array; hipErrorNotSupported: fold apart
+hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
+                                       size_t halo, float coef, float *out, bool accumulate,
+                                       uint32_t *status, hipStream_t s);
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
                                   float *out, bool accumulate, hipStream_t s);
 hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint64_t *buf,

@@ -241,12 +241,17 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         e = launch_advanced_init(rec, n * k, d, M, A, s);
         if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
     }
-    if (e == hipSuccess) e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
     if (e != hipSuccess) return e;
     // Second sort (advanced.rs:106-111): with fold_len == L its [0, d) prefix is the
-    // order-preserving compaction of the idx < d representatives (k_compact.hip);
-    // the k_req != k quirk leaves unfolded records competing for that prefix and
-    // keeps the full network.
+    // order-preserving compaction of the idx < d representatives (k_compact.hip), and
+    // the fold runs inside the compaction's first pass; the k_req != k quirk leaves
+    // unfolded records competing for that prefix and keeps the full network.
+    if (fold_len == L && g_advanced_compaction) {
+        e = launch_fold_compact_extract(A, B, M, L, d, halo ? halo : n, coef, out, acc, status, s);
+        if (e != hipErrorNotSupported) return e;
+    }
+    e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
+    if (e != hipSuccess) return e;
     if (fold_len == L && g_advanced_compaction)
         return launch_compact_extract(B, A, L, d, coef, out, acc, s);
     e = bitonic_sort(B, M, 0, 0, s);
@@ -643,12 +648,14 @@ extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float si
                : FLTEE_ERROR_UNEXPECTED;
 }
 
-namespace fltee { void set_dense_variant(int v); void set_compact_variant(int v); }
+namespace fltee { void set_dense_variant(int v); void set_compact_variant(int v); void set_fold_compact(int on); }
 // tuning hook (not part of the public header)
 extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(v); }
 // A/B hook: 0 runs advanced's second bitonic sort instead of the compaction network
 extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_compaction = on != 0; }
 extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_variant(v); }
+// A/B hook: 0 runs advanced's fold as its own pass before the compaction
+extern "C" void fltee_debug_set_fold_compact(int on) { fltee::set_fold_compact(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes
 extern "C" void fltee_debug_set_nips19_fused_select(int on) { fltee::g_nips19_fused_select = on != 0; }

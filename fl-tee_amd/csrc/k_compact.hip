@@ -200,13 +200,13 @@ static uint32_t bitlen(uint64_t x) {
 // front of p); it sets the number of levels, bitlen(max_shift).
 static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t d,
                                  size_t max_shift, float coef, float *out, bool accumulate,
-                                 hipStream_t s) {
+                                 hipStream_t s, uint32_t j0_start = 0) {
     if (d == 0) return hipSuccess;
     const uint32_t nlev = bitlen(max_shift);
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
     if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets
     uint64_t *cur = src, *oth = tmp;
-    for (uint32_t j0 = 0; j0 < nlev;) {
+    for (uint32_t j0 = j0_start; j0 < nlev;) {
         const bool small = g_compact_variant == 1 || (g_compact_variant == 2 && j0 == 0);
         const uint32_t CAP = small ? 4096 : 8192;
         const uint32_t gmax = j0 == 0 ? (small ? 9 : 10) : (small ? 5 : 6);
@@ -258,6 +258,198 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
                                   float *out, bool accumulate, hipStream_t s) {
     return compact_levels(src, tmp, L, d, L > d ? L - d : 0, coef, out, accumulate, s);
+}
+
+// ------------------------------------------ fold fused into the first pass ---
+// advanced.rs:66-101 (the fold) and the compaction's first pass in one kernel: a tile
+// reads the SORTED array over its window [a - Hr, a + CAP] (Hr = the fold's halo, the
+// record after the tile for the run-end test), folds it in LDS and goes straight on
+// with the first G compaction levels.  The fold needs, per position p < L, only what
+// the compaction reads: whether p is its run's representative (the run's last
+// position: idx[p+1] != idx[p], or p = L-1) with idx < d, and then the run's sum —
+// v_head, (v_head + v_next), ... left to right, the enclave's order.  Every run head
+// in the window walks its run in LDS and leaves the sum in the val of the run's last
+// record; a run longer than the halo (its head before the window and its end at or
+// after the tile start) is reported as FLTEE_DEV_ERR_FOLD_OVERFLOW like the fold
+// kernel, and the caller reruns with a wider halo.  The folded array (1 GB at C5) is
+// never written and read back.  Dummies and non-representatives are never selected by
+// the compaction, so their contents do not matter.
+template <int NT, int PER, int FINAL>
+__global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__restrict__ A,
+                                                            uint64_t *__restrict__ dst, uint32_t L,
+                                                            uint32_t M, uint32_t d, uint32_t G,
+                                                            uint32_t S, uint32_t Hr,
+                                                            uint32_t ntiles, float coef,
+                                                            float *__restrict__ out,
+                                                            uint32_t *status) {
+    constexpr uint32_t CAP = (uint32_t)NT * PER;
+    constexpr uint32_t XMAX = 4096 / NT + 1;  // window slots beyond CAP per lane (Hr <= 4096)
+    extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1
+    const uint32_t H = (1u << G) - 1;
+    const uint32_t t = threadIdx.x;
+    const uint32_t Wn = Hr + CAP + 1;
+    const uint32_t chunk = (Wn + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, (short)0, (int)(M * 8u), 0x00020000);
+    // the window of tile tl into registers: lane t holds window slots t + i*NT; slots
+    // before position 0 or past M are dummies (clamped address, select after the load:
+    // no branch around the loads)
+    uint64_t pf[PER + XMAX];
+    auto prefetch = [&](uint32_t tl) {
+        const long long wlo = (long long)tl * S - (long long)Hr;
+#pragma unroll
+        for (uint32_t i = 0; i < PER + XMAX; ++i) {
+            const long long p = wlo + t + i * NT;
+            const bool ok = p >= 0 && p < (long long)M && t + i * NT < Wn;
+            const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
+                rs, (int)(ok ? (uint32_t)p * 8u : 0u), 0, 0);
+            pf[i] = ok ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
+        }
+    };
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    prefetch(tile);
+    for (;;) {
+        const long long a = (long long)tile * S, wlo = a - (long long)Hr;
+#pragma unroll
+        for (uint32_t i = 0; i < PER + XMAX; ++i)
+            if (t + i * NT < Wn) win[t + i * NT] = pf[i];
+        if (t == 0 && a < (long long)L && a - (long long)Hr - 1 >= 0 &&
+            (uint32_t)A[a - Hr - 1] == (uint32_t)A[a])
+            atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        // run heads walk their runs (left to right) and store the sum at the run's end
+        for (uint32_t x = t * chunk; x < (t + 1) * chunk && x < Wn; ++x) {
+            const long long p = wlo + x;
+            if (p < 0 || p >= (long long)L) continue;
+            const uint32_t k = (uint32_t)win[x];
+            if (!(x == 0 || p == 0 || (uint32_t)win[x - 1] != k)) continue;
+            float acc = rec_val(win[x]);
+            uint32_t y = x;
+            while (y + 1 < Wn && wlo + (long long)(y + 1) < (long long)L && (uint32_t)win[y + 1] == k) {
+                ++y;
+                acc = __fadd_rn(acc, rec_val(win[y]));
+            }
+            if (y + 1 < Wn || wlo + (long long)(y + 1) >= (long long)L)  // the run ends inside
+                win[y] = ((uint64_t)__float_as_uint(acc) << 32) | k;
+        }
+        __syncthreads();
+        // representatives with idx < d -> (c = p - idx, sum); the rest never move
+        uint64_t v[PER];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t f = t + i * NT, x = f + Hr;
+            const long long p = a + f;
+            const uint64_t r = win[x];
+            const uint32_t idx = (uint32_t)r;
+            const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
+            v[i] = (p < (long long)L && idx < d && end)
+                       ? ((r & 0xFFFFFFFF00000000ull) | (uint32_t)((uint32_t)p - idx))
+                       : CP_DUMMY;
+        }
+        __syncthreads();
+        uint64_t *sm = win;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) sm[t + i * NT] = v[i];
+        __syncthreads();
+        // the first G levels, exactly compact_pass's (contiguous: W = 1, j0 = 0)
+        uint64_t nv[PER];
+        for (uint32_t g = 0; g < G;) {
+            const uint32_t stepf = 1u << g;
+            const bool two = g + 1 < G;
+            const uint32_t gl = two ? g + 1 : g;
+            const uint32_t lim = S + H - ((2u << gl) - 1);
+            if (two) {
+#pragma unroll
+                for (uint32_t i = 0; i < PER; ++i) {
+                    const uint32_t f = t + i * NT;
+                    if (f < lim) {
+                        const uint64_t y0 = cp_pick(sm[f], sm[f + stepf], g);
+                        const uint64_t y2 = cp_pick(sm[f + 2 * stepf], sm[f + 3 * stepf], g);
+                        nv[i] = cp_pick(y0, y2, g + 1);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < PER; ++i) {
+                    const uint32_t f = t + i * NT;
+                    if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], g);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t i = 0; i < PER; ++i) {
+                const uint32_t f = t + i * NT;
+                if (f < lim) sm[f] = nv[i];
+            }
+            __syncthreads();
+            g += two ? 2 : 1;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t f = t + i * NT;
+            if (f < S) {
+                const long long p = a + f;
+                if (FINAL == 0) {
+                    if (p < (long long)L) dst[p] = sm[f];
+                } else if (p < (long long)d) {
+                    const float vv = rec_val(sm[f]);
+                    out[p] = FINAL == 2 ? __fadd_rn(out[p], vv) : __fmul_rn(vv, coef);
+                }
+            }
+        }
+        if (next >= ntiles) break;
+        __syncthreads();  // this tile's LDS reads retire before the next window lands
+        tile = next;
+    }
+}
+
+static bool g_fold_compact = true;  // fltee_debug_set_fold_compact (A/B)
+void set_fold_compact(int on) { g_fold_compact = on != 0; }
+
+// The fold (fold_len == L) + the compaction of `advanced`: sorted array A (M records,
+// [0, L) meaningful) -> out.  A and B are clobbered.  hipErrorNotSupported: not fused
+// here (halo wide against the 4096-record tile, or no levels): the caller folds separately.
+hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
+                                       size_t halo, float coef, float *out, bool accumulate,
+                                       uint32_t *status, hipStream_t s) {
+    constexpr uint32_t NT = 512, PER = 8, CAP = NT * PER;
+    const size_t Hr = fold_context(halo);
+    // A/B in one process (scripts/ab_fold_compact.py, profiles/r02/ab/fold_compact.jsonl):
+    // C3 (Hr = 112): 0.211 vs 0.214 ms with the separate fold; C5 (Hr = 1008, windows 25 %
+    // wider than the tile): 17.66 vs 17.48 ms.  Fused while the halo is under 1/8 of the tile.
+    if (!g_fold_compact || d == 0 || L <= d || Hr > 512 || M >= ((size_t)1 << 29) || L > M)
+        return hipErrorNotSupported;
+    const uint32_t nlev = bitlen(L - d);
+    const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1, S = CAP - H;
+    const uint64_t ntiles = (L + S - 1) / S;
+    const bool last = G == nlev;
+    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);
+    const size_t lds = (Hr + CAP + 1) * 8;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        attr = true;
+    }
+    net_account((uint64_t)(last ? 8 : 16) * L);
+#define FC_GO(F)                                                                                  \
+    hipLaunchKernelGGL((fold_compact_first<NT, PER, F>), dim3(grid), dim3(NT), lds, s, A, B,       \
+                       (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr,                 \
+                       (uint32_t)ntiles, coef, out, status)
+    if (!last) FC_GO(0);
+    else if (accumulate) FC_GO(2);
+    else FC_GO(1);
+#undef FC_GO
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || last) return e;
+    return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);
 }
 
 // ------------------------------------------------ one range of the array ---

@@ -473,6 +473,38 @@ def test_nips19_c4_full_size_bit_exact(dev, oracle):
     assert np.allclose(outdp, oracle.dp_noise(ref, 1.12, 1.0, n, seed), rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,d,k,repeat", [(100, 50890, 5089, False), (1000, 200000, 2000, False),
+                                          (3, 1000, 1000, False), (30, 3000, 400, True),
+                                          (3000, 30000, 16, False), (5000, 20000, 20, False)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_advanced_fold_fused_into_compaction(dev, oracle, n, d, k, repeat, fused):
+    """The fold run inside the compaction's first pass (halo n up to 4096 records; wider
+    halos fall back to the separate fold) == the oracle's advanced, bit for bit.  With a
+    repeated index (runs longer than the halo n) the default halo either still gives the
+    exact sums (the fused fold walks a run of any length inside its tile window) or
+    reports FLTEE_DEV_ERR_FOLD_OVERFLOW; the run-length halo is always exact."""
+    from fltee import _lib as L
+    rng = np.random.default_rng(n + d)
+    idx, val = rand_sparse(rng, n, d, k)
+    if repeat:
+        idx[:k] = 2200  # client 0 repeats one index k times: a run of ~k records
+    rec = cuda_records(dev, idx, val)
+    ref, rst = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert rst == 0
+    L.lib().fltee_debug_set_fold_compact(1 if fused else 0)
+    try:
+        out = dev.aggregate(1, rec, n, k, d, fold_halo=(k * n + d) if repeat else 0).cpu().numpy()
+        assert dev.status() == 0 and bits_equal(out, ref)
+        if repeat:
+            out2 = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+            st = dev.status()
+            assert st in (0, 0x4) and (st or bits_equal(out2, ref))
+            if not fused:
+                assert st == 0x4  # the separate fold's 16-record chunks see the long run
+    finally:
+        L.lib().fltee_debug_set_fold_compact(1)
+
+
 @pytest.mark.parametrize("n,d,k", [(10, 4000, 1000), (10, 8000, 1000), (10, 16000, 1000),
                                    (20, 20000, 2000)])
 @pytest.mark.parametrize("fused", [True, False])
