@@ -85,7 +85,11 @@ hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint
                               hipStream_t s);
 
 // k_bitonic.hip
-hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s);
+// valid: positions >= valid hold identical pad records (0: unknown); the stage blocks
+// made of pads alone are skipped (exact, data-independent)
+hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s,
+                        size_t valid = 0);
+void set_pad_skip(int on);
 // stages up to log2(seg) only: aligned segments of seg records sorted, alternating
 // ascending (even segments) / descending (odd segments)
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,

@@ -166,7 +166,7 @@ hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_
     if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
     uint64_t *keys = (uint64_t *)c->ws_keys.ptr;
     hipError_t e = launch_composite_init(sel, lc, d, mc, keys, status, s);
-    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s);
+    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, lc);  // ~0 keys past lc
     if (e == hipSuccess)
         e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
     return e;
@@ -213,7 +213,9 @@ static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, 
     if (ntl == 0 || d == 0) return hipErrorNotSupported;
     if (!c->ws_cnt.reserve((2 * ntl + 2) * 4) || !c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + ntl + 1;
-    hipError_t e = bitonic_sort_nips19_select(A, M, key, rec, nrec, r, d, tf, cnt, s);
+    // tiles of pads alone are skipped by the last pass and keep a zero count
+    hipError_t e = hipMemsetAsync(cnt, 0, ntl * 4, s);
+    if (e == hipSuccess) e = bitonic_sort_nips19_select(A, M, key, rec, nrec, r, d, tf, cnt, s);
     if (e != hipSuccess) return e;
     e = launch_select_scan(cnt, ntl, base, s);
     size_t lc = 0;
@@ -239,7 +241,7 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     hipError_t e = bitonic_sort_advanced(A, M, rec, n * k, d, s);  // init fused into the sort
     if (e == hipErrorNotSupported) {
         e = launch_advanced_init(rec, n * k, d, M, A, s);
-        if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s);
+        if (e == hipSuccess) e = bitonic_sort(A, M, 0, 0, s, L);
     }
     if (e != hipSuccess) return e;
     // Second sort (advanced.rs:106-111): with fold_len == L its [0, d) prefix is the
@@ -254,7 +256,7 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     if (e != hipSuccess) return e;
     if (fold_len == L && g_advanced_compaction)
         return launch_compact_extract(B, A, L, d, coef, out, acc, s);
-    e = bitonic_sort(B, M, 0, 0, s);
+    e = bitonic_sort(B, M, 0, 0, s, L);  // the fold copies the pads past fold_len
     if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
     return e;
 }
@@ -329,7 +331,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             const size_t M = next_pow2_sz(n * k);
             uint64_t *K = (uint64_t *)c->ws_a.ptr;
             e = launch_composite_init(rec, n * k, d, M, K, status, s);
-            if (e == hipSuccess) e = bitonic_sort(K, M, 1, 0, s);
+            if (e == hipSuccess) e = bitonic_sort(K, M, 1, 0, s, n * k);
             if (e == hipSuccess)
                 e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
         } else {
@@ -383,7 +385,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             e = bitonic_sort_nips19(A, M, key, rec, n * k, r, d, tf, s);
             if (e == hipErrorNotSupported) {
                 e = launch_nips19_build(rec, n * k, r, d, tf, M, A, s);
-                if (e == hipSuccess) e = bitonic_sort(A, M, 2, key, s);
+                if (e == hipSuccess) e = bitonic_sort(A, M, 2, key, s, L);
             }
             if (e == hipSuccess) e = safe_aggregate_ordered(c, A, M, d, coef, out, acc, status, s);
         }
@@ -656,6 +658,8 @@ extern "C" void fltee_debug_set_advanced_compaction(int on) { fltee::g_advanced_
 extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_variant(v); }
 // A/B hook: 0 runs advanced's fold as its own pass before the compaction
 extern "C" void fltee_debug_set_fold_compact(int on) { fltee::set_fold_compact(on); }
+// A/B hook: 0 runs the networks over the pad-only stage blocks too
+extern "C" void fltee_debug_set_pad_skip(int on) { fltee::set_pad_skip(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes
 extern "C" void fltee_debug_set_nips19_fused_select(int on) { fltee::g_nips19_fused_select = on != 0; }

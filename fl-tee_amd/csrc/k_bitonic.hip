@@ -520,12 +520,17 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
     for (int q = 0; q < (1 << R); ++q) bt_store(rs, voff, (uint32_t)q << (dlog + 3), v[q]);
 }
 
+// live_groups (0 = all): only the first live_groups groups run — the rest lie in stage
+// blocks made of pad records alone, which the step leaves as they are (see stage_steps)
 template <int MODE>
 static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jtop,
-                                int R, uint32_t seed, hipStream_t s, uint32_t pbase) {
-    const uint32_t ngroups = 1u << (mlog - R);
+                                int R, uint32_t seed, hipStream_t s, uint32_t pbase,
+                                uint32_t live_groups = 0) {
+    uint32_t ngroups = 1u << (mlog - R);
+    if (live_groups && live_groups < ngroups) ngroups = live_groups;
+    if (ngroups == 0) return hipSuccess;
     const unsigned blocks = (ngroups + 255) / 256;
-    net_account((uint64_t)16 << mlog);
+    net_account((uint64_t)16 * ngroups << R);
     switch (R) {
     case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
     case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
@@ -747,6 +752,7 @@ template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
                                const SelSink &sink = SelSink{}) {
+    if (c.tiles == 0) return hipSuccess;  // every tile in pad-only stage blocks
     if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
         if (c.NT == 1024 && sort32()) return launch_sort_direct<MODE, 32, 512>(as_e32(c), s, data, seed, pbase);
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
@@ -819,14 +825,41 @@ static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
     return c;
 }
 
+// Pad-only stage blocks.  Positions >= `valid` hold identical pad records (u32::MAX,
+// +0.0) — or ~0 composite keys — and a stage-ilog step only pairs positions inside one
+// aligned 2^ilog block, so every such block lying at or past roundup(valid, 2^ilog)
+// holds pads alone before and after the whole stage: swapping equal records changes
+// nothing.  Tiles and groups are numbered in position order (strided tiles by their
+// 2^(dtile+R) superblock first), so the live ones are a prefix: T-record tiles <
+// skip_from / T, 2^R-record groups < skip_from / 2^R.  The bound depends only on the
+// public sizes (n, k, d, T): the network stays oblivious, and bit-identical.
+static uint32_t skip_from(uint32_t valid, uint32_t ilog, uint32_t mlog) {
+    if (valid == 0 || ilog >= mlog) return 0;
+    const uint64_t b = ((uint64_t)valid + ((uint64_t)1 << ilog) - 1) >> ilog << ilog;
+    return b >= ((uint64_t)1 << mlog) ? 0u : (uint32_t)b;
+}
+static TileCfg live_tiles(const TileCfg &c, uint32_t skip) {
+    if (!skip) return c;
+    TileCfg l = c;
+    const uint32_t live = skip >> c.tlog;
+    if (live < l.tiles) l.tiles = live;
+    if (l.grid > l.tiles) l.grid = l.tiles;
+    return l;
+}
+static bool g_pad_skip = true;  // fltee_debug_set_pad_skip (A/B)
+void set_pad_skip(int on) { g_pad_skip = on != 0; }
+
 // Steps jtop..0 of stage ilog (ilog > c.tlog) over the m = 2^mlog records at global
 // positions pbase..pbase+m-1: the steps with j >= T in register passes (up to 6 steps)
 // or strided LDS passes (more than 6), then one merge tile pass for the steps j < T.
+// valid: positions >= valid hold identical pads (0: unknown, nothing skipped).
 template <int MODE>
-static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, uint32_t ilog,
+static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t ilog,
                               int jtop, uint32_t seed, uint32_t pbase, hipStream_t s,
-                              const SelSink &sink = SelSink{}) {
+                              const SelSink &sink = SelSink{}, uint32_t valid = 0) {
     const int kMaxGlobalR = max_global_r();
+    const uint32_t skip = g_pad_skip ? skip_from(valid, ilog, mlog) : 0u;
+    const TileCfg c = live_tiles(c0, skip);
     const uint32_t tlog = c.tlog, T = 1u << tlog;
     const int rs = (int)tlog - min_w_log();  // global steps per strided LDS pass (W >= 2^min_w_log)
     const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
@@ -841,7 +874,8 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, u
                 const uint32_t dtile = (uint32_t)(jtop - R + 1);
                 e = launch_tiles<MODE, false>(c, s, data, ilog, tlog - (uint32_t)R, dtile, seed, pbase);
             } else {
-                e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s, pbase);
+                e = launch_global<MODE>(data, mlog, ilog, (uint32_t)jtop, R, seed, s, pbase,
+                                        skip >> R);
             }
             if (e != hipSuccess) return e;
             jtop -= R;
@@ -857,21 +891,24 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c, u
 // ascending where bit slog of its first position is 0 and descending where it is 1.
 template <int MODE>
 static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t s,
-                            uint32_t slog, uint32_t pbase) {
+                            uint32_t slog, uint32_t pbase, uint32_t valid = 0) {
     const uint32_t mlog = log2_pow2(m);
     const TileCfg c = make_cfg(mlog, slog);
+    if (!g_pad_skip) valid = 0;
     hipError_t e;
     if (c.tlog <= 6) {  // tiles of <= 64 records: every stage is one register pass
         for (uint32_t ilog = 1; ilog <= slog; ++ilog) {
-            e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s, pbase);
+            e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s, pbase,
+                                    skip_from(valid, ilog, mlog) >> ilog);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    e = launch_tiles<MODE, true>(c, s, data, 0u, c.tlog, c.tlog, seed, pbase);
+    e = launch_tiles<MODE, true>(live_tiles(c, skip_from(valid, c.tlog, mlog)), s, data, 0u, c.tlog,
+                                 c.tlog, seed, pbase);
     if (e != hipSuccess) return e;
     for (uint32_t ilog = c.tlog + 1; ilog <= slog; ++ilog) {
-        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, pbase, s);
+        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, pbase, s, SelSink{}, valid);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -920,14 +957,16 @@ __global__ __launch_bounds__(256) void bitonic_exchange_kernel(uint4 *__restrict
     }
 }
 
-hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s) {
+hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s,
+                        size_t valid) {
     if (m < 2) return hipSuccess;
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;  // 32-bit byte offsets (4 GiB)
     const uint32_t mlog = log2_pow2(m);
+    const uint32_t v = valid >= m ? 0u : (uint32_t)valid;
     switch (mode) {
-    case 0: return sort_impl<0>(data, m, seed, s, mlog, 0u);
-    case 1: return sort_impl<1>(data, m, seed, s, mlog, 0u);
-    default: return sort_impl<2>(data, m, seed, s, mlog, 0u);
+    case 0: return sort_impl<0>(data, m, seed, s, mlog, 0u, v);
+    case 1: return sort_impl<1>(data, m, seed, s, mlog, 0u, v);
+    default: return sort_impl<2>(data, m, seed, s, mlog, 0u, v);
     }
 }
 
@@ -960,14 +999,25 @@ static bool last_pass_is_direct_merge(size_t m) {
            (c.NT == 1024 || c.E == 32 || (c.NT == 512 && c.E == 16));
 }
 
+__global__ void fill_pads_kernel(uint64_t *__restrict__ p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        p[i] = 0xFFFFFFFFull;  // (u32::MAX, +0.0)
+}
+
 template <int MODE, int GEN>
 static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const SortGen &g,
                                 hipStream_t s, const SelSink &sink = SelSink{}) {
     if (!g_fused_init || m < 2 || m > ((size_t)1 << 29)) return hipErrorNotSupported;
     const uint32_t mlog = log2_pow2(m);
-    const TileCfg c = make_cfg(mlog, mlog);
-    if (c.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
+    const TileCfg c0 = make_cfg(mlog, mlog);
+    if (c0.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
     if (sink.cnt && !last_pass_is_direct_merge(m)) return hipErrorNotSupported;
+    // the padded array's records (advanced: records ++ initial entries; nips19: records ++
+    // dummies); past them only (u32::MAX, +0.0) pads
+    const uint64_t nvalid = (uint64_t)g.nrec + (GEN == 1 ? (uint64_t)g.d : (uint64_t)g.d * g.tf);
+    const uint32_t valid = (g_pad_skip && nvalid < m) ? (uint32_t)nvalid : 0u;
+    // the first pass skips the tiles of pads alone and a store-only pass writes them
+    const TileCfg c = live_tiles(c0, skip_from(valid, c0.tlog, mlog));
     hipError_t e;
     if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, g);
     else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
@@ -976,9 +1026,17 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, g);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
-    for (uint32_t ilog = c.tlog + 1; ilog <= mlog; ++ilog) {
-        e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, 0u, s,
-                              ilog == mlog ? sink : SelSink{});
+    const size_t done = (size_t)c.tiles << c.tlog;
+    if (done < m) {
+        size_t blocks = (m - done + 255) / 256;
+        if (blocks > 16384) blocks = 16384;
+        net_account((uint64_t)8 * (m - done));
+        hipLaunchKernelGGL(fill_pads_kernel, dim3((unsigned)blocks), dim3(256), 0, s, data + done, m - done);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    for (uint32_t ilog = c0.tlog + 1; ilog <= mlog; ++ilog) {
+        e = stage_steps<MODE>(data, mlog, c0, ilog, (int)ilog - 1, seed, 0u, s,
+                              ilog == mlog ? sink : SelSink{}, valid);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

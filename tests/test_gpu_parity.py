@@ -473,6 +473,36 @@ def test_nips19_c4_full_size_bit_exact(dev, oracle):
     assert np.allclose(outdp, oracle.dp_noise(ref, 1.12, 1.0, n, seed), rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("alg,n,d,k", [(1, 100, 50890, 5089), (1, 7, 70000, 3000), (1, 3, 1000, 100),
+                                       (2, 12, 3000, 300), (2, 10, 16000, 1000), (4, 40, 1 << 22, 3000),
+                                       (1, 1000, 10_000_000, 100_000)])
+def test_pad_skip_bit_identical(dev, oracle, alg, n, d, k):
+    """The networks skip the stage blocks made of pads alone (k_bitonic.hip stage_steps):
+    the same bits as running them, at pad fractions from ~0 to ~50 % (advanced C3/C5
+    shapes, nips19, non_oblivious's composite sort)."""
+    from fltee import _lib as L
+    rng = np.random.default_rng(n * 7 + d)
+    if n * k > 10_000_000:
+        idx = ((rng.integers(0, d, n)[:, None] + np.arange(k)[None, :]) % d).reshape(-1).astype(np.uint32)
+        val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    else:
+        idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    outs = []
+    for on in (1, 0):
+        L.lib().fltee_debug_set_pad_skip(on)
+        try:
+            outs.append(dev.aggregate(alg, rec, n, k, d, seed=77).cpu().numpy())
+        finally:
+            L.lib().fltee_debug_set_pad_skip(1)
+        assert dev.status() == 0
+    assert bits_equal(outs[0], outs[1])
+    if n * k <= 2_000_000 and alg != 2:
+        ref, st = (oracle.advanced(k, oracle.as_weights(idx, val), d, n) if alg == 1
+                   else oracle.non_oblivious(oracle.as_weights(idx, val), d, n))
+        assert st == 0 and bits_equal(outs[0], ref)
+
+
 @pytest.mark.parametrize("n,d,k,repeat", [(100, 50890, 5089, False), (1000, 200000, 2000, False),
                                           (3, 1000, 1000, False), (30, 3000, 400, True),
                                           (3000, 30000, 16, False), (5000, 20000, 20, False)])
