@@ -252,10 +252,17 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         e = launch_fold_compact_extract(A, B, M, L, d, halo ? halo : n, coef, out, acc, status, s);
         if (e != hipErrorNotSupported) return e;
     }
+    if (fold_len == L && g_advanced_compaction) {
+        // the compaction reads [0, L) only: fold up to the first pad (position L is
+        // read as the run-end test of L - 1), not the pads after it
+        size_t mf = (L + 1 + 15) / 16 * 16;
+        if (mf > M) mf = M;
+        e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s);
+        if (e != hipSuccess) return e;
+        return launch_compact_extract(B, A, L, d, coef, out, acc, s);
+    }
     e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
     if (e != hipSuccess) return e;
-    if (fold_len == L && g_advanced_compaction)
-        return launch_compact_extract(B, A, L, d, coef, out, acc, s);
     e = bitonic_sort(B, M, 0, 0, s, L);  // the fold copies the pads past fold_len
     if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
     return e;
