@@ -263,8 +263,10 @@ def bench_c4_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
     shuffle is a bitonic network"; strong scaling): every rank draws the same Laplace
     counts (counter-based Philox, no exchange), builds its range of the padded array,
     the keyed shuffle runs as a distributed network with pairwise RCCL range
-    exchanges, each rank runs safe_aggregate on its range and one RCCL reduce adds the
-    partial sums on rank 0, x 1f32/n, + DP noise (fltee/parallel.py)."""
+    exchanges, each rank selects its entries with idx < d (safe_aggregate's filter, in
+    position order), the ragged lists gather on rank 0 in rank order (an all_gather of
+    the counts + one gather) and rank 0 adds each index's entries in that order, x
+    1f32/n, + DP noise (fltee/parallel.py): bit-identical to one GPU's nips19."""
     from fltee import parallel as P
     w = WORKLOADS["c4"]
     n, d, k, seed = w["n"], w["d"], w["k"], 7
@@ -307,7 +309,7 @@ def bench_c4_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
     del rec, chunk, ops
     wall = float(t[0]) / steps
     return dict(desc=w["desc"] + f", position-range sharded x{world}: distributed keyed shuffle "
-                "(RCCL pairwise range exchanges) + per-range safe_aggregate + one RCCL reduce",
+                "(RCCL pairwise range exchanges) + per-range selection + one RCCL gather + in-order sums",
                 alg="nips19", n=n, d=d, k=k, M=M, range_records=C, ms_per_step=wall * 1e3,
                 value=n * k / wall, unit="client-params/s", scaling="strong")
 

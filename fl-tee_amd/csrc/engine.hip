@@ -626,6 +626,43 @@ extern "C" fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t 
                : FLTEE_ERROR_UNEXPECTED;
 }
 
+// safe_aggregate split for position ranges (nips19 over several GPUs): each range's
+// entries with idx < d in position order, then the ordered fold of their concatenation
+// in range order on the root — the one-GPU result bit for bit.
+extern "C" fltee_status_t fltee_select_device(const void *d_src, size_t m, size_t d, void *d_list,
+                                              size_t cap, size_t *count, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c || !count || m >= ((size_t)1 << 31)) return FLTEE_ERROR_INVALID_PARAMETER;
+    hipStream_t s = (hipStream_t)stream;
+    *count = 0;
+    if (m == 0 || d == 0) return FLTEE_SUCCESS;
+    const size_t nb = select_tiles(m);
+    if (!c->ws_cnt.reserve((2 * nb + 2) * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
+    uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
+    size_t lc = 0;
+    if (launch_select_count((const uint64_t *)d_src, m, d, cnt, base, s) != hipSuccess ||
+        read_device_word(c, base + nb, &lc, s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    *count = lc;
+    if (lc > cap || (lc && !d_list)) return FLTEE_ERROR_INVALID_PARAMETER;  // caller grows the list
+    if (lc && launch_select_write((const uint64_t *)d_src, m, d, base, (uint64_t *)d_list, s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    return FLTEE_SUCCESS;
+}
+
+extern "C" fltee_status_t fltee_ordered_list_device(const void *d_list, size_t lc, size_t d,
+                                                    float coef, float *d_out, void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c || lc >= ((size_t)1 << 29)) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (d == 0) return FLTEE_SUCCESS;
+    return ordered_from_list(c, (const uint64_t *)d_list, lc, d, coef, d_out, false, c->status,
+                             (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
 
 // measurement hook: streaming passes launched and the bytes they sweep since the last reset

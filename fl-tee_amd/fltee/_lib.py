@@ -85,6 +85,8 @@ SIGNATURES = {
     "fltee_compact_range_device": (_U32, [_P, _S, _S, _P, _P, _F, _P, _P]),
     "fltee_nips19_build_range_device": (_U32, [_P, _S, _P, _S, _S, _S, _S, _P, _P]),
     "fltee_safe_aggregate_device": (_U32, [_P, _S, _S, _P, _P]),
+    "fltee_select_device": (_U32, [_P, _S, _S, _P, _S, _P, _P]),
+    "fltee_ordered_list_device": (_U32, [_P, _S, _S, _F, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_version": (ctypes.c_char_p, []),
     "fltee_device_init_multi": (_U32, [_P, ctypes.c_int, _P]),

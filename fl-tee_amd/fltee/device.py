@@ -218,3 +218,25 @@ def safe_aggregate(entries, d, out=None, stream=None):
                                                _stream(stream)),
            "fltee_safe_aggregate_device")
     return out
+
+
+def select(entries, d, stream=None):
+    """The entries of one range with idx < d, in position order (fltee_select_device):
+    the piece of nips19's safe_aggregate a range contributes, as an int64 tensor."""
+    count = ctypes.c_size_t(0)
+    lst = torch.empty(max(1, entries.numel()), dtype=torch.int64, device=entries.device)
+    _check(L.lib().fltee_select_device(_ptr(entries), entries.numel(), d, _ptr(lst), lst.numel(),
+                                       ctypes.byref(count), _stream(stream)),
+           "fltee_select_device")
+    return lst[: count.value]
+
+
+def ordered_list(lst, d, coef, out=None, stream=None):
+    """out[i] = coef * (+0 + v1 + v2 ...) over the list's entries with idx i, in list
+    order (fltee_ordered_list_device)."""
+    if out is None:
+        out = torch.empty(d, dtype=torch.float32, device=lst.device)
+    _check(L.lib().fltee_ordered_list_device(_ptr(lst), lst.numel(), d, coef, _ptr(out),
+                                             _stream(stream)),
+           "fltee_ordered_list_device")
+    return out

@@ -153,6 +153,12 @@ class DeviceRangeOps:
     def safe_aggregate(self, x, d):
         return self.D.safe_aggregate(x, d)
 
+    def select(self, x, d):
+        return self.D.select(x, d)
+
+    def ordered(self, lst, d, coef):
+        return self.D.ordered_list(lst, d, coef)
+
     def steps(self, x, pos, stage_log, step_top, step_bot):
         self.D.bitonic_range_steps(x, pos, stage_log, step_top, step_bot)
 
@@ -209,6 +215,10 @@ class VirtualRanks:
         for r in range(1, self.world):
             out += outs[r]
         return out
+
+    def gather_lists(self, lists, root):
+        """The ranges' lists concatenated in range order (on the root)."""
+        return torch.cat([lists[r] for r in range(self.world)])
 
 
 class DistRanks:
@@ -271,6 +281,26 @@ class DistRanks:
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
+    def gather_lists(self, lists, root):
+        """Variable-length lists to the root, concatenated in rank order: the counts go
+        first (all_gather), the lists padded to the longest (one gather)."""
+        x = lists[self.rank]
+        staged = dist.get_backend() == "gloo" and x.is_cuda
+        dev = "cpu" if (staged or not x.is_cuda) else x.device
+        n = torch.tensor([x.numel()], dtype=torch.int64, device=dev)
+        counts = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(counts, n)
+        counts = [int(c.item()) for c in counts]
+        width = max(1, max(counts))
+        buf = torch.full((width,), -1, dtype=torch.int64, device=dev)
+        buf[: x.numel()] = x.to(dev)
+        parts = [torch.empty_like(buf) for _ in range(self.world)] if self.rank == root else None
+        dist.gather(buf, parts, dst=root)
+        if self.rank != root:
+            return None
+        out = torch.cat([parts[r][: counts[r]] for r in range(self.world)])
+        return out.to(x.device)
+
     def reduce(self, outs, root):
         out = outs[self.rank]
         if dist.get_backend() == "gloo" and out.is_cuda:
@@ -328,19 +358,20 @@ def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None
     array (records ++ Laplace dummies ++ pads, fltee_nips19_build_range with the same
     Laplace counts on every rank: counter-based, no exchange); the keyed shuffle runs
     as a distributed network (pairwise exchanges, mode 2), every rank runs
-    safe_aggregate on its range and one reduce adds the partial sums on the root,
-    x 1f32/n, then DP noise.  The shuffle permutation is bit-identical to one GPU's;
-    the per-index sums are float atomics, as on one GPU (fp32 tolerance)."""
+    safe_aggregate's selection on its range (its entries with idx < d, in position
+    order), the lists are gathered to the root in rank order — the shuffled order — and
+    the root adds each index's entries in that order (fltee_ordered_list_device), x
+    1f32/n, then DP noise.  Bit-identical to one GPU's nips19."""
     assert world & (world - 1) == 0 and M % world == 0
     ops = ops if ops is not None else DeviceRangeOps()
     comm = comm if comm is not None else VirtualRanks(world)
     key = (seed ^ (seed >> 32)) & 0xFFFFFFFF  # the shuffle key of fltee_aggregate_device
     chunks = distributed_network(chunks, world, M, ops, comm, mode=2, seed=key, exchange="pairwise")
-    outs = {r: ops.safe_aggregate(x, d) for r, x in chunks.items()}
-    out = comm.reduce(outs, root)
-    if out is None:
+    lists = {r: ops.select(x, d) for r, x in chunks.items()}
+    full = comm.gather_lists(lists, root)
+    if full is None:
         return None
-    out = ops.finish(out, float(np.float32(1.0) / np.float32(n_total)))
+    out = ops.ordered(full, d, float(np.float32(1.0) / np.float32(n_total)))
     if dp is not None:
         ops.dp(out, dp["sigma"], dp["clipping"], n_total, dp.get("seed", 0))
     return out

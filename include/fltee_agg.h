@@ -298,6 +298,15 @@ fltee_status_t fltee_nips19_build_range_device(const void *d_records, size_t nre
                                                void *stream);
 fltee_status_t fltee_safe_aggregate_device(const void *d_src, size_t m, size_t d, float *d_out,
                                            void *stream);
+/* safe_aggregate split over ranges, bit-exact: the entries of one range with idx < d in
+ * position order into d_list (at most cap; *count = how many there are, also when they
+ * do not fit: INVALID_PARAMETER), synchronising `stream`; then, on the root, the ordered
+ * fold of the ranges' lists concatenated in range order (the shuffled order):
+ * d_out[i] = coef * (+0 + v1 + v2 ...) over the entries with idx i. */
+fltee_status_t fltee_select_device(const void *d_src, size_t m, size_t d, void *d_list,
+                                   size_t cap, size_t *count, void *stream);
+fltee_status_t fltee_ordered_list_device(const void *d_list, size_t lc, size_t d, float coef,
+                                         float *d_out, void *stream);
 
 /* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
 void fltee_debug_set_seed(uint64_t seed);

@@ -90,6 +90,19 @@ class NumpyRangeOps:
         np.add.at(out, idx[sel], val[sel])
         return torch.from_numpy(out)
 
+    def select(self, x, d):
+        a = _u(x)
+        return torch.from_numpy(a[(a & MASK) < d].view(np.int64).copy())
+
+    def ordered(self, lst, d, coef):
+        """common.rs:25-35 + 14-19 on the concatenated list: in-order f32 sums, x coef."""
+        a = _u(lst)
+        idx = (a & MASK).astype(np.int64)
+        val = (a >> np.uint64(32)).astype(np.uint32).view(np.float32)
+        out = np.zeros(d, np.float32)
+        np.add.at(out, idx, val)
+        return torch.from_numpy(out * np.float32(coef))
+
     def steps(self, x, pos, stage_log, step_top, step_bot):
         a = _u(x)
         for jlog in range(step_top, step_bot - 1, -1):

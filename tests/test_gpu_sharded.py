@@ -62,7 +62,8 @@ def test_distributed_network_equals_single_sort(dev, oracle, world, m, mode):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_index_sharded_nips19_matches_single_gpu(dev, world):
     """nips19 by position range == fltee_aggregate_device(nips19) with the same seed:
-    same Laplace counts, same shuffle; the sums are float atomics on both (tolerance)."""
+    same Laplace counts, same shuffle, each index's entries added in shuffled order on
+    both: bit-identical."""
     import torch
 
     from fltee.parallel import VirtualRanks, index_sharded_nips19
@@ -79,8 +80,7 @@ def test_index_sharded_nips19_matches_single_gpu(dev, world):
     chunks = {q: dev.nips19_build_range(rec[q * C:] if q * C < nrec else rec, nrec, r, d, tf,
                                         q * C, C) for q in range(world)}
     out = index_sharded_nips19(chunks, world, M, n, d, seed, comm=VirtualRanks(world)).cpu().numpy()
-    tol = 1e-6 * np.abs(val).max() * (n + 1)
-    assert np.abs(out - single).max() <= tol
+    assert np.array_equal(out.view(np.uint32), single.view(np.uint32))
 
 
 @pytest.mark.parametrize("exchange", ["transpose", "pairwise"])
@@ -120,3 +120,28 @@ def test_index_sharded_matches_single_gpu_at_scale(dev):
     out = index_sharded_advanced(init_chunks(dev, rec, n * k, d, 4, M), 4, M, n, k, d,
                                  comm=VirtualRanks(4)).cpu().numpy()
     assert np.array_equal(out.view(np.uint32), single.view(np.uint32))
+
+
+@pytest.mark.parametrize("m,d,hi", [(1, 10, 20), (777, 50, 80), (40000, 3000, 3100), (5000, 100, 100),
+                                    (5000, 100, 90000)])
+def test_select_and_ordered_list_match_numpy(dev, m, d, hi):
+    """fltee_select_device (entries with idx < d, position order) and
+    fltee_ordered_list_device (in-order f32 sums x coef) == numpy, bit for bit; hi = d:
+    nothing selected; the per-range lists concatenated reproduce one range's sums."""
+    import torch
+
+    from range_ops_np import NumpyRangeOps
+    rng = np.random.default_rng(m + d)
+    idx = rng.integers(0, hi, m).astype(np.uint32)
+    val = rng.normal(0, 1, m).astype(np.float32)
+    x = torch.from_numpy(dev.pack_records(idx, val).view(np.int64)).cuda()
+    lst = dev.select(x, d)
+    ref = NumpyRangeOps().select(x.cpu(), d)
+    assert np.array_equal(lst.cpu().numpy(), ref.numpy())
+    coef = float(np.float32(1.0) / np.float32(7))
+    out = dev.ordered_list(lst, d, coef).cpu().numpy()
+    want = NumpyRangeOps().ordered(ref, d, coef).numpy()
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32))
+    parts = [dev.select(x[a:b], d) for a, b in ((0, m // 3), (m // 3, m // 2), (m // 2, m))]
+    out2 = dev.ordered_list(torch.cat(parts), d, coef).cpu().numpy()
+    assert np.array_equal(out2.view(np.uint32), out.view(np.uint32))

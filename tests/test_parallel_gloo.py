@@ -148,3 +148,53 @@ def test_index_sharded_advanced_gloo(oracle, tmp_path, world, exchange):
     assert st == 0
     got = np.load(tmp_path / "adv_b.npy")
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+# ---- position-range sharded nips19: DistRanks.gather_lists over gloo ----
+NIPS_SEED = 0x1234_0000_00C0_FFEE
+
+
+def case_c():
+    rng = np.random.default_rng(11)
+    m, d, n = 1024, 50, 7
+    idx = rng.integers(0, 80, m).astype(np.uint32)  # idx >= d: pads/dummies, dropped
+    val = rng.normal(0, 0.01, m).astype(np.float32)
+    return m, d, n, idx, val
+
+
+def worker_c(rank, world, port, outdir):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "fl-tee_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from range_ops_np import NumpyRangeOps
+
+    from fltee import parallel as P
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    m, d, n, idx, val = case_c()
+    full = torch.from_numpy(O.as_weights(idx, val).view(np.int64).copy())
+    C = m // world
+    chunks = {rank: full[rank * C:(rank + 1) * C].clone()}
+    out = P.index_sharded_nips19(chunks, world, m, n, d, NIPS_SEED, ops=NumpyRangeOps(),
+                                 comm=P.DistRanks(rank, world))
+    if rank == 0:
+        np.save(os.path.join(outdir, "nips.npy"), out.numpy())
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_index_sharded_nips19_gloo(oracle, tmp_path, world):
+    """Ragged per-rank selections gathered in rank order == the single-array keyed
+    shuffle + in-order safe_aggregate (nips19.rs:51-61, common.rs:25-35), bit for bit."""
+    mp.spawn(worker_c, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    m, d, n, idx, val = case_c()
+    key = (NIPS_SEED ^ (NIPS_SEED >> 32)) & 0xFFFFFFFF
+    s = oracle.shuffle_keyed(oracle.as_weights(idx, val), key)
+    ref = oracle.safe_aggregate(s, d, n)
+    got = np.load(tmp_path / "nips.npy")
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
