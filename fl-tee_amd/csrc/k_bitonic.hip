@@ -857,7 +857,11 @@ template <int MODE>
 static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t ilog,
                               int jtop, uint32_t seed, uint32_t pbase, hipStream_t s,
                               const SelSink &sink = SelSink{}, uint32_t valid = 0) {
-    const int kMaxGlobalR = max_global_r();
+    // a register pass of R steps runs M / 2^R lanes: keep >= 2^16 of them (256 lanes per
+    // CU) down to R = 4 — at M = 2^20 (C3) R = 6 left 64 blocks of 256 for the whole chip (10.1 us for
+    // that pass; the cap, as FLTEE_BITONIC_MAXR=4 there: 0.1894 vs 0.1916 ms per aggregate)
+    const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
+    const int kMaxGlobalR = max_global_r() < rcap ? max_global_r() : rcap;
     const uint32_t skip = g_pad_skip ? skip_from(valid, ilog, mlog) : 0u;
     const TileCfg c = live_tiles(c0, skip);
     const uint32_t tlog = c.tlog, T = 1u << tlog;

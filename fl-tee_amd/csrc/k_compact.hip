@@ -274,7 +274,7 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 // kernel, and the caller reruns with a wider halo.  The folded array (1 GB at C5) is
 // never written and read back.  Dummies and non-representatives are never selected by
 // the compaction, so their contents do not matter.
-template <int NT, int PER, int FINAL>
+template <int NT, int PER, int FINAL, int XMAX>
 __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
                                                             uint32_t M, uint32_t d, uint32_t G,
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
                                                             float *__restrict__ out,
                                                             uint32_t *status) {
     constexpr uint32_t CAP = (uint32_t)NT * PER;
-    constexpr uint32_t XMAX = 4096 / NT + 1;  // window slots beyond CAP per lane (Hr <= 4096)
+    // XMAX: window slots beyond CAP per lane, ceil((Hr + 1) / NT)
     extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1
     const uint32_t H = (1u << G) - 1;
     const uint32_t t = threadIdx.x;
@@ -320,20 +320,44 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
-        // run heads walk their runs (left to right) and store the sum at the run's end
-        for (uint32_t x = t * chunk; x < (t + 1) * chunk && x < Wn; ++x) {
-            const long long p = wlo + x;
-            if (p < 0 || p >= (long long)L) continue;
-            const uint32_t k = (uint32_t)win[x];
-            if (!(x == 0 || p == 0 || (uint32_t)win[x - 1] != k)) continue;
-            float acc = rec_val(win[x]);
-            uint32_t y = x;
-            while (y + 1 < Wn && wlo + (long long)(y + 1) < (long long)L && (uint32_t)win[y + 1] == k) {
-                ++y;
-                acc = __fadd_rn(acc, rec_val(win[y]));
+        // Each lane owns window slots [x0, x1) and folds the runs whose heads lie there,
+        // left to right: one loop that goes past x1 only to finish its last run, so a
+        // wave's trip count is about chunk + the longest run (a loop per head nested in
+        // a loop over the slots cost chunk x the longest run).  The sum lands in the
+        // val of the run's last slot; idx words are never rewritten, so the head tests
+        // of the neighbouring lanes read the same keys whatever the order of the writes.
+        {
+            const uint32_t x0 = t * chunk, x1 = min(x0 + chunk, Wn);
+            const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
+            uint32_t prevk = x0 > 0 ? (uint32_t)win[x0 - 1] : 0u;
+            bool run = false;
+            float acc = 0.0f;
+            uint32_t k = 0;
+            for (uint32_t y = x0; y < Wn; ++y) {
+                const int p = pw + (int)y;
+                const bool valid = p >= 0 && p < (int)L;
+                const uint64_t r = win[y];
+                const uint32_t ky = (uint32_t)r;
+                const bool head = y == 0 || p == 0 || ky != prevk;
+                prevk = ky;
+                if (run) {
+                    if (valid && !head) {
+                        acc = __fadd_rn(acc, rec_val(r));
+                        continue;
+                    }
+                    win[y - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;  // ended at y - 1
+                    run = false;
+                }
+                if (y >= x1) break;
+                if (valid && head) {
+                    run = true;
+                    acc = rec_val(r);
+                    k = ky;
+                }
             }
-            if (y + 1 < Wn || wlo + (long long)(y + 1) >= (long long)L)  // the run ends inside
-                win[y] = ((uint64_t)__float_as_uint(acc) << 32) | k;
+            // a run still open at the window's end ends there only if position L follows
+            if (run && pw + (long long)Wn >= (long long)L)
+                win[Wn - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;
         }
         __syncthreads();
         // representatives with idx < d -> (c = p - idx, sum); the rest never move
@@ -428,25 +452,30 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);
     const size_t lds = (Hr + CAP + 1) * 8;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, 2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        attr = true;
-    }
     net_account((uint64_t)(last ? 8 : 16) * L);
-#define FC_GO(F)                                                                                  \
-    hipLaunchKernelGGL((fold_compact_first<NT, PER, F>), dim3(grid), dim3(NT), lds, s, A, B,       \
-                       (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr,                 \
-                       (uint32_t)ntiles, coef, out, status)
+    const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr <= 512)
+#define FC_GO1(F, X)                                                                              \
+    do {                                                                                          \
+        static bool attr = false; /* 33 KB at Hr = 112; up to 37 KB */                            \
+        if (!attr) {                                                                              \
+            (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, F, X>,            \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);     \
+            attr = true;                                                                          \
+        }                                                                                         \
+        hipLaunchKernelGGL((fold_compact_first<NT, PER, F, X>), dim3(grid), dim3(NT), lds, s, A,  \
+                           B, (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr,          \
+                           (uint32_t)ntiles, coef, out, status);                                  \
+    } while (0)
+#define FC_GO(F)                     \
+    do {                             \
+        if (x1) FC_GO1(F, 1);        \
+        else FC_GO1(F, 2);           \
+    } while (0)
     if (!last) FC_GO(0);
     else if (accumulate) FC_GO(2);
     else FC_GO(1);
 #undef FC_GO
+#undef FC_GO1
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || last) return e;
     return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);

@@ -1,0 +1,43 @@
+"""A/B of the build-time knobs that are read once per process (FLTEE_BITONIC_* env
+variables): one child process per variant, each timing bench.bench_workload.  The parent
+never touches the GPU.  One JSON line per (workload, variant, repeat).
+
+    python scripts/ab_env.py c3 'FLTEE_BITONIC_MINTILES_LOG=7' 'FLTEE_BITONIC_MINTILES_LOG=9'
+(the empty variant, the defaults, always runs first and last)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import json, sys, torch
+sys.path.insert(0, {root!r}); sys.path.insert(0, {root!r} + "/fl-tee_amd")
+import bench
+from fltee import device as D
+r = bench.bench_workload(torch, D, {w!r}, steps={steps}, warmup=5, device=torch.device("cuda", 0))
+print("RESULT " + json.dumps(dict(kernel_ms=r["kernel_s"] * 1e3, passes=r["net"]["passes"])))
+"""
+
+
+def main():
+    w = sys.argv[1]
+    steps = {"c3": 300, "c1": 300, "mnist100": 300}.get(w, 10)
+    variants = [""] + sys.argv[2:] + [""]
+    for rep in range(2):
+        for v in variants:
+            env = dict(os.environ)
+            for kv in v.split():
+                k, val = kv.split("=", 1)
+                env[k] = val
+            p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, w=w, steps=steps)],
+                               env=env, capture_output=True, text=True, timeout=240)
+            line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
+            res = json.loads(line[-1][7:]) if line else dict(error=p.stderr[-400:])
+            print(json.dumps(dict(workload=w, variant=v or "default", rep=rep, **res)), flush=True)
+            if p.returncode != 0:
+                sys.exit(p.returncode)
+
+
+if __name__ == "__main__":
+    main()
