@@ -389,6 +389,10 @@ struct SortGen {
     const uint64_t *rec;  // the record at global position p is rec[p - pbase] (p < nrec)
     const uint32_t *r;    // GEN 2: Laplace counts r_i
     uint32_t nrec, d, tf;
+    // pad_n > 0: blocks >= grid_live store (u32::MAX, +0.0) to positions pad_begin ..
+    // pad_begin + pad_n - 1 (the tiles of pads alone, which no sort step reads before
+    // a later stage's live region reaches them) instead of sorting
+    uint32_t grid_live = 0, pad_begin = 0, pad_n = 0;
 };
 template <int GEN>
 __device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint64_t v) {
@@ -414,10 +418,24 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     static_assert((1 << R1) == E && RL >= 1 && RL <= R1, "tile shape");
-    uint32_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
     const uint32_t t = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
+    if (g.pad_n && blockIdx.x >= g.grid_live) {  // store-only blocks (replace a fill launch)
+        const uint32_t nb = gridDim.x - g.grid_live;
+        const bt_u32x4 pad = {0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u};
+        for (uint32_t i = (blockIdx.x - g.grid_live) * (uint32_t)NT + t; i < g.pad_n / 2u;
+             i += nb * (uint32_t)NT) {
+            __builtin_amdgcn_raw_buffer_store_b128(pad, rs, (int)(i * 16u), (int)(g.pad_begin * 8u),
+                                                   kTileCP);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 1" ::: "memory");  // dwordx4 store data hazard (see above)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
+    const uint32_t stride = g.pad_n ? g.grid_live : gridDim.x;  // the sorting blocks
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
     // GEN: loads come from rec, range-checked to its nloc records from pbase (beyond:
     // zeros, replaced by gen_entry)
     uint32_t nloc = 0;
@@ -463,7 +481,7 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
         __syncthreads();
-        const uint32_t next = tile + gridDim.x;
+        const uint32_t next = tile + stride;
         load(next < ntiles ? next : tile);
         for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
             lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
@@ -709,6 +727,14 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
     net_account((uint64_t)16 * c.tiles << c.tlog);
+    SortGen gg = g;
+    unsigned grid = c.grid;
+    if (gg.pad_n) {  // + store-only blocks for the pad tiles, about 8 stores per lane
+        gg.grid_live = c.grid;
+        uint32_t nb = (gg.pad_n / 2u + NT * 8u - 1u) / (NT * 8u);
+        grid += nb < 1024u ? nb : 1024u;
+        net_account((uint64_t)8 * gg.pad_n);
+    }
 #define BS_GO(RL_)                                                                                 \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -717,8 +743,8 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN>), dim3(c.grid), dim3(NT),   \
-                           c.lds, s, data, c.tlog, seed, c.tiles, pbase, g);                       \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN>), dim3(grid), dim3(NT),     \
+                           c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);                      \
     } while (0)
     switch (rl) {
     case 1: BS_GO(1); break;
@@ -1003,11 +1029,6 @@ static bool last_pass_is_direct_merge(size_t m) {
            (c.NT == 1024 || c.E == 32 || (c.NT == 512 && c.E == 16));
 }
 
-__global__ void fill_pads_kernel(uint64_t *__restrict__ p, size_t n) {
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-        p[i] = 0xFFFFFFFFull;  // (u32::MAX, +0.0)
-}
-
 template <int MODE, int GEN>
 static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const SortGen &g,
                                 hipStream_t s, const SelSink &sink = SelSink{}) {
@@ -1022,22 +1043,18 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     const uint32_t valid = (g_pad_skip && nvalid < m) ? (uint32_t)nvalid : 0u;
     // the first pass skips the tiles of pads alone and a store-only pass writes them
     const TileCfg c = live_tiles(c0, skip_from(valid, c0.tlog, mlog));
+    const size_t done = (size_t)c.tiles << c.tlog;
+    SortGen gp = g;  // the pad tiles are stored by extra blocks of the same launch
+    gp.pad_begin = (uint32_t)done;
+    gp.pad_n = (uint32_t)(m - done);
     hipError_t e;
-    if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, g);
-    else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, g);
-    else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, g);
-    else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, g);
-    else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, g);
+    if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, gp);
+    else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, gp);
+    else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, gp);
+    else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, gp);
+    else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, gp);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
-    const size_t done = (size_t)c.tiles << c.tlog;
-    if (done < m) {
-        size_t blocks = (m - done + 255) / 256;
-        if (blocks > 16384) blocks = 16384;
-        net_account((uint64_t)8 * (m - done));
-        hipLaunchKernelGGL(fill_pads_kernel, dim3((unsigned)blocks), dim3(256), 0, s, data + done, m - done);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     for (uint32_t ilog = c0.tlog + 1; ilog <= mlog; ++ilog) {
         e = stage_steps<MODE>(data, mlog, c0, ilog, (int)ilog - 1, seed, 0u, s,
                               ilog == mlog ? sink : SelSink{}, valid);

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
     // before position 0 or past M are dummies (clamped address, select after the load:
     // no branch around the loads)
     uint64_t pf[PER + XMAX];
+    uint32_t ck0 = 0, ck1 = 0;  // idx at a - Hr - 1 and at a: the overflow test's keys
     auto prefetch = [&](uint32_t tl) {
         const long long wlo = (long long)tl * S - (long long)Hr;
 #pragma unroll
@@ -305,6 +306,11 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
                 rs, (int)(ok ? (uint32_t)p * 8u : 0u), 0, 0);
             pf[i] = ok ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
         }
+        // every lane loads the same two words (one request per wave), issued with the
+        // window instead of after it
+        const long long pa = (long long)tl * S;
+        ck0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(pa - Hr - 1 >= 0 ? (uint32_t)(pa - Hr - 1) * 8u : 0u), 0, 0);
+        ck1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(pa < (long long)M ? (uint32_t)pa * 8u : 0u), 0, 0);
     };
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -314,8 +320,7 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
 #pragma unroll
         for (uint32_t i = 0; i < PER + XMAX; ++i)
             if (t + i * NT < Wn) win[t + i * NT] = pf[i];
-        if (t == 0 && a < (long long)L && a - (long long)Hr - 1 >= 0 &&
-            (uint32_t)A[a - Hr - 1] == (uint32_t)A[a])
+        if (t == 0 && a < (long long)L && a - (long long)Hr - 1 >= 0 && ck0 == ck1)
             atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
@@ -333,10 +338,12 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
             bool run = false;
             float acc = 0.0f;
             uint32_t k = 0;
+            uint64_t rn = win[x0 < Wn ? x0 : Wn - 1];
             for (uint32_t y = x0; y < Wn; ++y) {
                 const int p = pw + (int)y;
                 const bool valid = p >= 0 && p < (int)L;
-                const uint64_t r = win[y];
+                const uint64_t r = rn;
+                rn = win[y + 1 < Wn ? y + 1 : y];  // read ahead: the LDS latency overlaps this slot
                 const uint32_t ky = (uint32_t)r;
                 const bool head = y == 0 || p == 0 || ky != prevk;
                 prevk = ky;
@@ -436,10 +443,39 @@ void set_fold_compact(int on) { g_fold_compact = on != 0; }
 // The fold (fold_len == L) + the compaction of `advanced`: sorted array A (M records,
 // [0, L) meaningful) -> out.  A and B are clobbered.  hipErrorNotSupported: not fused
 // here (halo wide against the 4096-record tile, or no levels): the caller folds separately.
+template <int PER, int F, int X>
+static hipError_t fc_launch(unsigned grid, size_t lds, hipStream_t s, const uint64_t *A, uint64_t *B,
+                            size_t L, size_t M, size_t d, uint32_t G, uint32_t S, size_t Hr,
+                            uint64_t ntiles, float coef, float *out, uint32_t *status) {
+    constexpr int NT = 512;
+    static bool attr = false;  // 26-37 KB of window
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, F, X>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((fold_compact_first<NT, PER, F, X>), dim3(grid), dim3(NT), lds, s, A, B,
+                       (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles,
+                       coef, out, status);
+    return hipGetLastError();
+}
+
+template <int PER>
+static hipError_t fc_dispatch(int F, bool x1, unsigned grid, size_t lds, hipStream_t s,
+                              const uint64_t *A, uint64_t *B, size_t L, size_t M, size_t d,
+                              uint32_t G, uint32_t S, size_t Hr, uint64_t ntiles, float coef,
+                              float *out, uint32_t *status) {
+#define FC_ARGS grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status
+    if (F == 0) return x1 ? fc_launch<PER, 0, 1>(FC_ARGS) : fc_launch<PER, 0, 2>(FC_ARGS);
+    if (F == 2) return x1 ? fc_launch<PER, 2, 1>(FC_ARGS) : fc_launch<PER, 2, 2>(FC_ARGS);
+    return x1 ? fc_launch<PER, 1, 1>(FC_ARGS) : fc_launch<PER, 1, 2>(FC_ARGS);
+#undef FC_ARGS
+}
+
 hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
                                        size_t halo, float coef, float *out, bool accumulate,
                                        uint32_t *status, hipStream_t s) {
-    constexpr uint32_t NT = 512, PER = 8, CAP = NT * PER;
+    constexpr uint32_t NT = 512;
     const size_t Hr = fold_context(halo);
     // A/B in one process (scripts/ab_fold_compact.py, profiles/r02/ab/fold_compact.jsonl):
     // C3 (Hr = 112): 0.211 vs 0.214 ms with the separate fold; C5 (Hr = 1008, windows 25 %
@@ -447,36 +483,29 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     if (!g_fold_compact || d == 0 || L <= d || Hr > 512 || M >= ((size_t)1 << 29) || L > M)
         return hipErrorNotSupported;
     const uint32_t nlev = bitlen(L - d);
-    const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1, S = CAP - H;
+    const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1;
+    // records per lane: the fewest (4, 6 or 8) that still leave at most one tile per CU —
+    // each lane's walk and levels are the critical path, the window re-read is cheap
+    uint32_t per = 8;
+    for (uint32_t p : {4u, 6u}) {
+        if (NT * p <= 2 * H) continue;  // the halo rows would swamp the tile
+        if ((L + NT * p - H - 1) / (NT * p - H) <= 256) {
+            per = p;
+            break;
+        }
+    }
+    const uint32_t CAP = NT * per, S = CAP - H;
     const uint64_t ntiles = (L + S - 1) / S;
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);
     const size_t lds = (Hr + CAP + 1) * 8;
     net_account((uint64_t)(last ? 8 : 16) * L);
     const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr <= 512)
-#define FC_GO1(F, X)                                                                              \
-    do {                                                                                          \
-        static bool attr = false; /* 33 KB at Hr = 112; up to 37 KB */                            \
-        if (!attr) {                                                                              \
-            (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, F, X>,            \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);     \
-            attr = true;                                                                          \
-        }                                                                                         \
-        hipLaunchKernelGGL((fold_compact_first<NT, PER, F, X>), dim3(grid), dim3(NT), lds, s, A,  \
-                           B, (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr,          \
-                           (uint32_t)ntiles, coef, out, status);                                  \
-    } while (0)
-#define FC_GO(F)                     \
-    do {                             \
-        if (x1) FC_GO1(F, 1);        \
-        else FC_GO1(F, 2);           \
-    } while (0)
-    if (!last) FC_GO(0);
-    else if (accumulate) FC_GO(2);
-    else FC_GO(1);
-#undef FC_GO
-#undef FC_GO1
-    hipError_t e = hipGetLastError();
+    const int F = !last ? 0 : (accumulate ? 2 : 1);
+    hipError_t e;
+    if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
+    else if (per == 6) e = fc_dispatch<6>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
+    else e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
     if (e != hipSuccess || last) return e;
     return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);
 }
