@@ -158,6 +158,42 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
     }
 }
 
+// The same rounds for contiguous tiles of a size known at compile time (the direct
+// merges of 2^13 / 2^14-record tiles): spread() and the slot offsets fold to constants,
+// lpad(b + q*2^DLOG) = lpad(b) + q*2^DLOG + (q*2^DLOG >> 4) (b has zeros at bits
+// [DLOG, DLOG+R) and its part above them is a multiple of 16), so every slot is a
+// ds_read/ds_write immediate offset off one per-group address — five VALU per slot
+// fewer.  Same greedy split into rounds as lds_steps: the same network.
+template <int MODE, int R, int E, int NT, int DLOG>
+__device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
+                                             uint32_t seed) {
+    static_assert(DLOG + R >= 4, "slot offsets split only above 16 records");
+    constexpr int G = E >> R;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+        const uint32_t g = threadIdx.x + (uint32_t)h * NT;
+        const uint32_t b = spread(g, (uint32_t)DLOG, (uint32_t)R);
+        uint64_t *row = sm + lpad(b);
+        uint64_t v[1 << R];
+#pragma unroll
+        for (int q = 0; q < (1 << R); ++q) v[q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
+        group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
+#pragma unroll
+        for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[q];
+    }
+}
+template <int MODE, int E, int NT, int JTOP, int JBOT>
+__device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
+                                             uint32_t seed) {
+    if constexpr (JTOP >= JBOT) {
+        constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+        constexpr int r = JTOP - JBOT + 1 < rmax ? JTOP - JBOT + 1 : rmax;
+        lds_round_ct<MODE, r, E, NT, JTOP - r + 1>(sm, base, ilog, seed);
+        __syncthreads();
+        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT>(sm, base, ilog, seed);
+    }
+}
+
 // Persistent tile kernels: a block walks tiles blockIdx.x, +gridDim.x, ...; the
 // next tile's records are prefetched into registers (E per lane) while the current
 // tile runs its LDS rounds, so HBM and LDS work overlap (T14-style issue-early /
@@ -232,7 +268,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // gives lane t the E consecutive records t*E .. t*E+E-1 (groups t*G .. t*G+G-1), so
 // one block-wide exclusive scan of the lanes' counts orders the tile's entries.  The
 // tile was read into LDS before, so the in-place writes are safe.
-template <int MODE, int E, int NT, int RL, bool STRIDED, bool SEL = false>
+template <int MODE, int E, int NT, int RL, bool STRIDED, bool SEL = false, int TL = 0>
 __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
                                                            uint32_t tlog, uint32_t ilog,
                                                            uint32_t wlog, uint32_t dtile,
@@ -273,13 +309,17 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         }
-        lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
-                               (int)(jbot + RL), seed);
+        if constexpr (TL != 0 && !STRIDED)  // tlog == TL (checked by the launcher)
+            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, seed);
+        else
+            lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
+                                   (int)(jbot + RL), seed);
         constexpr int G = E >> RL;
         if constexpr (SEL && !STRIDED) {
             uint64_t v[E];
+            const uint64_t *own = sm + lpad(t * (uint32_t)E);  // E >= 16: lpad splits
 #pragma unroll
-            for (int q = 0; q < E; ++q) v[q] = sm[lpad(t * (uint32_t)E + (uint32_t)q)];
+            for (int q = 0; q < E; ++q) v[q] = own[q + (q >> 4)];
             uint32_t c = 0;
 #pragma unroll
             for (int h = 0; h < G; ++h) {
@@ -324,8 +364,14 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         for (int h = 0; h < G; ++h) {
             const uint32_t b = spread(t + (uint32_t)h * NT, jbot, RL);
             uint64_t v[1 << RL];
+            if (!STRIDED) {  // b = g << RL: lpad(b + q) = lpad(b) + q + (q >> 4)
+                const uint64_t *row = sm + lpad(b);
 #pragma unroll
-            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + ((uint32_t)q << jbot))];
+                for (int q = 0; q < (1 << RL); ++q) v[q] = row[q + (q >> 4)];
+            } else {
+#pragma unroll
+                for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + ((uint32_t)q << jbot))];
+            }
             const uint32_t pb = tile_pos(0u, b, wlog, dtile);  // tile-relative position of v[0]
             group_steps<MODE, RL>(v, base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
             if (STRIDED) {  // v[q] sits 2^dtile positions after v[q-1]: 8-B stores
@@ -675,6 +721,15 @@ static bool direct_merge() {
     return on;
 }
 
+// compile-time LDS rounds in the contiguous direct merges (FLTEE_BITONIC_CT=0: off, A/B)
+static bool merge_ct() {
+    static bool on = [] {
+        const char *e = getenv("FLTEE_BITONIC_CT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // the selection sink of the last pass (see bitonic_merge_direct SEL)
 struct SelSink {
     uint32_t d = 0;
@@ -690,31 +745,45 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
     net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog);  // the select pass writes ~nothing
-#define BD_GO1(RL_, SEL_)                                                                          \
+#define BD_GO1(RL_, SEL_, TL_)                                                                     \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
             (void)hipFuncSetAttribute(                                                             \
-                (const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_>,               \
+                (const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_>,          \
                 hipFuncAttributeMaxDynamicSharedMemorySize,                                        \
                 160 * 1024 - (SEL_ ? 256 : 0)); /* static wtot[] counts against the 160 KB */      \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_>), dim3(c.grid),  \
-                           dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles,     \
-                           pbase, sink.d, sink.cnt);                                               \
+        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_>),           \
+                           dim3(c.grid), dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, \
+                           c.tiles, pbase, sink.d, sink.cnt);                                      \
     } while (0)
-#define BD_GO(RL_)                                                                                 \
+#define BD_GO(RL_, TL_)                                                                            \
     do {                                                                                           \
-        if (!STRIDED && sink.cnt) BD_GO1(RL_, true);                                               \
-        else BD_GO1(RL_, false);                                                                   \
+        if (!STRIDED && sink.cnt) BD_GO1(RL_, true, TL_);                                          \
+        else BD_GO1(RL_, false, TL_);                                                              \
     } while (0)
+    // contiguous tiles of the usual sizes: the LDS rounds unrolled at compile time
+    if constexpr (!STRIDED) {
+        if (merge_ct()) {
+            if constexpr (E == 16 && NT == 1024) {
+                if (c.tlog == 14 && rl == 2) { BD_GO(2, 14); return hipGetLastError(); }
+            }
+            if constexpr (E == 16 && NT == 512) {
+                if (c.tlog == 13 && rl == 1) { BD_GO(1, 13); return hipGetLastError(); }
+            }
+            if constexpr (E == 32 && NT == 512) {
+                if (c.tlog == 14 && rl == 4) { BD_GO(4, 14); return hipGetLastError(); }
+            }
+        }
+    }
     switch (rl) {
-    case 1: BD_GO(1); break;
-    case 2: if constexpr (R1 >= 2) BD_GO(2); break;
-    case 3: if constexpr (R1 >= 3) BD_GO(3); break;
-    case 4: if constexpr (R1 >= 4) BD_GO(4); break;
-    default: if constexpr (R1 >= 5) BD_GO(5); break;
+    case 1: BD_GO(1, 0); break;
+    case 2: if constexpr (R1 >= 2) BD_GO(2, 0); break;
+    case 3: if constexpr (R1 >= 3) BD_GO(3, 0); break;
+    case 4: if constexpr (R1 >= 4) BD_GO(4, 0); break;
+    default: if constexpr (R1 >= 5) BD_GO(5, 0); break;
     }
 #undef BD_GO
 #undef BD_GO1

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfltee_agg.so")
+# FLTEE_LIB: another build of the same library (A/B runs of two builds, scripts/ab_env.py)
+LIB_PATH = os.environ.get("FLTEE_LIB") or os.path.join(PKG_ROOT, "lib", "libfltee_agg.so")
 
 # include/fltee_agg.h
 SUCCESS = 0x0
