@@ -167,19 +167,26 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
 template <int MODE, int R, int E, int NT, int DLOG>
 __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed) {
-    static_assert(DLOG + R >= 4, "slot offsets split only above 16 records");
     constexpr int G = E >> R;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
         const uint32_t g = threadIdx.x + (uint32_t)h * NT;
         const uint32_t b = spread(g, (uint32_t)DLOG, (uint32_t)R);
-        uint64_t *row = sm + lpad(b);
         uint64_t v[1 << R];
+        if constexpr (DLOG + R >= 4) {
+            uint64_t *row = sm + lpad(b);
 #pragma unroll
-        for (int q = 0; q < (1 << R); ++q) v[q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
-        group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
+            for (int q = 0; q < (1 << R); ++q) v[q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
+            group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
 #pragma unroll
-        for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[q];
+            for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[q];
+        } else {  // a group inside 16 records: the padding slot may fall between its records
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << DLOG))];
+            group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << DLOG))] = v[q];
+        }
     }
 }
 template <int MODE, int E, int NT, int JTOP, int JBOT>
@@ -194,6 +201,17 @@ __device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32
     }
 }
 
+// stages IL..TL-1 in full and stage TL down to step RL (bitonic_sort_direct's LDS part)
+template <int MODE, int E, int NT, int IL, int TL, int RL>
+__device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
+    if constexpr (IL < TL) {
+        lds_steps_ct<MODE, E, NT, IL - 1, 0>(sm, base, (uint32_t)IL, seed);
+        sort_stages_ct<MODE, E, NT, IL + 1, TL, RL>(sm, base, seed);
+    } else {
+        lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base, (uint32_t)TL, seed);
+    }
+}
+
 // Persistent tile kernels: a block walks tiles blockIdx.x, +gridDim.x, ...; the
 // next tile's records are prefetched into registers (E per lane) while the current
 // tile runs its LDS rounds, so HBM and LDS work overlap (T14-style issue-early /
@@ -205,7 +223,7 @@ __device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32
 // around each prefetch load makes hipcc branch and wait vmcnt(0) per load
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
-template <int MODE, bool SORT, int E, int NT>
+template <int MODE, bool SORT, int E, int NT, int TL = 0>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase) {
@@ -238,6 +256,8 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
+        } else if constexpr (TL != 0) {  // contiguous merge, tlog == TL (launcher)
+            lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
         } else {
             lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
                                    wlog < tlog ? (int)wlog : 0, seed);
@@ -456,7 +476,7 @@ __device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint
 // 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
 // log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
 // stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
-template <int MODE, int E, int NT, int RL, int GEN = 0>
+template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0>
 __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t seed,
                                                           uint32_t ntiles, uint32_t pbase,
@@ -529,9 +549,13 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
         __syncthreads();
         const uint32_t next = tile + stride;
         load(next < ntiles ? next : tile);
-        for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
-            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
-        lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
+        if constexpr (TL != 0) {  // tlog == TL (launcher)
+            sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
+        } else {
+            for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
+                lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
+            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
+        }
         constexpr int G = E >> RL;
 #pragma unroll
         for (int h = 0; h < G; ++h) {
@@ -676,18 +700,36 @@ static bool strided_passes() {
     return on;
 }
 
-template <int MODE, bool SORT, int E, int NT>
+static bool knob_on(const char *name) {  // default on; "0" turns it off (A/B)
+    const char *e = getenv(name);
+    return !(e && e[0] == '0');
+}
+// compile-time LDS rounds (FLTEE_BITONIC_CT / _SORT_CT / _TILES_CT = 0: off, A/B)
+static bool merge_ct() {
+    static bool on = knob_on("FLTEE_BITONIC_CT");
+    return on;
+}
+static bool sort_ct() {
+    static bool on = knob_on("FLTEE_BITONIC_SORT_CT");
+    return on;
+}
+static bool tiles_ct() {
+    static bool on = knob_on("FLTEE_BITONIC_TILES_CT");
+    return on;
+}
+
+template <int MODE, bool SORT, int E, int NT, int TL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles, uint32_t pbase) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT>), dim3(grid), dim3(NT), lds, s, data,
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL>), dim3(grid), dim3(NT), lds, s, data,
                        tlog, ilog, wlog, dtile, seed, tiles, pbase);
     return hipGetLastError();
 }
@@ -716,15 +758,6 @@ static bool direct_strided() {
 static bool direct_merge() {
     static bool on = [] {
         const char *e = getenv("FLTEE_BITONIC_DIRECT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// compile-time LDS rounds in the contiguous direct merges (FLTEE_BITONIC_CT=0: off, A/B)
-static bool merge_ct() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_CT");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -804,23 +837,35 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
         grid += nb < 1024u ? nb : 1024u;
         net_account((uint64_t)8 * gg.pad_n);
     }
-#define BS_GO(RL_)                                                                                 \
+#define BS_GO(RL_, TL_)                                                                            \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN>,    \
+            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN>), dim3(grid), dim3(NT),     \
-                           c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);                      \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_>), dim3(grid),          \
+                           dim3(NT), c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);            \
     } while (0)
+    // the usual tile sizes: every stage's LDS rounds unrolled at compile time
+    if (sort_ct()) {
+        if constexpr (E == 16 && NT == 1024) {
+            if (c.tlog == 14 && rl == 2) { BS_GO(2, 14); return hipGetLastError(); }
+        }
+        if constexpr (E == 16 && NT == 512) {
+            if (c.tlog == 13 && rl == 1) { BS_GO(1, 13); return hipGetLastError(); }
+        }
+        if constexpr (E == 8 && NT == 512) {
+            if (c.tlog == 12 && rl == 3) { BS_GO(3, 12); return hipGetLastError(); }
+        }
+    }
     switch (rl) {
-    case 1: BS_GO(1); break;
-    case 2: if constexpr (R1 >= 2) BS_GO(2); break;
-    case 3: if constexpr (R1 >= 3) BS_GO(3); break;
-    case 4: if constexpr (R1 >= 4) BS_GO(4); break;
-    default: if constexpr (R1 >= 5) BS_GO(5); break;
+    case 1: BS_GO(1, 0); break;
+    case 2: if constexpr (R1 >= 2) BS_GO(2, 0); break;
+    case 3: if constexpr (R1 >= 3) BS_GO(3, 0); break;
+    case 4: if constexpr (R1 >= 4) BS_GO(4, 0); break;
+    default: if constexpr (R1 >= 5) BS_GO(5, 0); break;
     }
 #undef BS_GO
     return hipGetLastError();
@@ -877,6 +922,9 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
     if (c.NT == 64) BT_GO(2, 64);
+    if (!SORT && wlog == c.tlog && c.E == 8 && c.tlog == 12 && tiles_ct())  // contiguous 2^12 merge
+        return launch_tiles_e<MODE, SORT, 8, 512, 12>(c.grid, c.lds, s, data, c.tlog, ilog, wlog,
+                                                      dtile, seed, c.tiles, pbase);
     switch (c.E) {
     case 2: BT_GO(2, 512);
     case 4: BT_GO(4, 512);
