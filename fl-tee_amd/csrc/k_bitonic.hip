@@ -164,40 +164,45 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
 // [DLOG, DLOG+R) and its part above them is a multiple of 16), so every slot is a
 // ds_read/ds_write immediate offset off one per-group address — five VALU per slot
 // fewer.  Same greedy split into rounds as lds_steps: the same network.
-template <int MODE, int R, int E, int NT, int DLOG>
+// WL > 0: a strided tile (2^WL consecutive positions x rows 2^dtile apart, the rounds at
+// tile-local bits >= WL): the group's first position and global distance from tile_pos.
+template <int MODE, int R, int E, int NT, int DLOG, int WL = 0>
 __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
-                                             uint32_t seed) {
+                                             uint32_t seed, uint32_t dtile = 0) {
+    static_assert(WL == 0 || DLOG >= WL, "strided rounds stay above the row bits");
     constexpr int G = E >> R;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
         const uint32_t g = threadIdx.x + (uint32_t)h * NT;
         const uint32_t b = spread(g, (uint32_t)DLOG, (uint32_t)R);
+        const uint32_t p0 = WL ? tile_pos(base, b, (uint32_t)WL, dtile) : base + b;
+        const uint32_t dg = WL ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
         uint64_t v[1 << R];
         if constexpr (DLOG + R >= 4) {
             uint64_t *row = sm + lpad(b);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) v[q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
-            group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
+            group_steps<MODE, R>(v, p0, dg, ilog, seed);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[q];
         } else {  // a group inside 16 records: the padding slot may fall between its records
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << DLOG))];
-            group_steps<MODE, R>(v, base + b, (uint32_t)DLOG, ilog, seed);
+            group_steps<MODE, R>(v, p0, dg, ilog, seed);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << DLOG))] = v[q];
         }
     }
 }
-template <int MODE, int E, int NT, int JTOP, int JBOT>
+template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0>
 __device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
-                                             uint32_t seed) {
+                                             uint32_t seed, uint32_t dtile = 0) {
     if constexpr (JTOP >= JBOT) {
         constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
         constexpr int r = JTOP - JBOT + 1 < rmax ? JTOP - JBOT + 1 : rmax;
-        lds_round_ct<MODE, r, E, NT, JTOP - r + 1>(sm, base, ilog, seed);
+        lds_round_ct<MODE, r, E, NT, JTOP - r + 1, WL>(sm, base, ilog, seed, dtile);
         __syncthreads();
-        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT>(sm, base, ilog, seed);
+        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT, WL>(sm, base, ilog, seed, dtile);
     }
 }
 
@@ -223,7 +228,7 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 // around each prefetch load makes hipcc branch and wait vmcnt(0) per load
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
-template <int MODE, bool SORT, int E, int NT, int TL = 0>
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase) {
@@ -256,8 +261,10 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
-        } else if constexpr (TL != 0) {  // contiguous merge, tlog == TL (launcher)
+        } else if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
             lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
+        } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
+            lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
         } else {
             lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
                                    wlog < tlog ? (int)wlog : 0, seed);
@@ -408,6 +415,7 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                 for (int q = 0; q < (1 << RL); q += 2) {
                     const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
                                         (uint32_t)(v[q + 1] >> 32)};
+                    __builtin_amdgcn_sched_barrier(0);
                     __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((pb + (uint32_t)q) * 8u),
                                                            (int)(base * 8u), kTileCP);
                     __builtin_amdgcn_sched_barrier(0);
@@ -568,6 +576,9 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             for (int q = 0; q < (1 << RL); q += 2) {
                 const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
                                     (uint32_t)(v[q + 1] >> 32)};
+                // the fence in front too: no VALU of this group sinks below the store
+                // into the window the s_nop covers (seen with the compile-time rounds)
+                __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
                                                        (int)(base * 8u), kTileCP);
                 __builtin_amdgcn_sched_barrier(0);
@@ -718,18 +729,18 @@ static bool tiles_ct() {
     return on;
 }
 
-template <int MODE, bool SORT, int E, int NT, int TL = 0>
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles, uint32_t pbase) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL>), dim3(grid), dim3(NT), lds, s, data,
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL>), dim3(grid), dim3(NT), lds, s, data,
                        tlog, ilog, wlog, dtile, seed, tiles, pbase);
     return hipGetLastError();
 }
@@ -914,6 +925,20 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
         if (c.E == 32) return launch_direct<MODE, 32, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
+    }
+    // strided passes of the usual tile sizes, rows of 2^4 .. 2^7: compile-time rounds
+    if (!SORT && wlog < c.tlog && wlog >= 4 && wlog <= 7 && tiles_ct() &&
+        ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12))) {
+#define BT_ST(E_, NT_, TL_)                                                                        \
+    switch (wlog) {                                                                                \
+    case 4: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 4>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
+    case 5: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 5>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
+    case 6: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 6>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
+    default: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 7>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
+    }
+        if (c.NT == 1024) { BT_ST(16, 1024, 14) }
+        BT_ST(8, 512, 12)
+#undef BT_ST
     }
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
