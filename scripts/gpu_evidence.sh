@@ -33,4 +33,8 @@ for w in ${PMC}; do
       --no-e2e > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
   echo "pmc $w"
 done
+if [ "${CABI:-0}" = 1 ]; then  # the C-ABI multi-GPU eid over the visible GPUs (1-rank RCCL on one)
+  timeout -k 10 300 python -u scripts/ecall_multi_bench.py > "$OUT/c_abi_multi_gpu.json" 2> "$OUT/c_abi_multi_gpu.err" || exit 16
+  echo "c_abi"
+fi
 echo done
