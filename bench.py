@@ -291,7 +291,8 @@ def bench_c4_index_sharded(torch, D, dist, world, rank, device, steps, warmup):
     def step():
         D.laplace_r(d, k, n, seed, device=device)  # each call draws its counts (same seed here)
         D.nips19_build_range(rec, nrec, r, d, tf, lo, C, out=chunk)
-        P.index_sharded_nips19({rank: chunk}, world, M, n, d, seed, ops=ops, comm=comm, dp=dp)
+        P.index_sharded_nips19({rank: chunk}, world, M, n, d, seed, ops=ops, comm=comm, dp=dp,
+                               valid=nrec + d * tf)
 
     for _ in range(warmup):
         step()

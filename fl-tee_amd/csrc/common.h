@@ -90,6 +90,7 @@ hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint
 hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, hipStream_t s,
                         size_t valid = 0);
 void set_pad_skip(int on);
+bool pad_skip_enabled();
 // stages up to log2(seg) only: aligned segments of seg records sorted, alternating
 // ascending (even segments) / descending (odd segments)
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,
@@ -113,8 +114,9 @@ void set_fused_init(int on);
 // one range [pbase, pbase + m) of a larger network (pbase a multiple of m): stages
 // 1..log2 m; the steps j < m of stage ilog; the step 2^jlog >= m of stage ilog
 // between this range and the partner range pos_theirs = pos_mine ^ 2^jlog
+// valid (0 = unknown): positions >= valid of this range hold identical pads
 hipError_t bitonic_sort_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
-                              uint32_t pbase, hipStream_t s);
+                              uint32_t pbase, hipStream_t s, uint32_t valid = 0);
 hipError_t bitonic_merge_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
                                uint32_t ilog, uint32_t pbase, hipStream_t s);
 hipError_t bitonic_steps_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,

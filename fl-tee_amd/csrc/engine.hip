@@ -532,6 +532,18 @@ extern "C" fltee_status_t fltee_bitonic_range_sort_device(void *d_records, size_
                : FLTEE_ERROR_UNEXPECTED;
 }
 
+extern "C" fltee_status_t fltee_bitonic_range_sort_padded_device(void *d_records, size_t m,
+                                                                 size_t pos_base, size_t valid,
+                                                                 uint32_t mode, uint32_t seed,
+                                                                 void *stream) {
+    if (!range_ok(m, pos_base)) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (valid == 0) return FLTEE_SUCCESS;  // pads alone: sorted as they are
+    return bitonic_sort_range((uint64_t *)d_records, m, mode, seed, (uint32_t)pos_base,
+                              (hipStream_t)stream, valid >= m ? 0u : (uint32_t)valid) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
 extern "C" fltee_status_t fltee_bitonic_range_merge_device(void *d_records, size_t m,
                                                            size_t pos_base, uint32_t mode,
                                                            uint32_t seed, uint32_t stage_log,

@@ -449,15 +449,32 @@ uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const u
 // range sorts, then per stage the cross-range steps (transposed: two all-to-alls
 // around local register passes, mode 0; pairwise: a swap with partner r ^ j/C per
 // step) and the range merges — fltee/parallel.py distributed_network, on the ranks.
+// valid: positions >= valid hold identical pads.  As in the single-GPU network, a stage
+// leaves every aligned 2^stage block of pads alone unchanged: a range sort runs only on
+// its live prefix (none at all for a range of pads), and a later stage skips the ranges
+// at or past roundup(valid, 2^stage) — their pairwise partners lie in the same block,
+// so both sides of a skipped exchange are skipped.  The transposed exchange mixes
+// every range, so its stages skip nothing.  Public sizes only: still oblivious.
 static hipError_t network(Group &G, std::vector<uint64_t *> &chunk, std::vector<uint64_t *> &spare,
-                          size_t M, uint32_t mode, uint32_t key, bool transpose) {
+                          size_t M, uint32_t mode, uint32_t key, bool transpose, size_t valid) {
     const int W = G.W;
     const size_t C = M / W;
     const uint32_t clog = log2_pow2(C), mlog = log2_pow2(M), wlog = log2_pow2(W);
+    if (valid > M || !pad_skip_enabled()) valid = M;
+    auto live_from = [&](uint32_t stage) -> size_t {  // ranges r with r*C >= this are pads alone
+        const size_t blk = (size_t)1 << stage;
+        const size_t b = (valid + blk - 1) / blk * blk;
+        return b >= M ? M : b;
+    };
     hipError_t e;
     for (int i = 0; i < W; ++i) {
+        const size_t lo = (size_t)i * C;
+        if (lo >= valid) continue;  // pads alone
+        const size_t vl = valid - lo;
         if ((e = hipSetDevice(G.r[i].dev)) != hipSuccess) return e;
-        if ((e = bitonic_sort_range(chunk[i], C, mode, key, (uint32_t)(i * C), G.r[i].s)) != hipSuccess) return e;
+        if ((e = bitonic_sort_range(chunk[i], C, mode, key, (uint32_t)lo, G.r[i].s,
+                                    vl >= C ? 0u : (uint32_t)vl)) != hipSuccess)
+            return e;
     }
     const size_t b = C / W;
     for (uint32_t stage = clog + 1; stage <= mlog; ++stage) {
@@ -479,12 +496,15 @@ static hipError_t network(Group &G, std::vector<uint64_t *> &chunk, std::vector<
                     }
             }
         } else {
+            const size_t sf = live_from(stage);
             for (int j = (int)stage - 1; j >= (int)clog; --j) {
                 const int bit = 1 << (j - (int)clog);
                 std::vector<P2P> ops;
-                for (int r = 0; r < W; ++r) ops.push_back({r ^ bit, r, chunk[r ^ bit], spare[r], C * 8});
+                for (int r = 0; r < W; ++r)
+                    if ((size_t)r * C < sf) ops.push_back({r ^ bit, r, chunk[r ^ bit], spare[r], C * 8});
                 if ((e = p2p(G, ops)) != hipSuccess) return e;
                 for (int r = 0; r < W; ++r) {
+                    if ((size_t)r * C >= sf) continue;
                     if ((e = hipSetDevice(G.r[r].dev)) != hipSuccess) return e;
                     if ((e = bitonic_exchange(chunk[r], spare[r], C, (uint32_t)(r * C),
                                               (uint32_t)((r ^ bit) * C), mode, key, stage,
@@ -493,7 +513,9 @@ static hipError_t network(Group &G, std::vector<uint64_t *> &chunk, std::vector<
                 }
             }
         }
+        const size_t sf = transpose ? M : live_from(stage);
         for (int i = 0; i < W; ++i) {
+            if ((size_t)i * C >= sf) continue;
             if ((e = hipSetDevice(G.r[i].dev)) != hipSuccess) return e;
             if ((e = bitonic_merge_range(chunk[i], C, mode, key, stage, (uint32_t)(i * C), G.r[i].s)) != hipSuccess)
                 return e;
@@ -533,7 +555,7 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
             launch_advanced_init_range(rec[i], nrec, d, i * C, C, chunk[i], G.r[i].s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
     }
-    if (network(G, chunk, spare, M, 0, 0, W > 1) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (network(G, chunk, spare, M, 0, 0, W > 1, n * k + d) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     // fold (advanced.rs:66-101) with the previous range's tail in front and the next
     // range's head behind; a run longer than the halo widens it (as the ECALL does)
     const size_t fold_len = L, max_run = L;
@@ -616,7 +638,7 @@ uint32_t group_nips19(Group *Gp, DeviceCtx *root, const GroupInput &in, size_t n
                                       chunk[i], R.s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
     }
-    if (network(G, chunk, spare, M, 2, key, false) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (network(G, chunk, spare, M, 2, key, false, nrec + d * tf) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     // safe_aggregate (common.rs:25-35): every range selects its idx < d entries in order;
     // the lists, concatenated in range order, are the shuffled array's in position order
     const size_t nb = select_tiles(C);

@@ -1016,6 +1016,7 @@ static TileCfg live_tiles(const TileCfg &c, uint32_t skip) {
 }
 static bool g_pad_skip = true;  // fltee_debug_set_pad_skip (A/B)
 void set_pad_skip(int on) { g_pad_skip = on != 0; }
+bool pad_skip_enabled() { return g_pad_skip; }
 
 // Steps jtop..0 of stage ilog (ilog > c.tlog) over the m = 2^mlog records at global
 // positions pbase..pbase+m-1: the steps with j >= T in register passes (up to 6 steps)
@@ -1242,14 +1243,15 @@ hipError_t bitonic_sort_nips19_select(uint64_t *data, size_t m, uint32_t seed, c
 // stage ilog > log2 m the exchange steps j >= m (bitonic_exchange with the partner
 // range pbase ^ j) and merge_range.  Together: the reference network, step for step.
 hipError_t bitonic_sort_range(uint64_t *data, size_t m, uint32_t mode, uint32_t seed,
-                              uint32_t pbase, hipStream_t s) {
+                              uint32_t pbase, hipStream_t s, uint32_t valid) {
     if (m < 2) return hipSuccess;
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
     const uint32_t mlog = log2_pow2(m);
+    if (valid >= m) valid = 0;
     switch (mode) {
-    case 0: return sort_impl<0>(data, m, seed, s, mlog, pbase);
-    case 1: return sort_impl<1>(data, m, seed, s, mlog, pbase);
-    default: return sort_impl<2>(data, m, seed, s, mlog, pbase);
+    case 0: return sort_impl<0>(data, m, seed, s, mlog, pbase, valid);
+    case 1: return sort_impl<1>(data, m, seed, s, mlog, pbase, valid);
+    default: return sort_impl<2>(data, m, seed, s, mlog, pbase, valid);
     }
 }
 

@@ -78,6 +78,7 @@ SIGNATURES = {
     "fltee_encrypt_device": (_U32, [_P, _S, _P, _S, _P, _P]),
     "fltee_advanced_init_range_device": (_U32, [_P, _S, _S, _S, _S, _P, _P]),
     "fltee_bitonic_range_sort_device": (_U32, [_P, _S, _S, _U32, _U32, _P]),
+    "fltee_bitonic_range_sort_padded_device": (_U32, [_P, _S, _S, _S, _U32, _U32, _P]),
     "fltee_bitonic_range_merge_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _P]),
     "fltee_bitonic_range_exchange_device": (_U32, [_P, _P, _S, _S, _S, _U32, _U32, _U32, _P]),
     "fltee_bitonic_range_steps_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _U32, _U32, _P]),

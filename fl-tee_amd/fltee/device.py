@@ -144,7 +144,14 @@ def advanced_init_range(records, nrec, d, pos_base, m, out=None, stream=None):
     return out
 
 
-def bitonic_range_sort(records, pos_base, mode=0, seed=0, stream=None):
+def bitonic_range_sort(records, pos_base, mode=0, seed=0, stream=None, valid=None):
+    """valid: entries valid.. of this range are identical pads (None: unknown)."""
+    if valid is not None:
+        _check(L.lib().fltee_bitonic_range_sort_padded_device(_ptr(records), records.numel(),
+                                                              pos_base, valid, mode, seed,
+                                                              _stream(stream)),
+               "fltee_bitonic_range_sort_padded_device")
+        return records
     _check(L.lib().fltee_bitonic_range_sort_device(_ptr(records), records.numel(), pos_base, mode,
                                                    seed, _stream(stream)),
            "fltee_bitonic_range_sort_device")

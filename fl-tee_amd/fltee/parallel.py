@@ -141,8 +141,8 @@ class DeviceRangeOps:
     def fold_context(self, halo):
         return self.D.fold_context(halo)
 
-    def sort(self, x, pos, mode=0, seed=0):
-        self.D.bitonic_range_sort(x, pos, mode=mode, seed=seed)
+    def sort(self, x, pos, mode=0, seed=0, valid=None):
+        self.D.bitonic_range_sort(x, pos, mode=mode, seed=seed, valid=valid)
 
     def merge(self, x, pos, stage_log, mode=0, seed=0):
         self.D.bitonic_range_merge(x, pos, stage_log, mode=mode, seed=seed)
@@ -313,19 +313,35 @@ class DistRanks:
 
 
 def distributed_network(chunks, world, M, ops, comm, mode=0, seed=0, exchange="transpose",
-                        spare=None):
+                        spare=None, valid=None):
     """The reference network (advanced.rs:147-176; mode 2: the keyed shuffle of
     nips19.rs:66-105) over M positions split into `world` ranges of C = M / world:
     every range runs stages up to C on its own, then each later stage does its steps
     j >= C across ranges (see index_sharded_advanced for the two exchanges; the
     transposed one needs only directions, so mode 2 always swaps pairwise) and its
     steps j < C inside each range.  Returns the chunks dict (ranges may have moved to
-    the `spare` buffers)."""
+    the `spare` buffers).
+
+    valid (None: unknown): positions >= valid hold identical pads.  A stage leaves every
+    aligned 2^stage block of pads alone as it is, so a range sort runs on its live prefix
+    only (a range of pads alone not at all), and a pairwise stage skips the ranges at or
+    past roundup(valid, 2^stage) — a skipped range's partners lie in the same block, so
+    both sides skip the exchange.  The transposed exchange mixes every range: its stages
+    skip nothing.  Public sizes only: the network stays oblivious and bit-identical."""
     C = M // world
     clog, mlog = C.bit_length() - 1, M.bit_length() - 1
     assert 1 << clog == C and 1 << mlog == M
+    vbound = M if valid is None else min(int(valid), M)
+
+    def live_from(stage):
+        blk = 1 << stage
+        return min((vbound + blk - 1) // blk * blk, M)
+
     for r, x in chunks.items():
-        ops.sort(x, r * C, mode=mode, seed=seed)
+        lo = r * C
+        if lo >= vbound:
+            continue  # pads alone
+        ops.sort(x, lo, mode=mode, seed=seed, valid=None if vbound - lo >= C else vbound - lo)
     wlog = world.bit_length() - 1
     transpose = exchange == "transpose" and world > 1 and mode == 0
     if transpose:
@@ -341,19 +357,23 @@ def distributed_network(chunks, world, M, ops, comm, mode=0, seed=0, exchange="t
             comm.transpose(chunks, spare)
             chunks, spare = spare, chunks
         else:
+            sf = live_from(stage)
+            live = {r: x for r, x in chunks.items() if r * C < sf}
             for j in range(stage - 1, clog - 1, -1):
                 bit = 1 << (j - clog)
-                theirs = comm.swap(chunks, lambda q: q ^ bit)
-                for r, x in chunks.items():
+                theirs = comm.swap(live, lambda q: q ^ bit) if live else {}
+                for r, x in live.items():
                     ops.exchange(x, theirs[r], r * C, (r ^ bit) * C, stage, mode=mode, seed=seed)
                 del theirs
+        sf = M if transpose else live_from(stage)
         for r, x in chunks.items():
-            ops.merge(x, r * C, stage, mode=mode, seed=seed)
+            if r * C < sf:
+                ops.merge(x, r * C, stage, mode=mode, seed=seed)
     return chunks
 
 
 def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None, root=0,
-                         dp=None):
+                         dp=None, valid=None):
     """nips19 (nips19.rs:18-63) by position range: `chunks` = the ranges of the padded
     array (records ++ Laplace dummies ++ pads, fltee_nips19_build_range with the same
     Laplace counts on every rank: counter-based, no exchange); the keyed shuffle runs
@@ -361,12 +381,14 @@ def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None
     safe_aggregate's selection on its range (its entries with idx < d, in position
     order), the lists are gathered to the root in rank order — the shuffled order — and
     the root adds each index's entries in that order (fltee_ordered_list_device), x
-    1f32/n, then DP noise.  Bit-identical to one GPU's nips19."""
+    1f32/n, then DP noise.  Bit-identical to one GPU's nips19.  valid = n·k + d·⌊T⌋ (the
+    records and Laplace dummies in front of the pads) lets the network skip pad blocks."""
     assert world & (world - 1) == 0 and M % world == 0
     ops = ops if ops is not None else DeviceRangeOps()
     comm = comm if comm is not None else VirtualRanks(world)
     key = (seed ^ (seed >> 32)) & 0xFFFFFFFF  # the shuffle key of fltee_aggregate_device
-    chunks = distributed_network(chunks, world, M, ops, comm, mode=2, seed=key, exchange="pairwise")
+    chunks = distributed_network(chunks, world, M, ops, comm, mode=2, seed=key, exchange="pairwise",
+                                 valid=valid)
     lists = {r: ops.select(x, d) for r, x in chunks.items()}
     full = comm.gather_lists(lists, root)
     if full is None:
@@ -406,7 +428,8 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     ops = ops if ops is not None else DeviceRangeOps()
     comm = comm if comm is not None else VirtualRanks(world)
     C = M // world
-    chunks = distributed_network(chunks, world, M, ops, comm, exchange=exchange, spare=spare)
+    chunks = distributed_network(chunks, world, M, ops, comm, exchange=exchange, spare=spare,
+                                 valid=n_total * k + d)
     fold_len = n_total * k + d
     h = n_total if halo is None else halo
     while True:

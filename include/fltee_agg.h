@@ -252,6 +252,12 @@ fltee_status_t fltee_advanced_init_range_device(const void *d_records, size_t nr
  * direction of every compare-exchange comes from its GLOBAL position. */
 fltee_status_t fltee_bitonic_range_sort_device(void *d_records, size_t m, size_t pos_base,
                                                uint32_t mode, uint32_t seed, void *stream);
+/* the same, knowing that entries valid .. m-1 of the range are identical (u32::MAX,
+ * +0.0) pads (valid >= m: none): stage blocks made of pads alone are skipped, which
+ * leaves them as they are — the same permutation.  valid = 0: nothing to do. */
+fltee_status_t fltee_bitonic_range_sort_padded_device(void *d_records, size_t m, size_t pos_base,
+                                                      size_t valid, uint32_t mode, uint32_t seed,
+                                                      void *stream);
 /* the steps j = m/2 .. 1 of stage 2^stage_log (> m) on one range. */
 fltee_status_t fltee_bitonic_range_merge_device(void *d_records, size_t m, size_t pos_base,
                                                 uint32_t mode, uint32_t seed, uint32_t stage_log,

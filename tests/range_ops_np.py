@@ -58,7 +58,7 @@ class NumpyRangeOps:
     def fold_context(self, halo):
         return (halo + 15) // 16 * 16
 
-    def sort(self, x, pos, mode=0, seed=0):
+    def sort(self, x, pos, mode=0, seed=0, valid=None):  # valid: the full network is the same
         a = _u(x)
         for ilog in range(1, len(a).bit_length()):
             for jlog in range(ilog - 1, -1, -1):

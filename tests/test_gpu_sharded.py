@@ -79,7 +79,8 @@ def test_index_sharded_nips19_matches_single_gpu(dev, world):
     C = M // world
     chunks = {q: dev.nips19_build_range(rec[q * C:] if q * C < nrec else rec, nrec, r, d, tf,
                                         q * C, C) for q in range(world)}
-    out = index_sharded_nips19(chunks, world, M, n, d, seed, comm=VirtualRanks(world)).cpu().numpy()
+    out = index_sharded_nips19(chunks, world, M, n, d, seed, comm=VirtualRanks(world),
+                               valid=nrec + d * tf).cpu().numpy()
     assert np.array_equal(out.view(np.uint32), single.view(np.uint32))
 
 
