@@ -259,6 +259,109 @@ __global__ __launch_bounds__(DS_NT) void dense_accumulate_lds(const uint2 *__res
     }
 }
 
+// Small d, LDS-DMA ring: a 256-lane block owns 64 outputs; chunks of 16 clients (8 KB)
+// land in a 4-slot LDS ring straight from HBM (global_load_lds, 16 B per lane: one wave
+// instruction fills two clients' 512-B rows), so 4 chunks are in flight per block and a
+// CU holds 4-5 blocks — about 128 KB of loads in flight per CU, where the register-staged
+// kernel above has one 32 KB chunk per block.  Wave 0 sums each chunk's clients in client
+// order (lane = output), exactly the adds of dense_accumulate_v: bit-identical.  Waits
+// are counted per wave (each wave's own LDS-DMA, vmcnt) and the block syncs with raw
+// s_barrier: __syncthreads() would drain every load in flight (vmcnt(0)).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Four separately named ring slots with the slot of every access known at compile time
+// (the chunk loop unrolled by 4): hipcc's wait insertion then sees that a slot's reads
+// cannot alias the LDS-DMA still in flight into the other three, and waits only for the
+// counted vmcnt above instead of draining every load (vmcnt(0)) before the first read.
+constexpr int DG_OB = 64, DG_CC = 16;
+__shared__ __attribute__((aligned(16))) uint2 dg_ring0[DG_CC][DG_OB];
+__shared__ __attribute__((aligned(16))) uint2 dg_ring1[DG_CC][DG_OB];
+__shared__ __attribute__((aligned(16))) uint2 dg_ring2[DG_CC][DG_OB];
+__shared__ __attribute__((aligned(16))) uint2 dg_ring3[DG_CC][DG_OB];
+template <int S>
+__device__ __forceinline__ uint2 (&dg_slot())[DG_CC][DG_OB] {
+    if constexpr (S == 0) return dg_ring0;
+    else if constexpr (S == 1) return dg_ring1;
+    else if constexpr (S == 2) return dg_ring2;
+    else return dg_ring3;
+}
+
+template <int S>
+__device__ __forceinline__ void dg_issue(const uint2 *__restrict__ rec, size_t d, uint32_t n,
+                                         uint32_t ch, uint32_t w, uint32_t l, size_t jl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t row = 2 * (w + 4 * (uint32_t)i);
+        uint32_t c = ch * DG_CC + row + (l >> 5);
+        if (c >= n) c = n - 1;  // clamped, never summed
+        __builtin_amdgcn_global_load_lds((const void *)(rec + (size_t)c * d + jl),
+                                         (void __attribute__((address_space(3))) *)&dg_slot<S>()[row][0],
+                                         16, 0, 0);
+    }
+}
+
+// one chunk: wait for this wave's loads of it, sum it (wave 0), free the slot, refill it
+template <int S, bool CLIP>
+__device__ __forceinline__ void dg_step(const uint2 *__restrict__ rec, size_t d, uint32_t n,
+                                        uint32_t nch, uint32_t ch, uint32_t w, uint32_t l,
+                                        size_t jl, size_t j, const float *__restrict__ ccoef,
+                                        float &acc, uint32_t &bad) {
+    const uint32_t ahead = nch - ch - 1 < 3u ? nch - ch - 1 : 3u;  // later chunks in flight
+    if (ahead >= 3) wait_vmcnt<6>();
+    else if (ahead == 2) wait_vmcnt<4>();
+    else if (ahead == 1) wait_vmcnt<2>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (w == 0 && j < d) {
+        const uint32_t cend = n - ch * DG_CC < (uint32_t)DG_CC ? n - ch * DG_CC : (uint32_t)DG_CC;
+        for (uint32_t cl = 0; cl < cend; ++cl) {
+            const uint2 x = dg_slot<S>()[cl][l];
+            float a = __uint_as_float(x.y);
+            if (CLIP) a = __fmul_rn(a, ccoef[ch * DG_CC + cl]);
+            acc = __fadd_rn(acc, a);
+            bad |= x.x ^ (uint32_t)j;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave 0's reads of the slot retired
+    __builtin_amdgcn_s_barrier();
+    if (ch + 4 < nch) dg_issue<S>(rec, d, n, ch + 4, w, l, jl);
+}
+
+template <bool CLIP, bool ACC>
+__global__ __launch_bounds__(256) void dense_accumulate_glds(const uint2 *__restrict__ rec, size_t d,
+                                                             uint32_t n, float coef,
+                                                             float *__restrict__ out,
+                                                             const float *__restrict__ ccoef,
+                                                             uint32_t *status) {
+    const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+    const size_t j0 = (size_t)blockIdx.x * DG_OB;
+    const uint32_t nch = (n + DG_CC - 1) / DG_CC;
+    // lane l of wave w, instruction i: client 2*(w + 4i) + (l >> 5) of the chunk, record
+    // pair l & 31 (one wave instruction = two clients' 512-B rows, lane-linear in LDS)
+    size_t jl = j0 + 2 * (l & 31);
+    if (jl + 2 > d) jl = d - 2;  // d even (launcher); past d: clamped, never stored
+    dg_issue<0>(rec, d, n, 0, w, l, jl);
+    if (nch > 1) dg_issue<1>(rec, d, n, 1, w, l, jl);
+    if (nch > 2) dg_issue<2>(rec, d, n, 2, w, l, jl);
+    if (nch > 3) dg_issue<3>(rec, d, n, 3, w, l, jl);
+    float acc = 0.0f;
+    uint32_t bad = 0;
+    const size_t j = j0 + l;
+    for (uint32_t ch = 0; ch < nch; ch += 4) {
+        dg_step<0, CLIP>(rec, d, n, nch, ch, w, l, jl, j, ccoef, acc, bad);
+        if (ch + 1 < nch) dg_step<1, CLIP>(rec, d, n, nch, ch + 1, w, l, jl, j, ccoef, acc, bad);
+        if (ch + 2 < nch) dg_step<2, CLIP>(rec, d, n, nch, ch + 2, w, l, jl, j, ccoef, acc, bad);
+        if (ch + 3 < nch) dg_step<3, CLIP>(rec, d, n, nch, ch + 3, w, l, jl, j, ccoef, acc, bad);
+    }
+    if (w == 0 && j < d) {
+        out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
+        if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+    }
+}
+
 // Tuning hook (fltee_debug_set_dense_variant): 0 is the shipped configuration.
 static int g_dense_variant = 0;
 
@@ -300,6 +403,15 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         case 21: launch_lds<CLIP, ACC, 128, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
         case 22: launch_lds<CLIP, ACC, 256, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
         case 23: launch_lds<CLIP, ACC, 64, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        case 24:
+            if (vec && d >= 2) {
+                hipLaunchKernelGGL((dense_accumulate_glds<CLIP, ACC>), dim3((unsigned)((d + 63) / 64)),
+                                   dim3(256), 0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out,
+                                   ccoef, status);
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
         default: launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s); break;
         }
         return hipGetLastError();

@@ -17,7 +17,8 @@ VARIANTS = {0: "V1 U16 nt 512 lanes (shipped)", 1: "V1 U8 nt", 2: "V1 U32 nt", 3
             9: "V1 U16 nt 128 lanes", 10: "8 B/lane U16", 11: "8 B/lane U32", 12: "V1 U16 nt 64 lanes",
             13: "V1 U16 nt 256 lanes (round-1 default)",
             20: "small d: LDS 64 outputs x 32 clients", 21: "small d: LDS 128 x 16",
-            22: "small d: LDS 256 x 16", 23: "small d: LDS 64 x 16"}
+            22: "small d: LDS 256 x 16", 23: "small d: LDS 64 x 16",
+            24: "small d: LDS-DMA ring, 64 outputs x 4 chunks of 16 clients"}
 
 
 def main():
@@ -26,6 +27,8 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--n", type=int, default=100)
     ap.add_argument("--d", type=int, default=1_000_000)
+    ap.add_argument("--buffers", type=int, default=3, help="rotating inputs (10 at MNIST size: cold)")
+    ap.add_argument("--variants", default="", help="comma list (default: all)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +37,12 @@ def main():
     from fltee import _lib as L
     from fltee import device as D
     n, d = args.n, args.d
-    recs = [bench.make_records(torch, n, d, None, 7 + b, "cuda") for b in range(3)]
+    recs = [bench.make_records(torch, n, d, None, 7 + b, "cuda") for b in range(args.buffers)]
+    if args.variants:
+        keep = {int(v) for v in args.variants.split(",")}
+        for v in list(VARIANTS):
+            if v not in keep:
+                del VARIANTS[v]
     out = torch.empty(d, dtype=torch.float32, device="cuda")
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
     ref = None
@@ -51,7 +59,7 @@ def main():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for i in range(args.launches):
-                D.aggregate(3, recs[i % 3], n, d, d, out=out, dense=True, status=st)
+                D.aggregate(3, recs[i % len(recs)], n, d, d, out=out, dense=True, status=st)
             b.record()
             torch.cuda.synchronize()
             times[v].append(a.elapsed_time(b) / args.launches)

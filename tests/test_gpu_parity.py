@@ -59,11 +59,14 @@ def test_dense_bit_exact(dev, oracle, n, d, alg):
     assert st == 0 and bits_equal(out, ref)
 
 
-@pytest.mark.parametrize("n,d", [(100, 50890), (45, 1001)])
+@pytest.mark.parametrize("n,d", [(100, 50890), (45, 1001), (3, 130), (16, 2048), (65, 4096),
+                                 (1000, 256), (30, 50890)])
 @pytest.mark.parametrize("clip,acc", [(True, False), (False, True), (True, True)])
 def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
-    """The LDS-staged small-d kernel == the one-lane-per-pair streaming kernel (tuning
-    variant 13), bit for bit, with the per-client clip and accumulate fused."""
+    """The LDS-staged small-d kernels (register-staged chunks, variant 0's default; the
+    LDS-DMA ring, variant 24) == the one-lane-per-pair streaming kernel (variant 13), bit
+    for bit, with the per-client clip and accumulate fused; partial and whole chunks of
+    16 / 32 clients, a partial last block of outputs."""
     import torch
 
     from fltee import _lib as L
@@ -74,7 +77,7 @@ def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
     prev = torch.from_numpy(rng.normal(0, 1, d).astype(np.float32)).cuda()
     outs = []
     try:
-        for variant in (0, 13):
+        for variant in (0, 13, 24):
             L.lib().fltee_debug_set_dense_variant(variant)
             out = prev.clone()
             dev.aggregate(3, rec, n, d, d, out=out, dense=True, clip=clip, clipping=0.5,
@@ -83,7 +86,7 @@ def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
             outs.append(out.cpu().numpy())
     finally:
         L.lib().fltee_debug_set_dense_variant(0)
-    assert bits_equal(outs[0], outs[1])
+    assert bits_equal(outs[0], outs[1]) and bits_equal(outs[0], outs[2])
 
 
 def test_dense_order_violation_is_reported(dev):
