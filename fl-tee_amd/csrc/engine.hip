@@ -677,6 +677,12 @@ extern "C" fltee_status_t fltee_ordered_list_device(const void *d_list, size_t l
 
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
 
+// the planned network schedule (k_bitonic.hip plan_network), 8 words per launch
+extern "C" size_t fltee_debug_network_plan(uint32_t mlog, uint32_t tlog, uint32_t nt, int rmax,
+                                           uint32_t *out, size_t cap) {
+    return fltee::debug_plan(mlog, tlog, nt, rmax, out, cap);
+}
+
 // measurement hook: streaming passes launched and the bytes they sweep since the last reset
 extern "C" void fltee_debug_net_stats(uint64_t *launches, uint64_t *bytes, int reset) {
     if (launches) *launches = fltee::g_net_launches.load();

@@ -27,6 +27,10 @@
 //     merge     : steps j < T in one LDS launch (4 steps per barrier).
 // LDS layout pads one slot per 16 records so that the 64 lanes of a wave hit
 // distinct banks when each walks a 16-record group.
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "common.h"
 
 namespace fltee {
@@ -231,7 +235,8 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                                    uint32_t seed, uint32_t ntiles, uint32_t pbase) {
+                                                    uint32_t seed, uint32_t ntiles, uint32_t pbase,
+                                                    uint32_t seg0) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -261,13 +266,21 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
-        } else if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
-            lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
-        } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
-            lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
         } else {
-            lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
-                                   wlog < tlog ? (int)wlog : 0, seed);
+            // seg0 = (stage << 8) | top: first the last steps top..0 of an earlier stage on
+            // the tile's low (consecutive) bits — a stage's tail fused with the next
+            // stage's head (the planned schedule, plan_network)
+            if (seg0)
+                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, seg0 >> 8, (int)(seg0 & 0xFFu), 0,
+                                       seed);
+            if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
+                lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
+            } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
+                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+            } else if (ilog) {  // ilog = 0: no steps on the row bits
+                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
+                                       wlog < tlog ? (int)wlog : 0, seed);
+            }
         }
         {
             const uint32_t sb = base * 8u;
@@ -732,7 +745,7 @@ static bool tiles_ct() {
 template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                 uint32_t seed, uint32_t tiles, uint32_t pbase) {
+                                 uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL>,
@@ -741,7 +754,7 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
     }
     net_account((uint64_t)16 * tiles << tlog);
     hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL>), dim3(grid), dim3(NT), lds, s, data,
-                       tlog, ilog, wlog, dtile, seed, tiles, pbase);
+                       tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
     return hipGetLastError();
 }
 
@@ -902,8 +915,9 @@ static bool direct_sort() {
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
-                               const SelSink &sink = SelSink{}) {
+                               const SelSink &sink = SelSink{}, uint32_t seg0 = 0) {
     if (c.tiles == 0) return hipSuccess;  // every tile in pad-only stage blocks
+    const bool plain = seg0 == 0 && ilog != 0;  // one segment over every row bit
     if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
         if (c.NT == 1024 && sort32()) return launch_sort_direct<MODE, 32, 512>(as_e32(c), s, data, seed, pbase);
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
@@ -913,41 +927,41 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
-    if (!SORT && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
+    if (!SORT && plain && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
         if (c.E == 32) return launch_direct<MODE, 32, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
     }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
     if (sink.cnt) return hipErrorNotSupported;  // only the direct contiguous merge selects
     // strided tiles (W consecutive x 2^R rows), the same first / last round in registers
-    if (!SORT && wlog < c.tlog && c.tlog > 6 && direct_strided() &&
+    if (!SORT && plain && wlog < c.tlog && c.tlog > 6 && direct_strided() &&
         (int)(c.tlog - wlog) > (c.E >= 32 ? 5 : 4)) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
         if (c.E == 32) return launch_direct<MODE, 32, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
     }
     // strided passes of the usual tile sizes, rows of 2^4 .. 2^7: compile-time rounds
-    if (!SORT && wlog < c.tlog && wlog >= 4 && wlog <= 7 && tiles_ct() &&
+    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && wlog <= 7 && tiles_ct() &&
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12))) {
 #define BT_ST(E_, NT_, TL_)                                                                        \
     switch (wlog) {                                                                                \
-    case 4: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 4>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
-    case 5: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 5>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
-    case 6: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 6>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
-    default: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 7>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase); \
+    case 4: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 4>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
+    case 5: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 5>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
+    case 6: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 6>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
+    default: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 7>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
     }
         if (c.NT == 1024) { BT_ST(16, 1024, 14) }
         BT_ST(8, 512, 12)
 #undef BT_ST
     }
 #define BT_GO(E_, NT_) \
-    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase)
+    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0)
     if (c.NT == 1024) BT_GO(16, 1024);
     if (c.E == 32) BT_GO(32, 512);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
     if (c.NT == 64) BT_GO(2, 64);
-    if (!SORT && wlog == c.tlog && c.E == 8 && c.tlog == 12 && tiles_ct())  // contiguous 2^12 merge
+    if (!SORT && plain && wlog == c.tlog && c.E == 8 && c.tlog == 12 && tiles_ct())  // contiguous 2^12 merge
         return launch_tiles_e<MODE, SORT, 8, 512, 12>(c.grid, c.lds, s, data, c.tlog, ilog, wlog,
                                                       dtile, seed, c.tiles, pbase);
     switch (c.E) {
@@ -1057,6 +1071,181 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c0, 
     return launch_tiles<MODE, false>(c, s, data, ilog, tlog, tlog, seed, pbase, sink);
 }
 
+
+// ------------------------------------------------------------ planned schedule --
+// The steps of stages T+1 .. M (after the first pass) split into launches by a shortest
+// path over the step sequence, instead of "per stage: register / strided passes for the
+// steps j >= T, then one merge for j < T".  A launch is
+//   * a register pass: up to rmax consecutive steps of one stage (bitonic_global);
+//   * an LDS tile pass over 2^tlog records whose positions vary in bits [0, wlog) (W >= 16
+//     consecutive records: coalesced) and in tlog - wlog row bits from dtile up.  It runs
+//     at most two segments, in network order: a stage's LAST steps on bits aTop..0 (low
+//     bits) and then the next stage's FIRST steps on every row bit (a tail fused with the
+//     next head), or one of them alone.
+// Each launch costs about the same whatever the steps (HBM or launch bound), so fewer
+// launches win: at M = 2^27 / 2^14 tiles 23 instead of 35, at 2^20 / 2^12 tiles 13
+// instead of 17.  The steps and their order are the reference network's: bit-identical.
+// The last launch is always the contiguous merge of stage M's last tlog steps (the direct
+// merge, and the only pass that can carry the selection sink).
+struct NetPass {
+    bool reg = false;
+    uint32_t ilog = 0, jtop = 0, R = 0;  // register pass
+    uint32_t ilogA = 0, aTop = 0;        // tile: segment A (0: none), steps aTop..0
+    uint32_t ilogB = 0;                  // tile: segment B (0: none), steps on every row bit
+    uint32_t wlog = 0, dtile = 0;        // tile shape
+    uint32_t stage = 0;                  // the last stage the launch touches (pad skip)
+};
+
+static bool plan_enabled() {
+    static bool on = knob_on("FLTEE_BITONIC_PLAN");
+    return on;
+}
+
+static std::vector<NetPass> plan_network(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax) {
+    const uint32_t minw = (uint32_t)min_w_log();
+    uint32_t ntl = 0;
+    while ((1u << (ntl + 1)) <= NT) ++ntl;  // log2 NT: W <= NT for strided tiles
+    // relative launch costs (MI355X rocprof, `profiles/r02/`): register passes R <= 4 one
+    // unit (2^27: 268-280 us, 2^20: 4.5-5.2 us), R = 5 / 6 at 2^27 1.19 / 1.43; strided and
+    // two-segment tiles 1.5 (2^27: 404 us) / 1.45 (2^20: 7.3 us); the direct contiguous merge
+    // 1.35 (2^27: 360 us) / 1.55 (2^20: 7.8 us)
+    const bool large = mlog >= 23;
+    auto creg = [&](int R) { return R <= 4 ? 1.0 : (large ? (R == 5 ? 1.19 : 1.43) : 1.0); };
+    const double ctile = large ? 1.50 : 1.45, cmerge = large ? 1.35 : 1.55;
+    // steps: stage s (tlog < s <= mlog) has bits s-1 .. 0
+    std::vector<uint32_t> st, bt, first;  // stage, bit of step k; first step of stage s
+    first.assign(mlog + 2, 0);
+    for (uint32_t s = tlog + 1; s <= mlog; ++s) {
+        first[s] = (uint32_t)st.size();
+        for (int b = (int)s - 1; b >= 0; --b) st.push_back(s), bt.push_back((uint32_t)b);
+    }
+    const size_t N = st.size();
+    first[mlog + 1] = (uint32_t)N;
+    std::vector<double> best(N + 1, 1e30);
+    std::vector<NetPass> choice(N + 1);
+    std::vector<size_t> nxt(N + 1, N);
+    best[N] = 0.0;
+    for (size_t i = N; i-- > 0;) {
+        const uint32_t s = st[i], b = bt[i];
+        const size_t stage_end = first[s + 1];  // index after stage s's bit 0
+        auto consider = [&](size_t j, double c, const NetPass &p) {
+            if (j > N || best[j] >= 1e29) return;
+            if (c + best[j] < best[i] - 1e-9) {
+                best[i] = c + best[j];
+                choice[i] = p;
+                nxt[i] = j;
+            }
+        };
+        const bool last_stage = s == mlog;
+        // the last stage's steps below tlog belong to the final contiguous merge only
+        if (last_stage && b < tlog) {
+            if (b == tlog - 1) {
+                NetPass p;
+                p.ilogA = s; p.aTop = b; p.wlog = p.dtile = tlog; p.stage = s;
+                consider(N, cmerge, p);
+            }
+            continue;
+        }
+        // register pass: R steps b .. b-R+1 of stage s
+        for (int R = 1; R <= rmax && R <= (int)b + 1; ++R) {
+            if (last_stage && (int)b - R + 1 < (int)tlog) break;
+            NetPass p;
+            p.reg = true; p.ilog = s; p.jtop = b; p.R = (uint32_t)R; p.stage = s;
+            consider(i + (size_t)R, creg(R), p);
+        }
+        // tail of stage s alone (contiguous tile): steps b .. 0
+        if (!last_stage && b <= tlog - 1) {
+            NetPass p;
+            p.ilogA = s; p.aTop = b; p.wlog = p.dtile = tlog; p.stage = s;
+            consider(stage_end, b == tlog - 1 ? cmerge : ctile, p);
+        }
+        // middle of stage s (strided tile, low bits idle): steps b .. lo on the row bits
+        for (uint32_t rows = 1; rows <= b && rows < tlog; ++rows) {
+            const uint32_t lo = b - rows + 1, w = tlog - rows;
+            if (w < minw || w > ntl || lo < w) continue;
+            if (last_stage && lo < tlog) continue;
+            NetPass p;
+            p.ilogB = s; p.wlog = w; p.dtile = lo; p.stage = s;
+            consider(i + rows, ctile, p);
+        }
+        // tail of stage s (bits b..0, low bits) + head of stage s+1 (bits s .. lo, row bits)
+        if (s < mlog) {
+            for (uint32_t rows = 1; rows < tlog; ++rows) {
+                const uint32_t w = tlog - rows;
+                if (w < b + 1 || w < minw || w > ntl) continue;
+                if (rows > s) break;
+                const uint32_t lo = s - rows + 1;
+                if (lo < w) continue;
+                if (s + 1 == mlog && lo < tlog) continue;
+                NetPass p;
+                p.ilogA = s; p.aTop = b; p.ilogB = s + 1; p.wlog = w; p.dtile = lo; p.stage = s + 1;
+                consider(first[s + 1] + rows, ctile, p);
+            }
+        }
+    }
+    std::vector<NetPass> plan;
+    for (size_t i = 0; i < N;) {
+        if (best[i] >= 1e29) return {};  // no schedule (cannot happen for tlog >= 4): old path
+        plan.push_back(choice[i]);
+        i = nxt[i];
+    }
+    return plan;
+}
+
+static const std::vector<NetPass> &cached_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax) {
+    static std::mutex mu;
+    static std::map<uint64_t, std::vector<NetPass>> plans;
+    const uint64_t key = ((uint64_t)mlog << 40) | ((uint64_t)tlog << 32) | ((uint64_t)NT << 8) | (uint64_t)rmax;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = plans.find(key);
+    if (it == plans.end()) it = plans.emplace(key, plan_network(mlog, tlog, NT, rmax)).first;
+    return it->second;
+}
+
+// test hook: the plan as rows of 8 words {reg, ilog, jtop, R, ilogA, aTop, ilogB, wlog|dtile<<8}
+size_t debug_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax, uint32_t *out, size_t cap) {
+    const std::vector<NetPass> &plan = cached_plan(mlog, tlog, NT, rmax);
+    for (size_t k = 0; k < plan.size() && k < cap; ++k) {
+        const NetPass &p = plan[k];
+        const uint32_t row[8] = {p.reg ? 1u : 0u, p.ilog, p.jtop, p.R, p.ilogA, p.aTop, p.ilogB,
+                                 p.wlog | (p.dtile << 8)};
+        for (int q = 0; q < 8; ++q) out[k * 8 + q] = row[q];
+    }
+    return plan.size();
+}
+
+// stages tlog+1 .. mlog of a full sort by the planned launches (false: no plan, use stage_steps)
+template <int MODE>
+static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t seed, uint32_t pbase,
+                     hipStream_t s, const SelSink &sink, uint32_t valid, hipError_t &e) {
+    // the keyed shuffle (mode 2) keeps the per-stage schedule: its compare-exchanges cost
+    // more VALU (the hash multiply), which the planned tile-heavy schedule pays in LDS
+    // passes — C4: 10.15 vs 9.78 ms planned, against C5 (mode 0) 14.67 vs 15.34 ms and C3
+    // 0.157 vs 0.163 ms (`profiles/r02/ab/network_plan.jsonl`)
+    if (MODE == 2 || !plan_enabled() || c0.tlog <= 6 || mlog <= c0.tlog) return false;
+    const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
+    const int rmax = max_global_r() < rcap ? max_global_r() : rcap;
+    const std::vector<NetPass> &plan = cached_plan(mlog, c0.tlog, c0.NT, rmax);
+    if (plan.empty()) return false;
+    e = hipSuccess;
+    for (size_t k = 0; k < plan.size() && e == hipSuccess; ++k) {
+        const NetPass &p = plan[k];
+        const uint32_t skip = g_pad_skip ? skip_from(valid, p.stage, mlog) : 0u;
+        if (p.reg) {
+            e = launch_global<MODE>(data, mlog, p.ilog, p.jtop, (int)p.R, seed, s, pbase, skip >> p.R);
+            continue;
+        }
+        const TileCfg c = live_tiles(c0, skip);
+        if (p.ilogA && !p.ilogB && p.aTop == c0.tlog - 1)  // a whole contiguous merge
+            e = launch_tiles<MODE, false>(c, s, data, p.ilogA, c0.tlog, c0.tlog, seed, pbase,
+                                          k + 1 == plan.size() ? sink : SelSink{});
+        else
+            e = launch_tiles<MODE, false>(c, s, data, p.ilogB, p.wlog, p.dtile, seed, pbase, SelSink{},
+                                          p.ilogA ? ((p.ilogA << 8) | p.aTop) : 0u);
+    }
+    return true;
+}
+
 // Stages 1..slog of the network over m records at global positions pbase.. (pbase a
 // multiple of m; slog = log2 m: the full sort of this range, ascending where bit slog
 // of pbase is 0 and descending where it is 1 — the reference network's direction).
@@ -1080,6 +1269,7 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     e = launch_tiles<MODE, true>(live_tiles(c, skip_from(valid, c.tlog, mlog)), s, data, 0u, c.tlog,
                                  c.tlog, seed, pbase);
     if (e != hipSuccess) return e;
+    if (slog == mlog && run_plan<MODE>(data, mlog, c, seed, pbase, s, SelSink{}, valid, e)) return e;
     for (uint32_t ilog = c.tlog + 1; ilog <= slog; ++ilog) {
         e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, pbase, s, SelSink{}, valid);
         if (e != hipSuccess) return e;
@@ -1198,6 +1388,7 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, gp);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
+    if (run_plan<MODE>(data, mlog, c0, seed, 0u, s, sink, valid, e)) return e;
     for (uint32_t ilog = c0.tlog + 1; ilog <= mlog; ++ilog) {
         e = stage_steps<MODE>(data, mlog, c0, ilog, (int)ilog - 1, seed, 0u, s,
                               ilog == mlog ? sink : SelSink{}, valid);
