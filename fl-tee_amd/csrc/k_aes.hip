@@ -1,4 +1,4 @@
-// k_aes.hip — AES-128-CTR decrypt of the uploaded client slices (gfx950).
+// k_aes.hip — AES-128-CTR decrypt of the uploaded client slices (gfx950), constant time.
 //
 // lib.rs:312-343: each client's slice is decrypted with rsgx_aes_ctr_decrypt
 // under its session key (session_key_store.rs:17-32: 16 zero bytes with
@@ -7,87 +7,319 @@
 // plaintext is the record stream [u32 LE idx][f32 LE val] (parameters.rs:53-67),
 // which is also the in-HBM record layout: decrypt == parse.
 //
-// One lane per 16-byte block; T-tables (4 x 1 KB) and the S-box (1 KB) are
-// staged in LDS per workgroup; round keys (44 words per client) are expanded on
-// the host and read through L1.  Tables are generated at start-up from the
-// GF(2^8) definition of the S-box (FIPS-197 §5.1.1), not typed in.
+// The enclave's sgx_tcrypto runs AES-NI: no memory address depends on the key or the
+// data.  The kernel keeps that property by BITSLICING: state word s[r][i] holds bit i
+// of one state byte of 32 counter blocks at once, and the S-box is a boolean circuit
+// (aes_sbox_bs.h, generated and checked on all 256 inputs by scripts/gen_aes_sbox.py).
+// A quad of lanes carries 32 blocks, lane c the state's column c: ShiftRows is a DPP
+// quad_perm read of rows 1-3 from the neighbouring lanes, MixColumns XORs of planes,
+// AddRoundKey XORs with the key bits sign-extended from the round-key word of the
+// lane's column.  No table, no data-dependent branch or address.
+//
+// Quad g of a wave takes the counters W + g + 16 j (j = 0..31) of a 512-block window
+// W: bits 0-3 of the counter are g, bits 4-8 are j (constant planes), the rest W's, so
+// the counter planes cost nothing, and after one 32x32 bit transpose per lane, lane c of
+// quad g holds keystream word c of blocks W + 16 j + g: each of the 32 loads/stores of
+// the wave covers 256 B contiguously.
+//
+// The host key schedule and the CPU self-test block use the same circuit over 16-byte
+// bitsliced states (no S-box table on the host either).  The T-table kernel of round 1
+// (key- and data-dependent LDS addresses) stays as an opt-in A/B variant:
+// FLTEE_AES_TTABLE=1 (profiles/r02/ab/aes_variants.jsonl).
+#include <cstdlib>
 #include <mutex>
 
+#include "aes_sbox_bs.h"
 #include "common.h"
 
 namespace fltee {
 
-static uint8_t g_sbox[256];
-static uint32_t g_te[5][256];  // Te0..Te3, S-box widened (Te4)
-static std::once_flag g_tables_once;
-static uint32_t *g_dev_tables[64];  // per device
-static std::mutex g_dev_mu;
-
-static inline uint8_t xtime(uint8_t x) { return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0)); }
-static uint8_t gmul(uint8_t a, uint8_t b) {
-    uint8_t p = 0;
-    while (b) {
-        if (b & 1) p ^= a;
-        a = xtime(a);
-        b >>= 1;
-    }
-    return p;
+// ------------------------------------------------------------ bitsliced AES core
+// st[p][i]: bit i of state byte p (FIPS-197 column-major: p = 4 c + r) of every slice.
+// rk: the 44 big-endian round-key words.  Constant-time on host and device.
+__host__ __device__ __forceinline__ uint32_t key_plane(uint32_t w, int bit) {
+    return 0u - ((w >> bit) & 1u);
 }
-static inline uint8_t rotl8(uint8_t x, int s) { return (uint8_t)((x << s) | (x >> (8 - s))); }
-static inline uint32_t rotr32(uint32_t x, int s) { return (x >> s) | (x << (32 - s)); }
 
-static void build_tables() {
-    for (int x = 0; x < 256; ++x) {
-        uint8_t inv = 0;
-        if (x) {  // x^254 = x^-1 in GF(2^8)
-            uint8_t r = 1, b = (uint8_t)x;
-            int e = 254;
-            while (e) {
-                if (e & 1) r = gmul(r, b);
-                b = gmul(b, b);
-                e >>= 1;
+template <bool FOLD63>
+__host__ __device__ __forceinline__ void add_round_key_bs(uint32_t st[16][8], const uint32_t *rk) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        // the S-box circuit leaves out its 0x63; MixColumns and ShiftRows map the
+        // all-0x63 state to itself, so the constant joins every later round key
+        const uint32_t w = FOLD63 ? rk[c] ^ 0x63636363u : rk[c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st[4 * c + r][i] ^= key_plane(w, 24 - 8 * r + i);
+    }
+}
+
+// SubBytes, ShiftRows, MixColumns (MIX) into ns
+template <bool MIX>
+__host__ __device__ __forceinline__ void round_bs(uint32_t st[16][8], uint32_t ns[16][8]) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) aes_sbox_bs(st[p]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        // ShiftRows: row r of column c comes from column c + r
+        const int q0 = 4 * ((c + 0) & 3) + 0, q1 = 4 * ((c + 1) & 3) + 1,
+                  q2 = 4 * ((c + 2) & 3) + 2, q3 = 4 * ((c + 3) & 3) + 3;
+        if (!MIX) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                ns[4 * c + 0][i] = st[q0][i];
+                ns[4 * c + 1][i] = st[q1][i];
+                ns[4 * c + 2][i] = st[q2][i];
+                ns[4 * c + 3][i] = st[q3][i];
             }
-            inv = r;
+            continue;
         }
-        g_sbox[x] = (uint8_t)(inv ^ rotl8(inv, 1) ^ rotl8(inv, 2) ^ rotl8(inv, 3) ^ rotl8(inv, 4) ^ 0x63);
+        const int q[4] = {q0, q1, q2, q3};
+        uint32_t t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = st[q0][i] ^ st[q1][i] ^ st[q2][i] ^ st[q3][i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            // out_r = a_r ^ t ^ xtime(a_r ^ a_{r+1})  (2 a_r ^ 3 a_{r+1} ^ a_{r+2} ^ a_{r+3})
+            uint32_t u[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) u[i] = st[q[r]][i] ^ st[q[(r + 1) & 3]][i];
+            const uint32_t x[8] = {u[7], u[0] ^ u[7], u[1], u[2] ^ u[7], u[3] ^ u[7], u[4], u[5], u[6]};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ns[4 * c + r][i] = st[q[r]][i] ^ t[i] ^ x[i];
+        }
     }
-    for (int x = 0; x < 256; ++x) {
-        const uint8_t s = g_sbox[x];
-        const uint32_t t = ((uint32_t)gmul(s, 2) << 24) | ((uint32_t)s << 16) | ((uint32_t)s << 8) |
-                           (uint32_t)gmul(s, 3);
-        g_te[0][x] = t;
-        g_te[1][x] = rotr32(t, 8);
-        g_te[2][x] = rotr32(t, 16);
-        g_te[3][x] = rotr32(t, 24);
-        g_te[4][x] = s;
+}
+
+// The ten rounds after the input's AddRoundKey.
+__host__ __device__ __forceinline__ void aes128_rounds_bs(uint32_t st[16][8], const uint32_t *rk) {
+#pragma unroll 1
+    for (int R = 1; R < 10; ++R) {
+        uint32_t ns[16][8];
+        round_bs<true>(st, ns);
+        add_round_key_bs<true>(ns, rk + 4 * R);
+#pragma unroll
+        for (int p = 0; p < 16; ++p)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st[p][i] = ns[p][i];
     }
+    uint32_t ns[16][8];
+    round_bs<false>(st, ns);
+    add_round_key_bs<true>(ns, rk + 40);
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[p][i] = ns[p][i];
+}
+
+// SubWord of the key schedule: the four bytes as bit positions 0..3 of the planes.
+static uint32_t sub_word_bs(uint32_t t) {
+    uint32_t x[8];
+    for (int i = 0; i < 8; ++i) {
+        x[i] = 0;
+        for (int q = 0; q < 4; ++q) x[i] |= ((t >> (8 * q + i)) & 1u) << q;
+    }
+    aes_sbox_bs(x);
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i)
+        for (int q = 0; q < 4; ++q) r |= ((x[i] >> q) & 1u) << (8 * q + i);
+    return r ^ 0x63636363u;
 }
 
 void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]) {
-    std::call_once(g_tables_once, build_tables);
     for (int i = 0; i < 4; ++i)
         rk[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
                 ((uint32_t)key[4 * i + 2] << 8) | key[4 * i + 3];
-    uint8_t rc = 1;
+    uint32_t rc = 1;
     for (int i = 4; i < 44; ++i) {
         uint32_t t = rk[i - 1];
-        if (i % 4 == 0) {
-            t = (t << 8) | (t >> 24);  // RotWord
-            t = ((uint32_t)g_sbox[t >> 24] << 24) | ((uint32_t)g_sbox[(t >> 16) & 0xff] << 16) |
-                ((uint32_t)g_sbox[(t >> 8) & 0xff] << 8) | g_sbox[t & 0xff];
-            t ^= (uint32_t)rc << 24;
-            rc = xtime(rc);
+        if (i % 4 == 0) {  // public schedule position, not a secret
+            t = sub_word_bs((t << 8) | (t >> 24)) ^ (rc << 24);
+            rc = ((rc << 1) ^ (0x11bu & (0u - (rc >> 7)))) & 0xffu;
         }
         rk[i] = rk[i - 4] ^ t;
     }
 }
 
-// One AES-128 block encryption, big-endian word state (FIPS-197 / T-table form).
-__host__ __device__ __forceinline__ void aes128_block(const uint32_t *T0, const uint32_t *T1,
-                                                      const uint32_t *T2, const uint32_t *T3,
-                                                      const uint32_t *S, const uint32_t *rk,
-                                                      uint32_t s0, uint32_t s1, uint32_t s2,
-                                                      uint32_t s3, uint32_t out[4]) {
+// host-side single block, for the CPU self-test (no GPU needed): slice 0 of the planes
+void aes128_encrypt_block_host(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+    uint32_t rk[44];
+    aes128_expand_key(key, rk);
+    uint32_t st[16][8];
+    for (int p = 0; p < 16; ++p)
+        for (int i = 0; i < 8; ++i) st[p][i] = (in[p] >> i) & 1u;
+    add_round_key_bs<false>(st, rk);
+    aes128_rounds_bs(st, rk);
+    for (int p = 0; p < 16; ++p) {
+        uint32_t b = 0;
+        for (int i = 0; i < 8; ++i) b |= (st[p][i] & 1u) << i;
+        out[p] = (uint8_t)b;
+    }
+}
+
+// ------------------------------------------------------------- bitsliced kernel
+__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// In-place 32x32 bit transpose: afterwards m[j] bit r = (old m[r]) bit j.
+__device__ __forceinline__ void transpose32(uint32_t m[32]) {
+    constexpr uint32_t kMask[5] = {0x0000ffffu, 0x00ff00ffu, 0x0f0f0f0fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        const int s = 16 >> l;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            if (r & s) continue;
+            const uint32_t t = ((m[r] >> s) ^ m[r + s]) & kMask[l];
+            m[r + s] ^= t;
+            m[r] ^= t << s;
+        }
+    }
+}
+
+// ------------------------------------------------ column-per-lane bitsliced kernel
+// A quad of lanes holds 32 blocks: lane c of the quad keeps column c of the state (rows
+// 0-3, 32 planes), ShiftRows reads rows 1-3 from the lanes c+1..c+3 of the quad (DPP
+// quad_perm, no LDS), SubBytes and MixColumns stay in the lane.  127 VGPRs (4 waves per
+// SIMD).  A/B: one lane per 32 blocks with the whole state (452 VGPRs, one wave per
+// SIMD) ran 2.04 ms on the 800 MB headline payload and this form 1.39 ms.
+constexpr int kAesWindow4 = 512;  // counter blocks per wave: 16 quads x 32 slices
+
+__device__ __forceinline__ uint32_t quad_rot(uint32_t v, int r) {
+    // lane c of each quad reads lane (c + r) & 3
+    switch (r) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xf, 0xf, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);
+    case 3: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xf, 0xf, false);
+    default: return v;
+    }
+}
+
+__device__ __forceinline__ uint32_t sext_bit(uint32_t w, int pos) {
+    return (uint32_t)((int32_t)(w << (31 - pos)) >> 31);  // v_bfe_i32 w, pos, 1
+}
+
+template <bool MIX>
+__device__ __forceinline__ void round_col(uint32_t s[4][8]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) aes_sbox_bs(s[r]);
+#pragma unroll
+    for (int r = 1; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[r][i] = quad_rot(s[r][i], r);
+    if (!MIX) return;
+    uint32_t t[8], ns[4][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = s[0][i] ^ s[1][i] ^ s[2][i] ^ s[3][i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint32_t u[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) u[i] = s[r][i] ^ s[(r + 1) & 3][i];
+        const uint32_t x[8] = {u[7], u[0] ^ u[7], u[1], u[2] ^ u[7], u[3] ^ u[7], u[4], u[5], u[6]};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ns[r][i] = s[r][i] ^ t[i] ^ x[i];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[r][i] = ns[r][i];
+}
+
+__device__ __forceinline__ void ark_col(uint32_t s[4][8], uint32_t w) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[r][i] ^= sext_bit(w, 24 - 8 * r + i);
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restrict__ cipher,
+                                                          size_t n, size_t bpc, size_t rpc,
+                                                          const uint32_t *__restrict__ rks,
+                                                          uint8_t *__restrict__ plain,
+                                                          uint64_t block_off, uint32_t idx_sub,
+                                                          uint64_t wpc) {
+    const uint32_t lane = threadIdx.x & 63, col = lane & 3, g = lane >> 2;
+    const uint64_t bpcl = (rpc + 1) / 2;  // 16-byte blocks per client
+    const uint64_t waves = (uint64_t)n * wpc;
+    const uint64_t w0 = block_off / kAesWindow4;
+    for (uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gw < waves;
+         gw += (uint64_t)gridDim.x * 4) {
+        const uint64_t gu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gw >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)gw);
+        const uint64_t c = gu / wpc;
+        const uint64_t W = (w0 + (gu - c * wpc)) * kAesWindow4;
+        const uint32_t *rk = rks + c * 44 + col;  // this lane's column of every round key
+        const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
+        // counter block BE128(W + g + 16 j): column 3 = counter bits 0-31, column 2 =
+        // bits 32-63, columns 0-1 zero; bits 0-3 = g, 4-8 = j, the rest W's
+        uint32_t s[4][8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int t = 24 - 8 * r + i;
+                const uint32_t v3 = t < 4 ? 0u - ((g >> t) & 1u)
+                                  : t < 9 ? (t == 4 ? 0xaaaaaaaau : t == 5 ? 0xccccccccu
+                                             : t == 6 ? 0xf0f0f0f0u : t == 7 ? 0xff00ff00u : 0xffff0000u)
+                                          : 0u - ((wlo >> t) & 1u);
+                const uint32_t v2 = 0u - ((whi >> t) & 1u);
+                s[r][i] = col == 3 ? v3 : col == 2 ? v2 : 0u;
+            }
+        ark_col(s, rk[0]);
+#pragma unroll 1
+        for (int R = 1; R < 10; ++R) {
+            const uint32_t w = rk[4 * R] ^ 0x63636363u;  // the S-boxes' 0x63, folded
+            round_col<true>(s);
+            ark_col(s, w);
+        }
+        round_col<false>(s);
+        ark_col(s, rk[40] ^ 0x63636363u);
+        // rows 8 r + i -> word j = keystream word `col` of block j
+        transpose32(&s[0][0]);
+        const uint8_t *cbase = cipher + c * bpc + 4 * col;
+        uint8_t *dbase = plain + c * rpc * 8 + 4 * col;
+        const uint32_t sub = (col & 1) ? 0u : idx_sub;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint64_t ctr = W + 16 * j + g;
+            if (ctr < block_off || ctr - block_off >= bpcl) continue;
+            const uint64_t b = ctr - block_off;
+            if (2 * b + (col >> 1) >= rpc) continue;  // the half last block
+            const uint32_t x = ALIGNED ? *reinterpret_cast<const uint32_t *>(cbase + 16 * b)
+                                       : ld_u32_bytes(cbase + 16 * b);
+            *reinterpret_cast<uint32_t *>(dbase + 16 * b) = (x ^ (&s[0][0])[j]) - sub;
+        }
+    }
+}
+
+// ------------------------------------------------- T-table kernel (A/B variant only)
+static uint32_t g_te[5][256];  // Te0..Te3, S-box widened (Te4)
+static std::once_flag g_tables_once;
+static uint32_t *g_dev_tables[64];  // per device
+static std::mutex g_dev_mu;
+
+static void build_tables() {
+    for (int x = 0; x < 256; ++x) {
+        const uint8_t s = (uint8_t)(sub_word_bs((uint32_t)x) & 0xff);
+        const uint8_t s2 = (uint8_t)((s << 1) ^ ((s & 0x80) ? 0x1b : 0));
+        const uint32_t t = ((uint32_t)s2 << 24) | ((uint32_t)s << 16) | ((uint32_t)s << 8) |
+                           (uint32_t)(s2 ^ s);
+        g_te[0][x] = t;
+        g_te[1][x] = (t >> 8) | (t << 24);
+        g_te[2][x] = (t >> 16) | (t << 16);
+        g_te[3][x] = (t >> 24) | (t << 8);
+        g_te[4][x] = s;
+    }
+}
+
+__device__ __forceinline__ void aes128_block_tt(const uint32_t *T, const uint32_t *rk, uint32_t s0,
+                                                uint32_t s1, uint32_t s2, uint32_t s3,
+                                                uint32_t out[4]) {
+    const uint32_t *T0 = T, *T1 = T + 256, *T2 = T + 512, *T3 = T + 768, *S = T + 1024;
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
@@ -103,39 +335,24 @@ __host__ __device__ __forceinline__ void aes128_block(const uint32_t *T0, const 
     out[3] = ((S[s3 >> 24] << 24) | (S[(s0 >> 16) & 0xff] << 16) | (S[(s1 >> 8) & 0xff] << 8) | S[s2 & 0xff]) ^ rk[43];
 }
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-// lane -> (client c, block b); blocks_per_client = ceil(rec_per_client * 8 / 16).
-// ALIGNED: every slice starts on an 8-byte boundary (bpc % 8 == 0, the unchanged
-// client).  Otherwise (enc_len % n != 0: lib.rs:305 floors bpc, so slice i starts
-// at i*bpc) the ciphertext is read byte by byte; the output stays compact records.
-__device__ __forceinline__ uint32_t ld_u32_bytes(const uint8_t *p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// block_off: the slices are the bytes [16 * block_off, ...) of each client's payload (a
-// column slice of dense uploads, one GPU's parameter range): counter block b + block_off.
-// idx_sub is subtracted from every record's idx (the slice's first parameter), so that
-// the dense kernels' idx == position check runs on slice-local positions.
 template <bool ALIGNED>
-__global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict__ cipher,
-                                                      size_t n, size_t bpc, size_t rpc,
-                                                      const uint32_t *__restrict__ rks,
-                                                      const uint32_t *__restrict__ tables,
-                                                      uint8_t *__restrict__ plain,
-                                                      uint64_t block_off, uint32_t idx_sub) {
+__global__ __launch_bounds__(256) void aes_ctr_tt_kernel(const uint8_t *__restrict__ cipher,
+                                                         size_t n, size_t bpc, size_t rpc,
+                                                         const uint32_t *__restrict__ rks,
+                                                         const uint32_t *__restrict__ tables,
+                                                         uint8_t *__restrict__ plain,
+                                                         uint64_t block_off, uint32_t idx_sub) {
     __shared__ uint32_t T[5 * 256];
     for (uint32_t e = threadIdx.x; e < 5 * 256; e += 256) T[e] = tables[e];
     __syncthreads();
-    const size_t bpcl = (rpc + 1) / 2;  // 16-byte blocks per client
+    const size_t bpcl = (rpc + 1) / 2;
     const size_t total = n * bpcl;
     for (size_t g = (size_t)blockIdx.x * 256 + threadIdx.x; g < total;
          g += (size_t)gridDim.x * 256) {
         const size_t c = g / bpcl, b = g - c * bpcl;
         const uint64_t ctr = (uint64_t)b + block_off;
         uint32_t ks[4];
-        aes128_block(T, T + 256, T + 512, T + 768, T + 1024, rks + c * 44, 0u, 0u,
-                     (uint32_t)(ctr >> 32), (uint32_t)ctr, ks);
+        aes128_block_tt(T, rks + c * 44, 0u, 0u, (uint32_t)(ctr >> 32), (uint32_t)ctr, ks);
         uint2 *dst = reinterpret_cast<uint2 *>(plain + c * rpc * 8) + 2 * b;
         const bool two = 2 * b + 1 < rpc;
         uint2 x, y = make_uint2(0, 0);
@@ -148,12 +365,12 @@ __global__ __launch_bounds__(256) void aes_ctr_kernel(const uint8_t *__restrict_
             x = make_uint2(ld_u32_bytes(src), ld_u32_bytes(src + 4));
             if (two) y = make_uint2(ld_u32_bytes(src + 8), ld_u32_bytes(src + 12));
         }
-        dst[0] = make_uint2((x.x ^ bswap32(ks[0])) - idx_sub, x.y ^ bswap32(ks[1]));
-        if (two) dst[1] = make_uint2((y.x ^ bswap32(ks[2])) - idx_sub, y.y ^ bswap32(ks[3]));
+        dst[0] = make_uint2((x.x ^ __builtin_bswap32(ks[0])) - idx_sub, x.y ^ __builtin_bswap32(ks[1]));
+        if (two) dst[1] = make_uint2((y.x ^ __builtin_bswap32(ks[2])) - idx_sub, y.y ^ __builtin_bswap32(ks[3]));
     }
 }
 
-static uint32_t *device_tables(hipStream_t s) {
+static uint32_t *device_tables() {
     std::call_once(g_tables_once, build_tables);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
@@ -164,27 +381,51 @@ static uint32_t *device_tables(hipStream_t s) {
         if (hipMemcpy(p, g_te, sizeof(g_te), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
         g_dev_tables[dev] = p;
     }
-    (void)s;
     return g_dev_tables[dev];
+}
+
+static bool ttable_variant() {
+    static const bool on = [] {
+        const char *e = getenv("FLTEE_AES_TTABLE");
+        return e && atoi(e) != 0;
+    }();
+    return on;
 }
 
 hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                                 size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
                                 uint64_t block_off, uint32_t idx_sub, hipStream_t s) {
-    const size_t total = n * ((rec_per_client + 1) / 2);
-    if (total == 0) return hipSuccess;
-    uint32_t *tables = device_tables(s);
-    if (!tables) return hipErrorOutOfMemory;
-    size_t blocks = (total + 255) / 256;
-    if (blocks > 16384) blocks = 16384;
-    if (bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0)
-        hipLaunchKernelGGL(aes_ctr_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, cipher, n,
-                           bytes_per_client, rec_per_client, round_keys, tables, plain, block_off,
-                           idx_sub);
+    const size_t bpcl = (rec_per_client + 1) / 2;
+    if (n == 0 || bpcl == 0) return hipSuccess;
+    const bool aligned = bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0;
+    if (ttable_variant()) {
+        uint32_t *tables = device_tables();
+        if (!tables) return hipErrorOutOfMemory;
+        size_t blocks = (n * bpcl + 255) / 256;
+        if (blocks > 16384) blocks = 16384;
+        if (aligned)
+            hipLaunchKernelGGL(aes_ctr_tt_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
+                               cipher, n, bytes_per_client, rec_per_client, round_keys, tables,
+                               plain, block_off, idx_sub);
+        else
+            hipLaunchKernelGGL(aes_ctr_tt_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
+                               cipher, n, bytes_per_client, rec_per_client, round_keys, tables,
+                               plain, block_off, idx_sub);
+        return hipGetLastError();
+    }
+    // windows of 512 counter blocks (absolute counter space) touching each client's slice
+    const uint64_t wpc = (block_off + bpcl - 1) / kAesWindow4 - block_off / kAesWindow4 + 1;
+    const uint64_t waves = (uint64_t)n * wpc;
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 16384) blocks = 16384;  // grid-stride beyond 16 waves per SIMD
+    if (aligned)
+        hipLaunchKernelGGL(aes_ctr_bs4_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
+                           cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
+                           block_off, idx_sub, wpc);
     else
-        hipLaunchKernelGGL(aes_ctr_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, cipher,
-                           n, bytes_per_client, rec_per_client, round_keys, tables, plain,
-                           block_off, idx_sub);
+        hipLaunchKernelGGL(aes_ctr_bs4_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
+                           cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
+                           block_off, idx_sub, wpc);
     return hipGetLastError();
 }
 
@@ -193,23 +434,6 @@ hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_clie
                           hipStream_t s) {
     return launch_aes_ctr_slice(cipher, n, bytes_per_client, rec_per_client, round_keys, plain, 0,
                                 0, s);
-}
-
-// host-side single block, for the CPU self-test (no GPU needed)
-void aes128_encrypt_block_host(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
-    uint32_t rk[44], o[4];
-    aes128_expand_key(key, rk);
-    uint32_t w[4];
-    for (int i = 0; i < 4; ++i)
-        w[i] = ((uint32_t)in[4 * i] << 24) | ((uint32_t)in[4 * i + 1] << 16) |
-               ((uint32_t)in[4 * i + 2] << 8) | in[4 * i + 3];
-    aes128_block(g_te[0], g_te[1], g_te[2], g_te[3], g_te[4], rk, w[0], w[1], w[2], w[3], o);
-    for (int i = 0; i < 4; ++i) {
-        out[4 * i] = (uint8_t)(o[i] >> 24);
-        out[4 * i + 1] = (uint8_t)(o[i] >> 16);
-        out[4 * i + 2] = (uint8_t)(o[i] >> 8);
-        out[4 * i + 3] = (uint8_t)o[i];
-    }
 }
 
 }  // namespace fltee

@@ -662,6 +662,29 @@ def test_gpu_decrypt_reference_client_payloads(dev, name):
     assert out.cpu().numpy().tobytes() == fx["plaintext"].tobytes()
 
 
+# The bitsliced kernel takes 2048-block counter windows per wave (64 lanes x 32 slices):
+# slices shorter than a window, ending one record into a window, a half last block (odd
+# record count), several clients per window row, unaligned slices (bpc % 8 != 0) and
+# 32-bit client ids.
+@pytest.mark.parametrize("n,bpc", [(1, 8), (3, 24), (2, 16 * 2048), (2, 16 * 2048 + 8),
+                                   (5, 16 * 2048 * 2 - 8), (7, 40712), (4, 8 * 5089 + 3),
+                                   (3, 16 * 4096 + 13)])
+def test_gpu_decrypt_bitsliced_windows(dev, oracle, n, bpc):
+    import torch
+    rng = np.random.default_rng(bpc * 31 + n)
+    ids = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    ids[0] = 0xFFFFFFFF
+    ct = rng.integers(0, 256, n * bpc, dtype=np.uint8)
+    rpc = bpc // 8
+    want = b"".join(oracle.aes128_ctr(oracle.session_key(int(ids[c])),
+                                      ct[c * bpc:(c + 1) * bpc].tobytes())[:rpc * 8]
+                    for c in range(n))
+    out = torch.full((n * rpc,), -1, dtype=torch.int64, device="cuda")
+    dev.decrypt(ids, torch.from_numpy(ct).cuda(), bpc, out)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == want
+
+
 # ------------------------------------------------------- full size NS ------
 def test_headline_shape_100x1M_bit_exact(dev):
     import torch
