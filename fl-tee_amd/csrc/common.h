@@ -185,6 +185,8 @@ hipError_t launch_apply_clip(void *rec, size_t n, size_t k, const float *coef, h
 
 // k_aes.hip
 void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
+// the round keys of the n clients' session keys (constant time, 8 keys per circuit pass)
+void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk);
 hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                           size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
                           hipStream_t s);

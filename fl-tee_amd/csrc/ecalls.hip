@@ -112,14 +112,7 @@ static uint32_t check_uploaded(const FLConfig &cfg, const uint32_t *ids, size_t 
 // AES-128 round keys of the n clients' session keys (session_key_store.rs:21-22)
 static void client_round_keys(const uint32_t *ids, size_t n, std::vector<uint32_t> &rk) {
     rk.resize(n * 44);
-    for (size_t i = 0; i < n; ++i) {
-        uint8_t key[16] = {0};
-        key[4] = (uint8_t)(ids[i] >> 24);
-        key[5] = (uint8_t)(ids[i] >> 16);
-        key[6] = (uint8_t)(ids[i] >> 8);
-        key[7] = (uint8_t)ids[i];
-        aes128_expand_key(key, &rk[i * 44]);
-    }
+    aes128_session_round_keys(ids, n, rk.data());
 }
 
 // H2D + GPU AES-CTR decrypt of n slices of bpc bytes -> c->records (n * (bpc/8) records)
@@ -529,14 +522,7 @@ static fltee_status_t aes_ctr_device(const uint32_t *client_ids, size_t n, const
     if (!c) return FLTEE_ERROR_INVALID_PARAMETER;
     if (!c->round_keys.reserve(n * 44 * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
     std::vector<uint32_t> rk(n * 44);
-    for (size_t i = 0; i < n; ++i) {
-        uint8_t key[16] = {0};
-        key[4] = (uint8_t)(client_ids[i] >> 24);
-        key[5] = (uint8_t)(client_ids[i] >> 16);
-        key[6] = (uint8_t)(client_ids[i] >> 8);
-        key[7] = (uint8_t)client_ids[i];
-        aes128_expand_key(key, &rk[i * 44]);
-    }
+    aes128_session_round_keys(client_ids, n, rk.data());
     if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     if (launch_aes_ctr((const uint8_t *)d_in, n, bytes_per_client, bytes_per_client / 8,

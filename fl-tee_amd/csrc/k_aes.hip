@@ -113,33 +113,62 @@ __host__ __device__ __forceinline__ void aes128_rounds_bs(uint32_t st[16][8], co
         for (int i = 0; i < 8; ++i) st[p][i] = ns[p][i];
 }
 
-// SubWord of the key schedule: the four bytes as bit positions 0..3 of the planes.
-static uint32_t sub_word_bs(uint32_t t) {
+// The key schedule of up to 8 keys at once: SubWord's 4 bytes of key k are the slices
+// 4 k .. 4 k + 3 of the planes (the AND/XOR form of the same S-box circuit).
+static void expand_keys8(const uint8_t (*key)[16], int nk, uint32_t *rk) {
+    for (int k = 0; k < nk; ++k)
+        for (int i = 0; i < 4; ++i)
+            rk[44 * k + i] = ((uint32_t)key[k][4 * i] << 24) | ((uint32_t)key[k][4 * i + 1] << 16) |
+                             ((uint32_t)key[k][4 * i + 2] << 8) | key[k][4 * i + 3];
+    uint32_t rc = 1;
+    for (int i = 4; i < 44; ++i) {
+        if (i % 4) {
+            for (int k = 0; k < nk; ++k) rk[44 * k + i] = rk[44 * k + i - 4] ^ rk[44 * k + i - 1];
+            continue;
+        }
+        uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < nk; ++k) {
+            const uint32_t t = rk[44 * k + i - 1], rot = (t << 8) | (t >> 24);  // RotWord
+            for (int b = 0; b < 8; ++b)
+                for (int q = 0; q < 4; ++q) x[b] |= ((rot >> (8 * q + b)) & 1u) << (4 * k + q);
+        }
+        aes_sbox_gates(x);
+        for (int k = 0; k < nk; ++k) {
+            uint32_t sw = 0;
+            for (int b = 0; b < 8; ++b)
+                for (int q = 0; q < 4; ++q) sw |= ((x[b] >> (4 * k + q)) & 1u) << (8 * q + b);
+            rk[44 * k + i] = rk[44 * k + i - 4] ^ sw ^ 0x63636363u ^ (rc << 24);
+        }
+        rc = ((rc << 1) ^ (0x11bu & (0u - (rc >> 7)))) & 0xffu;  // public schedule
+    }
+}
+
+void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]) {
+    expand_keys8(reinterpret_cast<const uint8_t (*)[16]>(key), 1, rk);
+}
+
+// session_key_store.rs:17-32: 16 zero bytes with bytes[4..8] = client_id big-endian
+void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk) {
+    for (size_t c0 = 0; c0 < n; c0 += 8) {
+        const int nk = (int)(n - c0 < 8 ? n - c0 : 8);
+        uint8_t key[8][16] = {};
+        for (int k = 0; k < nk; ++k)
+            for (int b = 0; b < 4; ++b) key[k][4 + b] = (uint8_t)(ids[c0 + k] >> (24 - 8 * b));
+        expand_keys8(key, nk, rk + 44 * c0);
+    }
+}
+
+static uint32_t sub_word_bs(uint32_t t) {  // S-box of each byte of t (T-table build)
     uint32_t x[8];
     for (int i = 0; i < 8; ++i) {
         x[i] = 0;
         for (int q = 0; q < 4; ++q) x[i] |= ((t >> (8 * q + i)) & 1u) << q;
     }
-    aes_sbox_bs(x);
+    aes_sbox_gates(x);
     uint32_t r = 0;
     for (int i = 0; i < 8; ++i)
         for (int q = 0; q < 4; ++q) r |= ((x[i] >> q) & 1u) << (8 * q + i);
     return r ^ 0x63636363u;
-}
-
-void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]) {
-    for (int i = 0; i < 4; ++i)
-        rk[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
-                ((uint32_t)key[4 * i + 2] << 8) | key[4 * i + 3];
-    uint32_t rc = 1;
-    for (int i = 4; i < 44; ++i) {
-        uint32_t t = rk[i - 1];
-        if (i % 4 == 0) {  // public schedule position, not a secret
-            t = sub_word_bs((t << 8) | (t >> 24)) ^ (rc << 24);
-            rc = ((rc << 1) ^ (0x11bu & (0u - (rc >> 7)))) & 0xffu;
-        }
-        rk[i] = rk[i - 4] ^ t;
-    }
 }
 
 // host-side single block, for the CPU self-test (no GPU needed): slice 0 of the planes
@@ -182,9 +211,11 @@ __device__ __forceinline__ void transpose32(uint32_t m[32]) {
 // ------------------------------------------------ column-per-lane bitsliced kernel
 // A quad of lanes holds 32 blocks: lane c of the quad keeps column c of the state (rows
 // 0-3, 32 planes), ShiftRows reads rows 1-3 from the lanes c+1..c+3 of the quad (DPP
-// quad_perm, no LDS), SubBytes and MixColumns stay in the lane.  127 VGPRs (4 waves per
-// SIMD).  A/B: one lane per 32 blocks with the whole state (452 VGPRs, one wave per
-// SIMD) ran 2.04 ms on the 800 MB headline payload and this form 1.39 ms.
+// quad_perm, no LDS), SubBytes and MixColumns stay in the lane.  96 VGPRs (5 waves per
+// SIMD).  A/B (profiles/r02/ab/aes_variants.jsonl): one lane per 32 blocks with the
+// whole state (452 VGPRs, one wave per SIMD) ran 2.04 ms on the 800 MB headline payload
+// and this form 1.39 ms with two-input gates, 1.19 ms with the S-box as 119 bitop3s
+// (the T-table kernel: 1.21 ms).
 constexpr int kAesWindow4 = 512;  // counter blocks per wave: 16 quads x 32 slices
 
 __device__ __forceinline__ uint32_t quad_rot(uint32_t v, int r) {

@@ -281,6 +281,136 @@ def build(mu, lam, beta):
     return C, wires
 
 
+
+# ------------------------------------------------------------ 3-input LUT mapping
+# gfx950's v_bitop3_b32 evaluates any boolean function of three 32-bit operands in one
+# instruction (the 8-bit truth table is an immediate).  Covering the AND/XOR circuit
+# with 3-input cuts (area flow, then exact-area recovery, as FPGA LUT mappers do) turns
+# it into the fewest such instructions.
+def lut_map(gates, outputs, K=3):
+    op = {w: (o, a, b) for o, w, a, b in gates}
+    order = [w for _, w, _, _ in gates]
+    is_pi = lambda w: w not in op
+    cuts = {}
+
+    def cuts_of(w):
+        if w in cuts:
+            return cuts[w]
+        if is_pi(w):
+            cuts[w] = [frozenset([w])]
+            return cuts[w]
+        _, a, b = op[w]
+        cs = set()
+        for c1 in cuts_of(a):
+            for c2 in cuts_of(b):
+                u = c1 | c2
+                if len(u) <= K:
+                    cs.add(u)
+        cs = [c for c in cs if not any(o < c for o in cs)]  # drop dominated cuts
+        cuts[w] = cs + [frozenset([w])]
+        return cuts[w]
+
+    for w in order:
+        cuts_of(w)
+    fanout = {w: 0 for w in list(op) + list(range(8))}
+    for w in order:
+        _, a, b = op[w]
+        fanout[a] += 1
+        fanout[b] += 1
+    for w in outputs:
+        fanout[w] += 1
+    af, best = {}, {}
+    for w in range(8):
+        af[w] = 0.0
+    for w in order:
+        opts = [c for c in cuts[w] if c != frozenset([w])]
+        scored = [(1 + sum(af[l] / max(1, fanout[l]) for l in c), len(c), sorted(c), c) for c in opts]
+        scored.sort(key=lambda t: (t[0], t[1], t[2]))
+        af[w], best[w] = scored[0][0], scored[0][3]
+    ref = {w: 0 for w in fanout}
+
+    def do_ref(w):
+        a = 1
+        for l in best[w]:
+            if not is_pi(l):
+                if ref[l] == 0:
+                    a += do_ref(l)
+            ref[l] += 1
+        return a
+
+    def do_deref(w):
+        a = 1
+        for l in best[w]:
+            ref[l] -= 1
+            if not is_pi(l) and ref[l] == 0:
+                a += do_deref(l)
+        return a
+
+    for w in outputs:
+        if not is_pi(w):
+            if ref[w] == 0:
+                do_ref(w)
+        ref[w] += 1
+    for _ in range(3):  # exact-area recovery
+        for w in order:
+            if ref[w] == 0:
+                continue
+            do_deref(w)
+            cand = []
+            for c in cuts[w]:
+                if c == frozenset([w]):
+                    continue
+                best[w] = c
+                a = do_ref(w)
+                do_deref(w)
+                cand.append((a, len(c), sorted(c), c))
+            cand.sort(key=lambda t: (t[0], t[1], t[2]))
+            best[w] = cand[0][3]
+            do_ref(w)
+    mapped = [w for w in order if ref[w] > 0]
+
+    def tt(w, leaves):
+        """Truth table of w over its cut leaves (leaf 0 the most significant variable)."""
+        pat = {l: p for l, p in zip(leaves, (0xF0, 0xCC, 0xAA))}
+        memo = {}
+
+        def ev(x):
+            if x in pat:
+                return pat[x]
+            if x in memo:
+                return memo[x]
+            o, a, b = op[x]
+            v = ev(a) ^ ev(b) if o == "^" else ev(a) & ev(b)
+            memo[x] = v
+            return v
+
+        return ev(w) & 0xFF
+
+    luts = []
+    for w in mapped:
+        leaves = sorted(best[w])
+        luts.append((w, leaves, tt(w, leaves)))
+    return luts
+
+
+def check_luts(luts, outputs, S):
+    val = {i: sum(((x >> i) & 1) << x for x in range(256)) for i in range(8)}
+    full = (1 << 256) - 1
+    for w, leaves, imm in luts:
+        ops = [val[l] for l in leaves] + [val[leaves[0]]] * (3 - len(leaves))
+        r = 0
+        for m in range(8):
+            if (imm >> m) & 1:
+                t = full
+                for k, v in enumerate(ops):
+                    t &= v if (m >> (2 - k)) & 1 else full ^ v
+                r |= t
+        val[w] = r
+    for j in range(8):
+        want = sum((((S[x] ^ 0x63) >> j) & 1) << x for x in range(256))
+        assert val[outputs[j]] == want, f"LUT output bit {j} wrong"
+
+
 def main():
     S = aes_sbox()
     best = None
@@ -301,9 +431,11 @@ def main():
                 C, wires = r
                 nx = sum(1 for g in C.gates if g[0] == "^")
                 na = sum(1 for g in C.gates if g[0] == "&")
-                if best is None or nx + na < best[0]:
-                    best = (nx + na, nx, na, mu, lam, beta, C, wires)
-    total, nx, na, mu, lam, beta, C, wires = best
+                luts = lut_map(C.gates, wires)
+                if best is None or (len(luts), nx + na) < best[0]:
+                    best = ((len(luts), nx + na), nx, na, mu, lam, beta, C, wires, luts)
+    _, nx, na, mu, lam, beta, C, wires, luts = best
+    check_luts(luts, wires, S)
     # exhaustive check on all 256 inputs
     for j in range(8):
         want = sum((((S[x] ^ 0x63) >> j) & 1) << x for x in range(256))
@@ -320,25 +452,52 @@ def main():
         "// Bitsliced AES S-box without its affine constant 0x63 (folded into the round",
         "// keys by k_aes.hip): x[i] holds bit i of the input byte of every slice; on",
         f"// return x[i] holds bit i of S(x) ^ 0x63.  Tower GF(((2^2)^2)^2) with mu = {mu},",
-        f"// lambda = {lam}, beta = {beta} (see the script); {sum(g[0] == '^' for g in gates)} XOR + "
-        f"{sum(g[0] == '&' for g in gates)} AND,",
-        "// checked on all 256 inputs when generated.  No table, no branch: constant time.",
+        f"// lambda = {lam}, beta = {beta} (see the script): {sum(g[0] == '^' for g in gates)} XOR + "
+        f"{sum(g[0] == '&' for g in gates)} AND, covered by",
+        f"// {len(luts)} three-input functions (one v_bitop3_b32 each on gfx950); circuit and",
+        "// cover checked on all 256 inputs when generated.  No table, no branch: constant time.",
         "#pragma once",
         "#include <hip/hip_runtime.h>",
+        "#include <stdint.h>",
         "",
-        "template <class W>",
-        "__host__ __device__ __forceinline__ void aes_sbox_bs(W x[8]) {",
+        "// f(a, b, c) bitwise, truth table T indexed by (a << 2) | (b << 1) | c",
+        "template <unsigned T>",
+        "__host__ __device__ __forceinline__ uint32_t lut3(uint32_t a, uint32_t b, uint32_t c) {",
+        "#if __HIP_DEVICE_COMPILE__",
+        "    return __builtin_amdgcn_bitop3_b32(a, b, c, T);",
+        "#else",
+        "    uint32_t r = 0;",
+        "    for (unsigned m = 0; m < 8; ++m)",
+        "        if ((T >> m) & 1u)",
+        "            r |= ((m & 4) ? a : ~a) & ((m & 2) ? b : ~b) & ((m & 1) ? c : ~c);",
+        "    return r;",
+        "#endif",
+        "}",
+        "",
+        "__host__ __device__ __forceinline__ void aes_sbox_bs(uint32_t x[8]) {",
     ]
     for i in range(8):
-        lines.append(f"    const W w{i} = x[{i}];")
+        lines.append(f"    const uint32_t w{i} = x[{i}];")
+    for w, leaves, imm in luts:
+        ops = [f"w{l}" for l in leaves] + [f"w{leaves[0]}"] * (3 - len(leaves))
+        lines.append(f"    const uint32_t w{w} = lut3<0x{imm:02x}>({', '.join(ops)});")
+    for j in range(8):
+        lines.append(f"    x[{j}] = w{wires[j]};")
+    lines.append("}")
+    # the same circuit as two-input gates, for the host key schedule (no bitop3 there)
+    lines += ["", "// Host form: the AND/XOR circuit itself.",
+              "inline void aes_sbox_gates(uint32_t x[8]) {"]
+    for i in range(8):
+        lines.append(f"    const uint32_t w{i} = x[{i}];")
     for op, w, a, b in gates:
-        lines.append(f"    const W w{w} = w{a} {op} w{b};")
+        lines.append(f"    const uint32_t w{w} = w{a} {op} w{b};")
     for j in range(8):
         lines.append(f"    x[{j}] = w{wires[j]};")
     lines.append("}")
     with open(OUT, "w") as f:
         f.write("\n".join(lines) + "\n")
-    print(f"mu={mu} lambda={lam} beta={beta}: {nx} XOR + {na} AND -> {OUT}", file=sys.stderr)
+    print(f"mu={mu} lambda={lam} beta={beta}: {nx} XOR + {na} AND, {len(luts)} LUT3 -> {OUT}",
+          file=sys.stderr)
 
 
 if __name__ == "__main__":
