@@ -19,6 +19,10 @@ struct DeviceCtx {
     int device = -1;
     uint32_t *status = nullptr;  // library-owned device status word
     Buffer ws_a, ws_b, ws_mat, ws_r, ws_coef, ws_rec;  // aggregation scratch
+    // bytes of ws_mat (from its start) known to hold the scatter path's empty sentinel:
+    // the scatter sum restores every slot it used, so the fill runs once per buffer
+    size_t mat_clean = 0, mat_clean_cap = 0;
+    void *mat_clean_ptr = nullptr;
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel, ws_keys, ws_start;            // ordered folds (nips19, non_oblivious)

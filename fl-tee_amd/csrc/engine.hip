@@ -25,6 +25,7 @@ hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t 
 hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
                                   bool accumulate, hipStream_t s);
 hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uint32_t *mat,
+                              size_t *mat_clean,
                               uint32_t *dup, float coef, float *out, bool accumulate,
                               uint32_t *status, hipStream_t s);
 
@@ -332,8 +333,13 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         if (dense) {
             e = launch_dense_accumulate(rec, n, d, coef, out, ccoef, acc, status, s);
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS && use_scatter_rows(n, k, d)) {
-            e = launch_scatter_sum(rec, n, k, d, (uint32_t *)c->ws_mat.ptr, c->status + 16, coef,
-                                   out, acc, status, s);
+            if (c->mat_clean_ptr != c->ws_mat.ptr || c->mat_clean_cap != c->ws_mat.cap) {
+                c->mat_clean = 0;  // a new allocation: contents unknown
+                c->mat_clean_ptr = c->ws_mat.ptr;
+                c->mat_clean_cap = c->ws_mat.cap;
+            }
+            e = launch_scatter_sum(rec, n, k, d, (uint32_t *)c->ws_mat.ptr, &c->mat_clean,
+                                   c->status + 16, coef, out, acc, status, s);
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
             const size_t M = next_pow2_sz(n * k);
             uint64_t *K = (uint64_t *)c->ws_a.ptr;
@@ -344,6 +350,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         } else {
             if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
                 e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
+            c->mat_clean = 0;  // the rows below overwrite the scatter sentinels
             if (e == hipSuccess)
                 e = launch_sweep_materialize(rec, n, k, d, (float *)c->ws_mat.ptr, status, s);
             if (e == hipSuccess)

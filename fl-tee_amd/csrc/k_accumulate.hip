@@ -645,9 +645,11 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restri
 }
 
 // One lane per output j: the n rows' slots j are read U at a time (wave-coalesced
-// 256-B loads) and added in client order.
+// 256-B loads) and added in client order.  Every slot a record filled is set back to the
+// sentinel (on the repeated-index path: the whole column), so the rows are empty again
+// for the next call and no fill launch is needed (launch_scatter_sum).
 template <bool ACC, int U>
-__global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restrict__ mat, size_t d,
+__global__ __launch_bounds__(256) void scatter_rows_sum(uint32_t *__restrict__ mat, size_t d,
                                                         uint32_t n, const uint2 *__restrict__ rec,
                                                         size_t nrec, const uint32_t *dup,
                                                         uint32_t epoch, float coef,
@@ -657,7 +659,7 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
     bool hit = false;
     if (*dup != epoch) {
         if (j >= d) return;
-        const uint32_t *col = mat + j;
+        uint32_t *col = mat + j;
         uint32_t c = 0;
         for (; c + U <= n; c += U) {
             uint32_t x[U];
@@ -668,6 +670,7 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
                 const bool h = x[u] != kEmptySlot;
                 acc = __fadd_rn(acc, h ? __uint_as_float(x[u]) : 0.0f);
                 hit |= h;
+                if (h) col[(size_t)(c + u) * d] = kEmptySlot;
             }
         }
         if (c < n) {  // the last n % U rows as one predicated batch (all loads in flight)
@@ -681,6 +684,7 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
                     const bool h = x[u] != kEmptySlot;
                     acc = __fadd_rn(acc, h ? __uint_as_float(x[u]) : 0.0f);
                     hit |= h;
+                    if (h) col[(size_t)(c + u) * d] = kEmptySlot;
                 }
             }
         }
@@ -699,6 +703,7 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
             }
         }
         if (j >= d) return;
+        for (uint32_t c = 0; c < n; ++c) mat[(size_t)c * d + j] = kEmptySlot;
     }
     if (ACC) {
         if (hit) out[j] = __fadd_rn(out[j], acc);
@@ -708,7 +713,7 @@ __global__ __launch_bounds__(256) void scatter_rows_sum(const uint32_t *__restri
 }
 
 hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uint32_t *mat,
-                              uint32_t *dup, float coef, float *out, bool accumulate,
+                              size_t *mat_clean, uint32_t *dup, float coef, float *out, bool accumulate,
                               uint32_t *status, hipStream_t s) {
     if (d == 0) return hipSuccess;
     // *dup holds the epoch of the last call that saw a repeated index: a fresh epoch per
@@ -716,8 +721,13 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
     static std::atomic<uint32_t> epochs{0};
     uint32_t epoch = ++epochs;
     if (epoch == 0) epoch = ++epochs;
-    hipError_t e = hipMemsetAsync(mat, 0xFF, n * d * 4, s);
-    if (e != hipSuccess) return e;
+    // the rows [0, n*d) must hold the sentinel: filled once per buffer, then kept so by
+    // scatter_rows_sum, which empties every slot it consumed
+    if (*mat_clean < n * d * 4) {
+        hipError_t e = hipMemsetAsync(mat, 0xFF, n * d * 4, s);
+        if (e != hipSuccess) return e;
+        *mat_clean = n * d * 4;
+    }
     if (k) {
         const size_t bx = (k + 255) / 256 < 1024 ? (k + 255) / 256 : 1024;
         const size_t by = n < 65535 ? n : 65535;

@@ -155,6 +155,34 @@ def test_non_oblivious_scatter_sentinel_value(dev, oracle):
     assert bits_equal(out[~nan], ref[~nan])
 
 
+def test_non_oblivious_scatter_rows_reused_across_calls(dev, oracle):
+    """The scatter rows are filled with the empty sentinel once per buffer and emptied
+    again by each sum: calls of other shapes (the same bytes, another [n][d] layout), the
+    baseline sweep writing its dense rows into the same scratch, a repeated index, the
+    sentinel value and an out-of-range index in between leave every later call exact."""
+    rng = np.random.default_rng(11)
+    seq = [(4, 1000, 100, 4, None), (2, 3000, 50, 4, None), (4, 1000, 100, 3, None),
+           (4, 1000, 100, 4, None), (3, 700, 60, 4, "repeat"), (3, 700, 60, 4, None),
+           (5, 900, 80, 4, "sentinel"), (5, 900, 80, 4, None), (2, 400, 30, 4, "range"),
+           (6, 1500, 200, 4, None), (2, 3000, 50, 4, None)]
+    for n, d, k, alg, kind in seq:
+        idx, val = rand_sparse(rng, n, d, k)
+        if kind == "repeat":
+            idx[k + 1] = idx[k]
+        elif kind == "sentinel":
+            val[5] = np.uint32(0xFFFFFFFF).view(np.float32)
+        elif kind == "range":
+            idx[3] = d + 7
+        out = dev.aggregate(alg, cuda_records(dev, idx, val), n, k, d).cpu().numpy()
+        if kind == "range":
+            assert dev.status() & 0x2
+            continue
+        assert dev.status() == 0
+        ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+        ok = ~np.isnan(ref)
+        assert st == 0 and bits_equal(out[ok], ref[ok]), (n, d, k, alg, kind)
+
+
 def test_non_oblivious_index_out_of_range(dev):
     rec = cuda_records(dev, np.array([0, 9], np.uint32), np.ones(2, np.float32))
     dev.aggregate(4, rec, 1, 2, 5)
