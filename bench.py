@@ -22,6 +22,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -572,7 +573,7 @@ def e2e_sample(torch, D, n, d, device, reps=3):
                 "AES left after the last chunk landed, aggregate+D2H}")
 
 
-def c_abi_multi_gpu(world):
+def c_abi_multi_gpu(world, timeout=420):
     """The multi-GPU path as the Rust host reaches it: ECALLs on one enclave id over all
     `world` GPUs (fltee_device_init_multi), host-inclusive, vs a one-GPU eid
     (scripts/ecall_multi_bench.py).  Run in a child process: it opens its own RCCL
@@ -581,7 +582,7 @@ def c_abi_multi_gpu(world):
     cmd = [sys.executable, os.path.join(ROOT, "scripts", "ecall_multi_bench.py"), "--devices",
            str(world)]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=420)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     except Exception as ex:  # noqa: BLE001 - reported, never fatal for the bench line
         return {"error": repr(ex)}
     lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
@@ -708,29 +709,7 @@ def main():
     value = world * n * kk / (elapsed / args.steps)
     algo_bytes = n * kk * 8 + d * 4  # records read + averaged output written, per launch
     del recs, gathered
-    sharded = None
-    if world > 1 and not args.no_extra:
-        sharded = {"c5_sharded": bench_c5_sharded(torch, D, dist, world, rank, device,
-                                                  steps=max(3, args.steps // 10), warmup=1)}
-        if world & (world - 1) == 0:
-            sharded["c5_index_sharded"] = bench_c5_index_sharded(
-                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
-            sharded["c5_index_sharded_pairwise"] = bench_c5_index_sharded(
-                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1,
-                exchange="pairwise")
-            sharded["c4_index_sharded"] = bench_c4_index_sharded(
-                torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)
-        if os.environ.get("FLTEE_BENCH_NO_CABI") != "1":
-            # the C-ABI multi-GPU eid, in a child of rank 0 while every rank waits on a
-            # host (gloo) barrier with its cached HBM released
-            hostpg = dist.new_group(backend="gloo")
-            torch.cuda.synchronize()
-            torch.cuda.empty_cache()
-            dist.barrier(group=hostpg)
-            if rank == 0:
-                sharded["c_abi_multi_gpu"] = c_abi_multi_gpu(world)
-            dist.barrier(group=hostpg)
-
+    line = None
     if rank == 0:
         line = {
             "metric": "aggregated params/sec (device-resident), 100 clients x MLP-MNIST updates",
@@ -751,6 +730,59 @@ def main():
                          "kernel": "dense_accumulate_v", "algorithmic_bytes": algo_bytes,
                          "kernel_ms": kern * 1e3},
         }
+    sharded = None
+    if world > 1 and not args.no_extra:
+        # Every sharded leg runs under a watchdog: if the legs overrun the budget (a stuck
+        # collective), rank 0 prints the line with what finished and every rank exits, so
+        # the headline measurement above is never lost to an extra.
+        sharded = {}
+        if rank == 0:
+            line["extra"] = sharded
+        budget = float(os.environ.get("FLTEE_BENCH_EXTRA_BUDGET_S", "420"))
+        t_extra = time.monotonic()
+        state = {"leg": None, "printed": False}
+        lock = threading.Lock()
+
+        def watchdog():
+            time.sleep(budget)
+            with lock:
+                if rank == 0 and not state["printed"]:
+                    line["extra_timed_out"] = state["leg"]
+                    print(json.dumps(line), flush=True)
+                    state["printed"] = True
+            os._exit(0)
+
+        threading.Thread(target=watchdog, daemon=True).start()
+        legs = [("c5_sharded", lambda: bench_c5_sharded(
+            torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1))]
+        if world & (world - 1) == 0:
+            legs += [
+                ("c5_index_sharded", lambda: bench_c5_index_sharded(
+                    torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1)),
+                ("c5_index_sharded_pairwise", lambda: bench_c5_index_sharded(
+                    torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1,
+                    exchange="pairwise")),
+                ("c4_index_sharded", lambda: bench_c4_index_sharded(
+                    torch, D, dist, world, rank, device, steps=max(3, args.steps // 10), warmup=1))]
+        for name, fn in legs:
+            state["leg"] = name
+            sharded[name] = fn()
+        if os.environ.get("FLTEE_BENCH_NO_CABI") != "1":
+            # the C-ABI multi-GPU eid, in a child of rank 0 while every rank waits on a
+            # host (gloo) barrier with its cached HBM released
+            state["leg"] = "c_abi_multi_gpu"
+            hostpg = dist.new_group(backend="gloo")
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            dist.barrier(group=hostpg)
+            if rank == 0:
+                left = budget - (time.monotonic() - t_extra) - 15
+                sharded["c_abi_multi_gpu"] = (c_abi_multi_gpu(world, timeout=left) if left > 30
+                                              else {"error": "skipped: extras budget spent"})
+            dist.barrier(group=hostpg)
+        state["leg"] = None
+
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_sample(d, n, args.cpu_seconds)
         if world == 1 and not args.no_e2e and k is None:
@@ -804,8 +836,12 @@ def main():
             line["reference_configs"] = bench_reference_configs(torch, D, device)
             line["next_rows"] = bench_next_rows(torch, D, device)
         if sharded is not None:
-            line["extra"] = sharded
-        print(json.dumps(line), flush=True)
+            with lock:
+                if not state["printed"]:
+                    print(json.dumps(line), flush=True)
+                    state["printed"] = True
+        else:
+            print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
