@@ -33,6 +33,11 @@ for w in ${PMC}; do
       --no-e2e > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
   echo "pmc $w"
 done
+if [ "${AESPROF:-0}" = 1 ]; then  # the constant-time AES-CTR kernel (scripts/bench_aes.py shapes)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_aes" -o run \
+      -- python3 scripts/bench_aes.py > "$OUT/prof_aes.log" 2>&1 || exit 17
+  echo "profiled aes"
+fi
 if [ "${CABI:-0}" = 1 ]; then  # the C-ABI multi-GPU eid over the visible GPUs (1-rank RCCL on one)
   timeout -k 10 300 python -u scripts/ecall_multi_bench.py > "$OUT/c_abi_multi_gpu.json" 2> "$OUT/c_abi_multi_gpu.err" || exit 16
   echo "c_abi"
