@@ -214,8 +214,8 @@ __device__ __forceinline__ void transpose32(uint32_t m[32]) {
 // quad_perm, no LDS), SubBytes and MixColumns stay in the lane.  96 VGPRs (5 waves per
 // SIMD).  A/B (profiles/r02/ab/aes_variants.jsonl): one lane per 32 blocks with the
 // whole state (452 VGPRs, one wave per SIMD) ran 2.04 ms on the 800 MB headline payload
-// and this form 1.39 ms with two-input gates, 1.19 ms with the S-box as 119 bitop3s
-// (the T-table kernel: 1.21 ms).
+// and this form 1.39 ms with two-input gates, 1.19 ms with the S-box as 119 bitop3s, 1.14
+// ms with MixColumns + AddRoundKey as XOR3s too (the T-table kernel: 1.20 ms).
 constexpr int kAesWindow4 = 512;  // counter blocks per wave: 16 quads x 32 slices
 
 __device__ __forceinline__ uint32_t quad_rot(uint32_t v, int r) {
@@ -232,31 +232,14 @@ __device__ __forceinline__ uint32_t sext_bit(uint32_t w, int pos) {
     return (uint32_t)((int32_t)(w << (31 - pos)) >> 31);  // v_bfe_i32 w, pos, 1
 }
 
-template <bool MIX>
-__device__ __forceinline__ void round_col(uint32_t s[4][8]) {
+// SubBytes + ShiftRows of the lane's column
+__device__ __forceinline__ void sub_shift_col(uint32_t s[4][8]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) aes_sbox_bs(s[r]);
 #pragma unroll
     for (int r = 1; r < 4; ++r)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s[r][i] = quad_rot(s[r][i], r);
-    if (!MIX) return;
-    uint32_t t[8], ns[4][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = s[0][i] ^ s[1][i] ^ s[2][i] ^ s[3][i];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        uint32_t u[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) u[i] = s[r][i] ^ s[(r + 1) & 3][i];
-        const uint32_t x[8] = {u[7], u[0] ^ u[7], u[1], u[2] ^ u[7], u[3] ^ u[7], u[4], u[5], u[6]};
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ns[r][i] = s[r][i] ^ t[i] ^ x[i];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s[r][i] = ns[r][i];
 }
 
 __device__ __forceinline__ void ark_col(uint32_t s[4][8], uint32_t w) {
@@ -264,6 +247,40 @@ __device__ __forceinline__ void ark_col(uint32_t s[4][8], uint32_t w) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s[r][i] ^= sext_bit(w, 24 - 8 * r + i);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return lut3<0x96>(a, b, c);
+}
+
+// MixColumns and AddRoundKey (key word w of the lane's column) as three-input XORs:
+// out_r = a_r ^ t ^ xtime(a_r ^ a_{r+1}) ^ k_r with t = a_0 ^ a_1 ^ a_2 ^ a_3, i.e.
+// 2 a_r ^ 3 a_{r+1} ^ a_{r+2} ^ a_{r+3}; plane i of xtime(u) is u_{i-1}, plus u_7 for
+// i = 1, 3, 4 (0x1b).  Two v_bitop3 per plane (three where u_7 enters).
+__device__ __forceinline__ void mix_ark_col(uint32_t s[4][8], uint32_t w) {
+    uint32_t t[8], ns[4][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = xor3(s[0][i], s[1][i], s[2][i]) ^ s[3][i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t *a = s[r], *b = s[(r + 1) & 3];
+        const uint32_t u7 = a[7] ^ b[7];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t k = sext_bit(w, 24 - 8 * r + i);
+            if (i == 0) {
+                ns[r][i] = xor3(xor3(a[0], t[0], a[7]), b[7], k);
+            } else if (i == 1 || i == 3 || i == 4) {
+                ns[r][i] = xor3(xor3(a[i], t[i], a[i - 1]), b[i - 1], u7) ^ k;
+            } else {
+                ns[r][i] = xor3(xor3(a[i], t[i], a[i - 1]), b[i - 1], k);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[r][i] = ns[r][i];
 }
 
 template <bool ALIGNED>
@@ -304,10 +321,10 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
 #pragma unroll 1
         for (int R = 1; R < 10; ++R) {
             const uint32_t w = rk[4 * R] ^ 0x63636363u;  // the S-boxes' 0x63, folded
-            round_col<true>(s);
-            ark_col(s, w);
+            sub_shift_col(s);
+            mix_ark_col(s, w);
         }
-        round_col<false>(s);
+        sub_shift_col(s);
         ark_col(s, rk[40] ^ 0x63636363u);
         // rows 8 r + i -> word j = keystream word `col` of block j
         transpose32(&s[0][0]);
