@@ -340,6 +340,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             }
             e = launch_scatter_sum(rec, n, k, d, (uint32_t *)c->ws_mat.ptr, &c->mat_clean,
                                    c->status + 16, coef, out, acc, status, s);
+            if (e != hipSuccess) c->mat_clean = 0;  // the emptying pass may not have run
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
             const size_t M = next_pow2_sz(n * k);
             uint64_t *K = (uint64_t *)c->ws_a.ptr;
