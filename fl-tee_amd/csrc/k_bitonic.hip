@@ -168,19 +168,21 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
 // [DLOG, DLOG+R) and its part above them is a multiple of 16), so every slot is a
 // ds_read/ds_write immediate offset off one per-group address — five VALU per slot
 // fewer.  Same greedy split into rounds as lds_steps: the same network.
-// WL > 0: a strided tile (2^WL consecutive positions x rows 2^dtile apart, the rounds at
-// tile-local bits >= WL): the group's first position and global distance from tile_pos.
+// WL > 0: a strided tile (2^WL consecutive positions x rows 2^dtile apart): the group's
+// first position from tile_pos, its global distance 2^(DLOG - WL + dtile) for the rounds
+// on the row bits (>= WL) and 2^DLOG for those on the consecutive bits (< WL: a stage's
+// tail fused into the tile, plan_network).
 template <int MODE, int R, int E, int NT, int DLOG, int WL = 0>
 __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
-    static_assert(WL == 0 || DLOG >= WL, "strided rounds stay above the row bits");
+    static_assert(WL == 0 || DLOG >= WL || DLOG + R <= WL, "a round stays on one side of bit WL");
     constexpr int G = E >> R;
 #pragma unroll
     for (int h = 0; h < G; ++h) {
         const uint32_t g = threadIdx.x + (uint32_t)h * NT;
         const uint32_t b = spread(g, (uint32_t)DLOG, (uint32_t)R);
         const uint32_t p0 = WL ? tile_pos(base, b, (uint32_t)WL, dtile) : base + b;
-        const uint32_t dg = WL ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
+        const uint32_t dg = (WL && DLOG >= WL) ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
         uint64_t v[1 << R];
         if constexpr (DLOG + R >= 4) {
             uint64_t *row = sm + lpad(b);
@@ -270,9 +272,24 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
             // seg0 = (stage << 8) | top: first the last steps top..0 of an earlier stage on
             // the tile's low (consecutive) bits — a stage's tail fused with the next
             // stage's head (the planned schedule, plan_network)
-            if (seg0)
-                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, seg0 >> 8, (int)(seg0 & 0xFFu), 0,
-                                       seed);
+            if (seg0) {
+                // the tail on every consecutive bit (top = WL - 1, what plan_network emits):
+                // compile-time rounds like the rows below; any other top: runtime rounds
+                // (bit 31: runtime rounds regardless, FLTEE_BITONIC_TAIL_CT=0, A/B)
+                const uint32_t st = (seg0 >> 8) & 0xFFFFu;
+                bool done = false;
+                // (2^12 tiles of 512 lanes; the 1024-lane 2^14 tiles are held to 128 VGPRs
+                // and spill with the tail unrolled: C5 14.82 -> 15.44 ms, so they keep
+                // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
+                if constexpr (TL != 0 && WL != 0 && MODE != 2 && NT <= 512) {
+                    if ((seg0 & 0x800000FFu) == (uint32_t)WL - 1u) {
+                        lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
+                        done = true;
+                    }
+                }
+                if (!done)
+                    lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, seed);
+            }
             if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
                 lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
@@ -733,6 +750,11 @@ static bool merge_ct() {
     static bool on = knob_on("FLTEE_BITONIC_CT");
     return on;
 }
+// the planned tiles' fused tails with compile-time rounds (FLTEE_BITONIC_TAIL_CT=0: off, A/B)
+static bool tail_ct() {
+    static bool on = knob_on("FLTEE_BITONIC_TAIL_CT");
+    return on;
+}
 static bool sort_ct() {
     static bool on = knob_on("FLTEE_BITONIC_SORT_CT");
     return on;
@@ -940,19 +962,34 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
         if (c.E == 32) return launch_direct<MODE, 32, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
     }
-    // strided passes of the usual tile sizes, rows of 2^4 .. 2^7: compile-time rounds
-    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && wlog <= 7 && tiles_ct() &&
-        ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12))) {
-#define BT_ST(E_, NT_, TL_)                                                                        \
-    switch (wlog) {                                                                                \
-    case 4: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 4>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
-    case 5: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 5>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
-    case 6: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 6>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
-    default: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, 7>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0); \
-    }
-        if (c.NT == 1024) { BT_ST(16, 1024, 14) }
-        BT_ST(8, 512, 12)
-#undef BT_ST
+    // strided passes of the usual tile sizes, rows of 2^4 .. 2^7 (and, for 2^12 tiles, the
+    // planned tiles' 2^8 .. 2^9, whose tails fill the consecutive bits): compile-time rounds
+    if (seg0 && !tail_ct()) seg0 |= 0x80000000u;
+    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && (1u << wlog) <= c.NT && tiles_ct() &&
+        ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
+        (wlog <= 7 || (seg0 && MODE != 2 && tail_ct() && c.NT <= 512))) {
+#define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
+    case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0);
+        if (c.NT == 1024) {
+            switch (wlog) {
+                BT_ST_CASE(16, 1024, 14, 4) BT_ST_CASE(16, 1024, 14, 5) BT_ST_CASE(16, 1024, 14, 6)
+                BT_ST_CASE(16, 1024, 14, 7)
+            default: break;
+            }
+        } else {
+            switch (wlog) {
+                BT_ST_CASE(8, 512, 12, 4) BT_ST_CASE(8, 512, 12, 5) BT_ST_CASE(8, 512, 12, 6)
+                BT_ST_CASE(8, 512, 12, 7)
+            default: break;
+            }
+            if constexpr (MODE != 2) {  // planned tiles only (the keyed shuffle runs per stage)
+                switch (wlog) {
+                    BT_ST_CASE(8, 512, 12, 8) BT_ST_CASE(8, 512, 12, 9)
+                default: break;
+                }
+            }
+        }
+#undef BT_ST_CASE
     }
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0)
