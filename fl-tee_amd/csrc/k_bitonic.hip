@@ -514,7 +514,7 @@ __device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint
 // 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
 // log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
 // stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
-template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0>
+template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0, bool LPF = true>
 __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t seed,
                                                           uint32_t ntiles, uint32_t pbase,
@@ -586,10 +586,22 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
         for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
         __syncthreads();
         const uint32_t next = tile + stride;
-        load(next < ntiles ? next : tile);
         if constexpr (TL != 0) {  // tlog == TL (launcher)
-            sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
+            // the next tile's loads go out before the LAST stage's rounds, not before the
+            // first: the prefetch registers stay free through the rounds of stages
+            // log2 E + 1 .. TL - 1 (1024 lanes are held to 128 VGPRs; with the prefetch
+            // live across every round the 2^14-tile kernels spilled), and stage TL's
+            // rounds still cover the load latency (FLTEE_BITONIC_SORT_LATEPF=0: A/B)
+            if constexpr (LPF) {
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                load(next < ntiles ? next : tile);
+                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, seed);
+            } else {
+                load(next < ntiles ? next : tile);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
+            }
         } else {
+            load(next < ntiles ? next : tile);
             for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
             lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
@@ -755,6 +767,12 @@ static bool tail_ct() {
     static bool on = knob_on("FLTEE_BITONIC_TAIL_CT");
     return on;
 }
+// the first pass's prefetch before the last stage (FLTEE_BITONIC_SORT_LATEPF=0: before
+// the first LDS round, A/B)
+static bool sort_late_pf() {
+    static bool on = knob_on("FLTEE_BITONIC_SORT_LATEPF");
+    return on;
+}
 static bool sort_ct() {
     static bool on = knob_on("FLTEE_BITONIC_SORT_CT");
     return on;
@@ -883,16 +901,25 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
         grid += nb < 1024u ? nb : 1024u;
         net_account((uint64_t)8 * gg.pad_n);
     }
-#define BS_GO(RL_, TL_)                                                                            \
+#define BS_GO_PF(RL_, TL_, LPF_)                                                                   \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_>, \
+            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_>), dim3(grid),          \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_>), dim3(grid),    \
                            dim3(NT), c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);            \
+    } while (0)
+#define BS_GO(RL_, TL_)                                                                            \
+    do {                                                                                           \
+        if constexpr (TL_ != 0) {                                                                  \
+            if (!sort_late_pf()) BS_GO_PF(RL_, TL_, false);                                        \
+            else BS_GO_PF(RL_, TL_, true);                                                         \
+        } else {                                                                                   \
+            BS_GO_PF(RL_, TL_, true);                                                              \
+        }                                                                                          \
     } while (0)
     // the usual tile sizes: every stage's LDS rounds unrolled at compile time
     if (sort_ct()) {
@@ -914,6 +941,7 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     default: if constexpr (R1 >= 5) BS_GO(5, 0); break;
     }
 #undef BS_GO
+#undef BS_GO_PF
     return hipGetLastError();
 }
 
