@@ -234,7 +234,7 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 // around each prefetch load makes hipcc branch and wait vmcnt(0) per load
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
-template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase,
@@ -260,11 +260,15 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
-        {
+        auto prefetch = [&]() {
             const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) * 8u;
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
-        }
+        };
+        // compile-time strided tiles: the prefetch after the fused tail's rounds (its
+        // registers are then not live through the tail; FLTEE_BITONIC_TILE_LATEPF=0: A/B)
+        constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT;
+        if (!kLate) prefetch();
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
@@ -290,6 +294,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                 if (!done)
                     lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, seed);
             }
+            if (kLate) prefetch();
             if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
                 lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
@@ -782,20 +787,40 @@ static bool tiles_ct() {
     return on;
 }
 
-template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
-static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
-                                 uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                 uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
+// the compile-time strided tiles' prefetch after their fused tail (FLTEE_BITONIC_TILE_LATEPF=0:
+// before it, A/B)
+static bool tile_late_pf() {
+    static bool on = knob_on("FLTEE_BITONIC_TILE_LATEPF");
+    return on;
+}
+
+template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
+static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                   uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                   uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL>), dim3(grid), dim3(NT), lds, s, data,
-                       tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF>), dim3(grid), dim3(NT), lds, s,
+                       data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
     return hipGetLastError();
+}
+
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
+static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                 uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                 uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
+    if constexpr (TL != 0 && WL != 0 && !SORT) {
+        if (!tile_late_pf())
+            return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, false>(grid, lds, s, data, tlog, ilog, wlog,
+                                                                      dtile, seed, tiles, pbase, seg0);
+    }
+    return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, true>(grid, lds, s, data, tlog, ilog, wlog, dtile,
+                                                             seed, tiles, pbase, seg0);
 }
 
 struct TileCfg {
