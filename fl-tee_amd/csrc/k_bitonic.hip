@@ -787,11 +787,16 @@ static bool tiles_ct() {
     return on;
 }
 
-// the compile-time strided tiles' prefetch after their fused tail (FLTEE_BITONIC_TILE_LATEPF=0:
-// before it, A/B)
-static bool tile_late_pf() {
-    static bool on = knob_on("FLTEE_BITONIC_TILE_LATEPF");
-    return on;
+// the compile-time strided tiles' prefetch after their fused tail, except the tiles with
+// a tail on rows of 2^5 (their 9 row steps cover the load less well: 514 -> 553 us at
+// C5 with it late, while every other shape gains, `profiles/r02/ab/tile_late_prefetch.jsonl`)
+// FLTEE_BITONIC_TILE_LATEPF: 0 = never late, 2 = always late (A/B), default 1
+static int tile_late_pf_mode() {
+    static int m = [] {
+        const char *e = getenv("FLTEE_BITONIC_TILE_LATEPF");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
 }
 
 template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
@@ -815,7 +820,8 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
     if constexpr (TL != 0 && WL != 0 && !SORT) {
-        if (!tile_late_pf())
+        const int m = tile_late_pf_mode();
+        if (m == 0 || (m == 1 && WL == 5 && seg0 != 0))
             return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, false>(grid, lds, s, data, tlog, ilog, wlog,
                                                                       dtile, seed, tiles, pbase, seg0);
     }
