@@ -563,6 +563,15 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
     uint64_t pf[E];
     auto load = [&](uint32_t tl) {
         const uint32_t sb = (tl << tlog) * 8u;
+        // GEN 2: the lane's E positions are consecutive, so dummy e = p - nrec of the first
+        // one is divided by tf once and (i, j) = (e / tf, e % tf) advance with p
+        uint32_t gi = 0, gj = 0;
+        if (GEN == 2) {
+            const uint32_t p0 = pbase + (tl << tlog) + t * (uint32_t)E;
+            const uint32_t e0 = p0 > g.nrec ? p0 - g.nrec : 0u;
+            gi = g.tf ? e0 / g.tf : 0u;
+            gj = e0 - gi * g.tf;
+        }
 #pragma unroll
         for (int r = 0; r < E; r += 2) {
             const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ls, (int)(voff + (uint32_t)r * 8u),
@@ -573,8 +582,19 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
                 const uint32_t xl = (tl << tlog) + t * (uint32_t)E + (uint32_t)r;  // local index of pf[r]
                 if (xl + 1u == nloc)  // the 16-B load straddles the end of rec: reload 8 B
                     pf[r] = bt_load<kTileCP>(ls, voff + (uint32_t)r * 8u, sb);
-                pf[r] = gen_entry<GEN>(g, pbase + xl, pf[r]);
-                pf[r + 1] = gen_entry<GEN>(g, pbase + xl + 1u, pf[r + 1]);
+                if (GEN == 1) {
+                    pf[r] = gen_entry<GEN>(g, pbase + xl, pf[r]);
+                    pf[r + 1] = gen_entry<GEN>(g, pbase + xl + 1u, pf[r + 1]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        if (pbase + xl + (uint32_t)u >= g.nrec) {  // entry (i, j): (r_i < j) ? i : MAX
+                            pf[r + u] = (g.tf == 0 || gi >= g.d || g.r[gi] >= gj) ? 0xFFFFFFFFull
+                                                                                  : (uint64_t)gi;
+                            if (++gj == g.tf) { gj = 0; ++gi; }
+                        }
+                    }
+                }
             }
         }
     };
