@@ -819,11 +819,14 @@ def main():
             line["extra"] = extra
             # the metric's literal configuration (100 clients x MLP-MNIST, dense baseline),
             # inputs rotated through > 1.5 x the Infinity Cache so every launch reads HBM
-            lit = bench_workload(torch, D, "mnist100", steps=max(20, args.steps), warmup=5,
-                                 device=device, cold=True)
+            # best of 3 trials, each warming every rotating buffer once (one trial on a
+            # busy box measured 18.6 us against 10.4-10.6 us on three others)
+            lit = min((bench_workload(torch, D, "mnist100", steps=max(20, args.steps), warmup=12,
+                                      device=device, cold=True) for _ in range(3)),
+                      key=lambda r: r["kernel_s"])
             line["metric_literal_config"] = dict(
                 workload=WORKLOADS["mnist100"]["desc"], value=lit["rate"], unit="client-params/s",
-                kernel_ms=lit["kernel_s"] * 1e3, input_buffers=lit["nbuf"],
+                kernel_ms=lit["kernel_s"] * 1e3, input_buffers=lit["nbuf"], trials=3,
                 roofline=dict(bound="hbm", achieved=lit["bytes"] / lit["kernel_s"] / 1e9,
                               peak=HBM_PEAK_GBS, unit="GB/s",
                               frac=lit["bytes"] / lit["kernel_s"] / 1e9 / HBM_PEAK_GBS,
