@@ -519,7 +519,7 @@ __device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint
 // 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
 // log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
 // stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
-template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0, bool LPF = true>
+template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0, int LPF = 1>
 __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t seed,
                                                           uint32_t ntiles, uint32_t pbase,
@@ -617,7 +617,14 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             // log2 E + 1 .. TL - 1 (1024 lanes are held to 128 VGPRs; with the prefetch
             // live across every round the 2^14-tile kernels spilled), and stage TL's
             // rounds still cover the load latency (FLTEE_BITONIC_SORT_LATEPF=0: A/B)
-            if constexpr (LPF) {
+            // (LPF 2: later still, before stage TL's last LDS round)
+            constexpr int kLast = RL + R1 - 1;  // the last round's top step (greedy split)
+            if constexpr (LPF == 2 && kLast < TL - 1) {
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, seed);
+                load(next < ntiles ? next : tile);
+                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, seed);
+            } else if constexpr (LPF != 0) {
                 sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
                 load(next < ntiles ? next : tile);
                 lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, seed);
@@ -794,9 +801,15 @@ static bool tail_ct() {
 }
 // the first pass's prefetch before the last stage (FLTEE_BITONIC_SORT_LATEPF=0: before
 // the first LDS round, A/B)
-static bool sort_late_pf() {
-    static bool on = knob_on("FLTEE_BITONIC_SORT_LATEPF");
-    return on;
+// 0 = before the first round, 1 = before the last stage, 2 = before its last round;
+// default (-1): 2 for the sorts by key (C5 14.25 -> 14.21 ms), 1 for the keyed shuffle
+// (C4 9.34 vs 9.38 ms with 2; `profiles/r02/ab/sort_late_prefetch.jsonl`)
+static int sort_late_pf() {
+    static int m = [] {
+        const char *e = getenv("FLTEE_BITONIC_SORT_LATEPF");
+        return e ? atoi(e) : -1;
+    }();
+    return m;
 }
 static bool sort_ct() {
     static bool on = knob_on("FLTEE_BITONIC_SORT_CT");
@@ -966,10 +979,12 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
 #define BS_GO(RL_, TL_)                                                                            \
     do {                                                                                           \
         if constexpr (TL_ != 0) {                                                                  \
-            if (!sort_late_pf()) BS_GO_PF(RL_, TL_, false);                                        \
-            else BS_GO_PF(RL_, TL_, true);                                                         \
+            const int lpf_ = sort_late_pf() >= 0 ? sort_late_pf() : (MODE == 2 ? 1 : 2);          \
+            if (lpf_ == 0) BS_GO_PF(RL_, TL_, 0);                                                  \
+            else if (lpf_ == 2) BS_GO_PF(RL_, TL_, 2);                                             \
+            else BS_GO_PF(RL_, TL_, 1);                                                            \
         } else {                                                                                   \
-            BS_GO_PF(RL_, TL_, true);                                                              \
+            BS_GO_PF(RL_, TL_, 1);                                                                 \
         }                                                                                          \
     } while (0)
     // the usual tile sizes: every stage's LDS rounds unrolled at compile time
