@@ -591,6 +591,12 @@ def c_abi_multi_gpu(world, timeout=420):
     return json.loads(lines[-1])
 
 
+def _build_id():
+    """fltee_version(): the source hash the loaded library was built from (provenance)."""
+    from fltee import _lib as L
+    return L.lib().fltee_version().decode()
+
+
 def traffic_from_profiles(name):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
@@ -716,6 +722,7 @@ def main():
             "value": value, "unit": "client-params/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "build": _build_id(),
             "config": {"workload": ("north-star target (BASELINE.json north_star: >= 70 % of the "
                                     "HBM roofline on 100 clients x 1M-param fp32 updates, 1 GPU): "
                                     if args.workload == "ns" else "") + w["desc"],
@@ -742,15 +749,17 @@ def main():
         t_extra = time.monotonic()
         state = {"leg": None, "printed": False}
         lock = threading.Lock()
+        disarm = threading.Event()
 
         def watchdog():
-            time.sleep(budget)
+            if disarm.wait(budget):
+                return  # the extras finished in time
             with lock:
                 if rank == 0 and not state["printed"]:
                     line["extra_timed_out"] = state["leg"]
                     print(json.dumps(line), flush=True)
                     state["printed"] = True
-            os._exit(0)
+            os._exit(3)  # the headline line is printed, but a stuck leg is a failure
 
         threading.Thread(target=watchdog, daemon=True).start()
         legs = [("c5_sharded", lambda: bench_c5_sharded(
@@ -781,6 +790,7 @@ def main():
                                               else {"error": "skipped: extras budget spent"})
             dist.barrier(group=hostpg)
         state["leg"] = None
+        disarm.set()
 
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:

@@ -225,7 +225,7 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
 
 using namespace fltee;
 
-extern "C" const char *fltee_version(void) { return "fltee-mi355x 0.1 (gfx950)"; }
+// fltee_version(): build/version.cpp, generated by the Makefile (source hash + tune flags)
 
 extern "C" fltee_status_t fltee_device_init(int hip_device, fltee_eid_t *eid) {
     std::lock_guard<std::recursive_mutex> lk(api_mutex());
@@ -245,7 +245,10 @@ extern "C" fltee_status_t fltee_device_init_multi(const int *hip_devices, int n,
     uint32_t st = 0;
     Group *G = group_create(hip_devices, n, &st);
     if (!G) return st;
-    if (hipSetDevice(hip_devices[0]) != hipSuccess || !device_ctx(hip_devices[0])) return FLTEE_ERROR_UNEXPECTED;
+    if (hipSetDevice(hip_devices[0]) != hipSuccess || !device_ctx(hip_devices[0])) {
+        group_destroy(G);
+        return FLTEE_ERROR_UNEXPECTED;
+    }
     g_eid_dev.push_back(hip_devices[0]);
     *eid = (fltee_eid_t)g_eid_dev.size();
     g_groups[*eid] = G;
@@ -385,6 +388,10 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     }
     const bool sharded = G && ((aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc) ||
                                aggregation_alg == FLTEE_ALG_NIPS19);
+    // nips19 draws its seed (Laplace counts, shuffle key) once per call, whichever path
+    // runs it, so a multi-GPU eid consumes the seed sequence exactly as one GPU does
+    const uint64_t seed = aggregation_alg == FLTEE_ALG_NIPS19 ? next_seed() : 0;
+    bool group_tried = false;  // a shape the group declined is not offered to it again
     if (st == FLTEE_GROUP_FALLBACK && sharded && group_splits_host_copy(G)) {
         // every GPU copies and decrypts the clients of its own position range
         std::vector<uint32_t> rk;
@@ -399,7 +406,8 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         if (aggregation_alg == FLTEE_ALG_ADVANCED)
             st = group_advanced(G, in, n, rpc, d, coef, d_out);
         else
-            st = group_nips19(G, c, in, n, rpc, k_req, d, next_seed(), coef, d_out);
+            st = group_nips19(G, c, in, n, rpc, k_req, d, seed, coef, d_out);
+        group_tried = true;
         if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
         // "Aggregation" = the call minus its load and decrypt phases
         t2 = ta + execution_time_results[0] + execution_time_results[1];
@@ -410,13 +418,14 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         if (st) return fail(st);
         t2 = now_s();
         st = FLTEE_GROUP_FALLBACK;
-        uint64_t seed = 0;
         GroupInput in;
         in.root_rec = (const uint64_t *)c->records.ptr;
-        if (G && aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc)
-            st = group_advanced(G, in, n, rpc, d, coef, d_out);
-        else if (G && aggregation_alg == FLTEE_ALG_NIPS19)
-            st = group_nips19(G, c, in, n, rpc, k_req, d, seed = next_seed(), coef, d_out);
+        if (sharded && !group_tried) {
+            if (aggregation_alg == FLTEE_ALG_ADVANCED)
+                st = group_advanced(G, in, n, rpc, d, coef, d_out);
+            else
+                st = group_nips19(G, c, in, n, rpc, k_req, d, seed, coef, d_out);
+        }
         if (st == FLTEE_GROUP_FALLBACK)  // one device (or a shape the group does not shard)
             st = aggregate_records(c, aggregation_alg, n, rpc, d, k_req, 0, d_out, seed);
     }

@@ -12,6 +12,7 @@ struct Buffer {
     void *ptr = nullptr;
     size_t cap = 0;
     bool reserve(size_t bytes);  // grow-only hipMalloc
+    void release();              // hipFree (the owning device must be current)
 };
 
 struct DeviceCtx {

@@ -92,6 +92,12 @@ bool Buffer::reserve(size_t bytes) {
     return true;
 }
 
+void Buffer::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
 float nips19_threshold(size_t d, size_t k, size_t n) {
     const float epsilon = 100.0f, delta = 1.0f / (float)n;
     const float l1 = 2.0f * (float)k;

@@ -113,6 +113,8 @@ static const char *nccl_err(ncclResult_t r) {
     return rccl() ? rccl()->GetErrorString(r) : "RCCL unavailable";
 }
 
+static void group_free(Group *G);
+
 Group *group_create(const int *devs, int n, uint32_t *status) {
     *status = FLTEE_ERROR_INVALID_PARAMETER;
     if (!devs || n < 1 || n > 64 || (n & (n - 1))) return nullptr;  // ranges need a power of two
@@ -136,42 +138,60 @@ Group *group_create(const int *devs, int n, uint32_t *status) {
     for (int i = 0; i < n; ++i) {
         Rank &R = G->r[i];
         R.dev = devs[i];
-        if (hipSetDevice(R.dev) != hipSuccess || !device_ctx(R.dev)) { delete G; return nullptr; }
+        if (hipSetDevice(R.dev) != hipSuccess || !device_ctx(R.dev)) { group_free(G); return nullptr; }
         if (G->rccl || i == 0) {
-            if (hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) != hipSuccess) { delete G; return nullptr; }
+            if (hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) != hipSuccess) { group_free(G); return nullptr; }
         } else {
             R.s = G->r[0].s;  // virtual ranks share one stream
         }
     }
     if (G->rccl) {
-        if (!rccl()) { delete G; return nullptr; }
+        if (!rccl()) { group_free(G); return nullptr; }
         std::vector<ncclComm_t> comms(n);
         const ncclResult_t nr = rccl()->CommInitAll(comms.data(), n, devs);
         if (nr != ncclSuccess) {
             std::fprintf(stderr, "[fltee] ncclCommInitAll: %s\n", nccl_err(nr));
-            delete G;
+            group_free(G);
             return nullptr;
         }
         for (int i = 0; i < n; ++i) G->r[i].comm = comms[i];
     }
     (void)hipSetDevice(devs[0]);
     if (hipHostMalloc((void **)&G->host, 64 * 8, hipHostMallocDefault) != hipSuccess) {
-        delete G;
+        G->host = nullptr;
+        group_free(G);
         return nullptr;
     }
     *status = FLTEE_SUCCESS;
     return G;
 }
 
-void group_destroy(Group *G) {
+// Everything the group owns: per-rank buffers (they belong to the eid, not to the
+// per-device scratch), the streams (virtual ranks share rank 0's), the communicators,
+// the root's rows and the pinned readback words.
+static void group_free(Group *G) {
     if (!G) return;
-    for (auto &R : G->r) {
-        (void)hipSetDevice(R.dev);
-        (void)hipDeviceSynchronize();
+    for (size_t i = 0; i < G->r.size(); ++i) {
+        Rank &R = G->r[i];
+        if (hipSetDevice(R.dev) != hipSuccess) continue;
+        if (R.s && (G->rccl || i == 0)) (void)hipStreamSynchronize(R.s);
+        for (Buffer *b : {&R.cipher, &R.rec, &R.rk, &R.out, &R.chunk, &R.spare, &R.fold, &R.fold_dst,
+                          &R.cbuf, &R.ctmp, &R.lap, &R.list, &R.cnt, &R.st})
+            b->release();
         if (R.comm) (void)rccl()->CommDestroy(R.comm);
+        R.comm = nullptr;
+        if (R.s && (G->rccl || i == 0)) (void)hipStreamDestroy(R.s);
+        R.s = nullptr;
     }
-    // buffers stay allocated (grow-only, process lifetime, like the per-device scratch)
+    if (!G->r.empty() && hipSetDevice(G->r[0].dev) == hipSuccess) {
+        G->rows.release();
+        if (G->host) (void)hipHostFree(G->host);
+        G->host = nullptr;
+    }
+    delete G;
 }
+
+void group_destroy(Group *G) { group_free(G); }
 
 int group_size(const Group *G) { return G ? G->W : 0; }
 int group_root_device(const Group *G) { return G ? G->r[0].dev : -1; }

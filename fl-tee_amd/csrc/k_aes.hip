@@ -23,9 +23,9 @@
 // the wave covers 256 B contiguously.
 //
 // The host key schedule and the CPU self-test block use the same circuit over 16-byte
-// bitsliced states (no S-box table on the host either).  The T-table kernel of round 1
-// (key- and data-dependent LDS addresses) stays as an opt-in A/B variant:
-// FLTEE_AES_TTABLE=1 (profiles/r02/ab/aes_variants.jsonl).
+// bitsliced states (no S-box table on the host either).  There is no table-based
+// variant in the library (round 1's T-table kernel had key- and data-dependent LDS
+// addresses; its last A/B is in profiles/r02/ab/aes_variants.jsonl).
 #include <cstdlib>
 #include <mutex>
 
@@ -156,19 +156,6 @@ void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk) {
             for (int b = 0; b < 4; ++b) key[k][4 + b] = (uint8_t)(ids[c0 + k] >> (24 - 8 * b));
         expand_keys8(key, nk, rk + 44 * c0);
     }
-}
-
-static uint32_t sub_word_bs(uint32_t t) {  // S-box of each byte of t (T-table build)
-    uint32_t x[8];
-    for (int i = 0; i < 8; ++i) {
-        x[i] = 0;
-        for (int q = 0; q < 4; ++q) x[i] |= ((t >> (8 * q + i)) & 1u) << q;
-    }
-    aes_sbox_gates(x);
-    uint32_t r = 0;
-    for (int i = 0; i < 8; ++i)
-        for (int q = 0; q < 4; ++q) r |= ((x[i] >> q) & 1u) << (8 * q + i);
-    return r ^ 0x63636363u;
 }
 
 // host-side single block, for the CPU self-test (no GPU needed): slice 0 of the planes
@@ -344,123 +331,12 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
     }
 }
 
-// ------------------------------------------------- T-table kernel (A/B variant only)
-static uint32_t g_te[5][256];  // Te0..Te3, S-box widened (Te4)
-static std::once_flag g_tables_once;
-static uint32_t *g_dev_tables[64];  // per device
-static std::mutex g_dev_mu;
-
-static void build_tables() {
-    for (int x = 0; x < 256; ++x) {
-        const uint8_t s = (uint8_t)(sub_word_bs((uint32_t)x) & 0xff);
-        const uint8_t s2 = (uint8_t)((s << 1) ^ ((s & 0x80) ? 0x1b : 0));
-        const uint32_t t = ((uint32_t)s2 << 24) | ((uint32_t)s << 16) | ((uint32_t)s << 8) |
-                           (uint32_t)(s2 ^ s);
-        g_te[0][x] = t;
-        g_te[1][x] = (t >> 8) | (t << 24);
-        g_te[2][x] = (t >> 16) | (t << 16);
-        g_te[3][x] = (t >> 24) | (t << 8);
-        g_te[4][x] = s;
-    }
-}
-
-__device__ __forceinline__ void aes128_block_tt(const uint32_t *T, const uint32_t *rk, uint32_t s0,
-                                                uint32_t s1, uint32_t s2, uint32_t s3,
-                                                uint32_t out[4]) {
-    const uint32_t *T0 = T, *T1 = T + 256, *T2 = T + 512, *T3 = T + 768, *S = T + 1024;
-    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
-#pragma unroll
-    for (int r = 1; r < 10; ++r) {
-        const uint32_t t0 = T0[s0 >> 24] ^ T1[(s1 >> 16) & 0xff] ^ T2[(s2 >> 8) & 0xff] ^ T3[s3 & 0xff] ^ rk[4 * r];
-        const uint32_t t1 = T0[s1 >> 24] ^ T1[(s2 >> 16) & 0xff] ^ T2[(s3 >> 8) & 0xff] ^ T3[s0 & 0xff] ^ rk[4 * r + 1];
-        const uint32_t t2 = T0[s2 >> 24] ^ T1[(s3 >> 16) & 0xff] ^ T2[(s0 >> 8) & 0xff] ^ T3[s1 & 0xff] ^ rk[4 * r + 2];
-        const uint32_t t3 = T0[s3 >> 24] ^ T1[(s0 >> 16) & 0xff] ^ T2[(s1 >> 8) & 0xff] ^ T3[s2 & 0xff] ^ rk[4 * r + 3];
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    out[0] = ((S[s0 >> 24] << 24) | (S[(s1 >> 16) & 0xff] << 16) | (S[(s2 >> 8) & 0xff] << 8) | S[s3 & 0xff]) ^ rk[40];
-    out[1] = ((S[s1 >> 24] << 24) | (S[(s2 >> 16) & 0xff] << 16) | (S[(s3 >> 8) & 0xff] << 8) | S[s0 & 0xff]) ^ rk[41];
-    out[2] = ((S[s2 >> 24] << 24) | (S[(s3 >> 16) & 0xff] << 16) | (S[(s0 >> 8) & 0xff] << 8) | S[s1 & 0xff]) ^ rk[42];
-    out[3] = ((S[s3 >> 24] << 24) | (S[(s0 >> 16) & 0xff] << 16) | (S[(s1 >> 8) & 0xff] << 8) | S[s2 & 0xff]) ^ rk[43];
-}
-
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void aes_ctr_tt_kernel(const uint8_t *__restrict__ cipher,
-                                                         size_t n, size_t bpc, size_t rpc,
-                                                         const uint32_t *__restrict__ rks,
-                                                         const uint32_t *__restrict__ tables,
-                                                         uint8_t *__restrict__ plain,
-                                                         uint64_t block_off, uint32_t idx_sub) {
-    __shared__ uint32_t T[5 * 256];
-    for (uint32_t e = threadIdx.x; e < 5 * 256; e += 256) T[e] = tables[e];
-    __syncthreads();
-    const size_t bpcl = (rpc + 1) / 2;
-    const size_t total = n * bpcl;
-    for (size_t g = (size_t)blockIdx.x * 256 + threadIdx.x; g < total;
-         g += (size_t)gridDim.x * 256) {
-        const size_t c = g / bpcl, b = g - c * bpcl;
-        const uint64_t ctr = (uint64_t)b + block_off;
-        uint32_t ks[4];
-        aes128_block_tt(T, rks + c * 44, 0u, 0u, (uint32_t)(ctr >> 32), (uint32_t)ctr, ks);
-        uint2 *dst = reinterpret_cast<uint2 *>(plain + c * rpc * 8) + 2 * b;
-        const bool two = 2 * b + 1 < rpc;
-        uint2 x, y = make_uint2(0, 0);
-        if (ALIGNED) {
-            const uint2 *src = reinterpret_cast<const uint2 *>(cipher + c * bpc) + 2 * b;
-            x = src[0];
-            if (two) y = src[1];
-        } else {
-            const uint8_t *src = cipher + c * bpc + 16 * b;
-            x = make_uint2(ld_u32_bytes(src), ld_u32_bytes(src + 4));
-            if (two) y = make_uint2(ld_u32_bytes(src + 8), ld_u32_bytes(src + 12));
-        }
-        dst[0] = make_uint2((x.x ^ __builtin_bswap32(ks[0])) - idx_sub, x.y ^ __builtin_bswap32(ks[1]));
-        if (two) dst[1] = make_uint2((y.x ^ __builtin_bswap32(ks[2])) - idx_sub, y.y ^ __builtin_bswap32(ks[3]));
-    }
-}
-
-static uint32_t *device_tables() {
-    std::call_once(g_tables_once, build_tables);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    if (!g_dev_tables[dev]) {
-        uint32_t *p = nullptr;
-        if (hipMalloc(&p, sizeof(g_te)) != hipSuccess) return nullptr;
-        if (hipMemcpy(p, g_te, sizeof(g_te), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
-        g_dev_tables[dev] = p;
-    }
-    return g_dev_tables[dev];
-}
-
-static bool ttable_variant() {
-    static const bool on = [] {
-        const char *e = getenv("FLTEE_AES_TTABLE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                                 size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
                                 uint64_t block_off, uint32_t idx_sub, hipStream_t s) {
     const size_t bpcl = (rec_per_client + 1) / 2;
     if (n == 0 || bpcl == 0) return hipSuccess;
     const bool aligned = bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0;
-    if (ttable_variant()) {
-        uint32_t *tables = device_tables();
-        if (!tables) return hipErrorOutOfMemory;
-        size_t blocks = (n * bpcl + 255) / 256;
-        if (blocks > 16384) blocks = 16384;
-        if (aligned)
-            hipLaunchKernelGGL(aes_ctr_tt_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
-                               cipher, n, bytes_per_client, rec_per_client, round_keys, tables,
-                               plain, block_off, idx_sub);
-        else
-            hipLaunchKernelGGL(aes_ctr_tt_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
-                               cipher, n, bytes_per_client, rec_per_client, round_keys, tables,
-                               plain, block_off, idx_sub);
-        return hipGetLastError();
-    }
     // windows of 512 counter blocks (absolute counter space) touching each client's slice
     const uint64_t wpc = (block_off + bpcl - 1) / kAesWindow4 - block_off / kAesWindow4 + 1;
     const uint64_t waves = (uint64_t)n * wpc;

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
-        // registers are then not live through the tail; FLTEE_BITONIC_TILE_LATEPF=0: A/B)
+        // registers are then not live through the tail)
         constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT;
         if (!kLate) prefetch();
         if (SORT) {
@@ -279,14 +279,13 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
             if (seg0) {
                 // the tail on every consecutive bit (top = WL - 1, what plan_network emits):
                 // compile-time rounds like the rows below; any other top: runtime rounds
-                // (bit 31: runtime rounds regardless, FLTEE_BITONIC_TAIL_CT=0, A/B)
                 const uint32_t st = (seg0 >> 8) & 0xFFFFu;
                 bool done = false;
                 // (2^12 tiles of 512 lanes; the 1024-lane 2^14 tiles are held to 128 VGPRs
                 // and spill with the tail unrolled: C5 14.82 -> 15.44 ms, so they keep
                 // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
                 if constexpr (TL != 0 && WL != 0 && MODE != 2 && NT <= 512) {
-                    if ((seg0 & 0x800000FFu) == (uint32_t)WL - 1u) {
+                    if ((seg0 & 0xFFu) == (uint32_t)WL - 1u) {
                         lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
                         done = true;
                     }
@@ -616,9 +615,13 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             // first: the prefetch registers stay free through the rounds of stages
             // log2 E + 1 .. TL - 1 (1024 lanes are held to 128 VGPRs; with the prefetch
             // live across every round the 2^14-tile kernels spilled), and stage TL's
-            // rounds still cover the load latency (FLTEE_BITONIC_SORT_LATEPF=0: A/B)
-            // (LPF 2: later still, before stage TL's last LDS round)
-            constexpr int kLast = RL + R1 - 1;  // the last round's top step (greedy split)
+            // rounds still cover the load latency (LPF 0: before the first round)
+            // LPF 2: later still, before stage TL's last LDS round.  That round is forced to
+            // a full R1-step round (steps kLast .. RL, kLast = RL + R1 - 1) and the steps
+            // above it are regrouped greedily; this is not always lds_steps_ct's own greedy
+            // split (whenever (TL - RL) % R1 != 0), but the steps still run one after the
+            // other in the same order, so the network and its output are unchanged.
+            constexpr int kLast = RL + R1 - 1;
             if constexpr (LPF == 2 && kLast < TL - 1) {
                 sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
                 lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, seed);
@@ -717,120 +720,28 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
 
 constexpr uint32_t kMaxTileLog = 14;  // 16384 records = 128 KB (+1/16 padding) of LDS
 
-// Steps per register-blocked global pass: 6 (64 records/lane; measured fastest at
-// M = 2^24, 2^27); the FLTEE_BITONIC_MAXR knob (1..6) exists for tuning runs only.
-static int max_global_r() {
-    static int r = [] {
-        const char *e = getenv("FLTEE_BITONIC_MAXR");
-        int v = e ? atoi(e) : 6;
-        return v < 1 ? 1 : (v > 6 ? 6 : v);
-    }();
-    return r;
-}
-// Largest LDS tile, log2 (13 or 14; FLTEE_BITONIC_TLOG, for A/B runs).
-static uint32_t max_tile_log() {
-    static uint32_t t = [] {
-        const char *e = getenv("FLTEE_BITONIC_TLOG");
-        int v = e ? atoi(e) : (int)kMaxTileLog;
-        return (uint32_t)(v < 11 ? 11 : (v > 14 ? 14 : v));
-    }();
-    return t;
-}
-// 2^14 tiles as 512 lanes x 32 records (5 steps per LDS round: 3 rounds per merge
-// instead of 4) instead of 1024 x 16 — A/B knob; measured no faster at M = 2^27
-// (merge 468 us either way, tile sort 2.51 vs 2.40 ms), so off by default.
-static bool tile32() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_TILE32");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-// First pass only: 512 lanes x 32 records for the 2^14 tiles (5 stages in registers,
-// 5 steps per LDS round) while the merges keep 1024 x 16 (FLTEE_BITONIC_SORT32=1, A/B).
-static bool sort32() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_SORT32");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-// Smaller tiles until there are at least 2^mt of them (FLTEE_BITONIC_MINTILES_LOG,
-// default 8 = 256 tiles, one per CU; for A/B runs).
-static uint32_t min_tiles_log() {
-    static uint32_t t = [] {
-        const char *e = getenv("FLTEE_BITONIC_MINTILES_LOG");
-        int v = e ? atoi(e) : 8;
-        return (uint32_t)(v < 0 ? 0 : (v > 12 ? 12 : v));
-    }();
-    return t;
-}
-// Narrowest strided-tile row, log2 (FLTEE_BITONIC_MINW_LOG, default 4 = 16 records =
-// 128-B row segments; smaller allows more steps per strided pass; A/B knob).
-static int min_w_log() {
-    static int w = [] {
-        const char *e = getenv("FLTEE_BITONIC_MINW_LOG");
-        int v = e ? atoi(e) : 4;
-        return v < 1 ? 1 : (v > 6 ? 6 : v);
-    }();
-    return w;
-}
-// Strided LDS passes for more than max_global_r() global steps (FLTEE_BITONIC_STRIDED=0
-// disables them, for A/B runs).
-static bool strided_passes() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_STRIDED");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-static bool knob_on(const char *name) {  // default on; "0" turns it off (A/B)
-    const char *e = getenv(name);
-    return !(e && e[0] == '0');
-}
-// compile-time LDS rounds (FLTEE_BITONIC_CT / _SORT_CT / _TILES_CT = 0: off, A/B)
-static bool merge_ct() {
-    static bool on = knob_on("FLTEE_BITONIC_CT");
-    return on;
-}
-// the planned tiles' fused tails with compile-time rounds (FLTEE_BITONIC_TAIL_CT=0: off, A/B)
-static bool tail_ct() {
-    static bool on = knob_on("FLTEE_BITONIC_TAIL_CT");
-    return on;
-}
-// the first pass's prefetch before the last stage (FLTEE_BITONIC_SORT_LATEPF=0: before
-// the first LDS round, A/B)
-// 0 = before the first round, 1 = before the last stage, 2 = before its last round;
-// default (-1): 2 for the sorts by key (C5 14.25 -> 14.21 ms), 1 for the keyed shuffle
-// (C4 9.34 vs 9.38 ms with 2; `profiles/r02/ab/sort_late_prefetch.jsonl`)
-static int sort_late_pf() {
-    static int m = [] {
-        const char *e = getenv("FLTEE_BITONIC_SORT_LATEPF");
-        return e ? atoi(e) : -1;
-    }();
-    return m;
-}
-static bool sort_ct() {
-    static bool on = knob_on("FLTEE_BITONIC_SORT_CT");
-    return on;
-}
-static bool tiles_ct() {
-    static bool on = knob_on("FLTEE_BITONIC_TILES_CT");
-    return on;
-}
-
-// the compile-time strided tiles' prefetch after their fused tail, except the tiles with
-// a tail on rows of 2^5 (their 9 row steps cover the load less well: 514 -> 553 us at
-// C5 with it late, while every other shape gains, `profiles/r02/ab/tile_late_prefetch.jsonl`)
-// FLTEE_BITONIC_TILE_LATEPF: 0 = never late, 2 = always late (A/B), default 1
-static int tile_late_pf_mode() {
-    static int m = [] {
-        const char *e = getenv("FLTEE_BITONIC_TILE_LATEPF");
-        return e ? atoi(e) : 1;
-    }();
-    return m;
-}
+// Network shape constants (compile time; the variants measured against them are in
+// profiles/r01/ab and profiles/r02/ab — the library has no runtime switches).
+// Steps per register-blocked global pass: 6 (64 records / lane; fastest at M = 2^24, 2^27).
+constexpr int kRegMaxSteps = 6;
+// Smaller tiles until there are at least 2^8 of them (one per CU).
+constexpr uint32_t kMinTilesLog = 8;
+// Narrowest strided-tile row, log2: 16 records = 128-B row segments (W = 8: 14.09 vs
+// 14.03 ms at 2^27, W = 4: 14.66, W = 2: 16.37).
+constexpr int kMinWLog = 4;
+// The first pass's prefetch of the next tile: 0 = before the first LDS round, 1 = before
+// the last stage's rounds, 2 = before that stage's last round.  2 for the sorts by key
+// (C5 14.25 -> 14.21 ms), 1 for the keyed shuffle (C4 9.34 vs 9.38 ms with 2;
+// `profiles/r02/ab/sort_late_prefetch.jsonl`).  Overridable at build time for A/B
+// libraries only (scripts/ab_build.sh).
+#ifndef FLTEE_SORT_LATEPF_KEY
+#define FLTEE_SORT_LATEPF_KEY 2
+#endif
+#ifndef FLTEE_SORT_LATEPF_SHUFFLE
+#define FLTEE_SORT_LATEPF_SHUFFLE 1
+#endif
+template <int MODE>
+constexpr int kSortLatePf = MODE == 2 ? FLTEE_SORT_LATEPF_SHUFFLE : FLTEE_SORT_LATEPF_KEY;
 
 template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
 static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
@@ -852,9 +763,12 @@ template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
-    if constexpr (TL != 0 && WL != 0 && !SORT) {
-        const int m = tile_late_pf_mode();
-        if (m == 0 || (m == 1 && WL == 5 && seg0 != 0))
+    // the compile-time strided tiles' prefetch goes after their fused tail, except for the
+    // tiles with a tail on rows of 2^5 (their 9 row steps cover the load less well: 514 ->
+    // 553 us at C5 with it late, while every other shape gains,
+    // `profiles/r02/ab/tile_late_prefetch.jsonl`)
+    if constexpr (TL != 0 && WL == 5 && !SORT) {
+        if (seg0 != 0)
             return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, false>(grid, lds, s, data, tlog, ilog, wlog,
                                                                       dtile, seed, tiles, pbase, seg0);
     }
@@ -867,30 +781,6 @@ struct TileCfg {
     unsigned tiles, grid;
     size_t lds;
 };
-static TileCfg as_e32(TileCfg c) {
-    c.E = 32;
-    c.NT = 512;
-    return c;
-}
-
-// Strided LDS passes with the direct first / last round: measured slower (A/B at 2^27:
-// 14.64 vs 14.03 ms mode 0; the last round's 8-B stores land 2^dtile apart), so off
-// unless FLTEE_BITONIC_DIRECT_STRIDED=1.
-static bool direct_strided() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_DIRECT_STRIDED");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-static bool direct_merge() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_DIRECT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // the selection sink of the last pass (see bitonic_merge_direct SEL)
 struct SelSink {
     uint32_t d = 0;
@@ -927,16 +817,11 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     } while (0)
     // contiguous tiles of the usual sizes: the LDS rounds unrolled at compile time
     if constexpr (!STRIDED) {
-        if (merge_ct()) {
-            if constexpr (E == 16 && NT == 1024) {
-                if (c.tlog == 14 && rl == 2) { BD_GO(2, 14); return hipGetLastError(); }
-            }
-            if constexpr (E == 16 && NT == 512) {
-                if (c.tlog == 13 && rl == 1) { BD_GO(1, 13); return hipGetLastError(); }
-            }
-            if constexpr (E == 32 && NT == 512) {
-                if (c.tlog == 14 && rl == 4) { BD_GO(4, 14); return hipGetLastError(); }
-            }
+        if constexpr (E == 16 && NT == 1024) {
+            if (c.tlog == 14 && rl == 2) { BD_GO(2, 14); return hipGetLastError(); }
+        }
+        if constexpr (E == 16 && NT == 512) {
+            if (c.tlog == 13 && rl == 1) { BD_GO(1, 13); return hipGetLastError(); }
         }
     }
     switch (rl) {
@@ -976,28 +861,16 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
         hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_>), dim3(grid),    \
                            dim3(NT), c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);            \
     } while (0)
-#define BS_GO(RL_, TL_)                                                                            \
-    do {                                                                                           \
-        if constexpr (TL_ != 0) {                                                                  \
-            const int lpf_ = sort_late_pf() >= 0 ? sort_late_pf() : (MODE == 2 ? 1 : 2);          \
-            if (lpf_ == 0) BS_GO_PF(RL_, TL_, 0);                                                  \
-            else if (lpf_ == 2) BS_GO_PF(RL_, TL_, 2);                                             \
-            else BS_GO_PF(RL_, TL_, 1);                                                            \
-        } else {                                                                                   \
-            BS_GO_PF(RL_, TL_, 1);                                                                 \
-        }                                                                                          \
-    } while (0)
+#define BS_GO(RL_, TL_) BS_GO_PF(RL_, TL_, ((TL_) != 0 ? kSortLatePf<MODE> : 1))
     // the usual tile sizes: every stage's LDS rounds unrolled at compile time
-    if (sort_ct()) {
-        if constexpr (E == 16 && NT == 1024) {
-            if (c.tlog == 14 && rl == 2) { BS_GO(2, 14); return hipGetLastError(); }
-        }
-        if constexpr (E == 16 && NT == 512) {
-            if (c.tlog == 13 && rl == 1) { BS_GO(1, 13); return hipGetLastError(); }
-        }
-        if constexpr (E == 8 && NT == 512) {
-            if (c.tlog == 12 && rl == 3) { BS_GO(3, 12); return hipGetLastError(); }
-        }
+    if constexpr (E == 16 && NT == 1024) {
+        if (c.tlog == 14 && rl == 2) { BS_GO(2, 14); return hipGetLastError(); }
+    }
+    if constexpr (E == 16 && NT == 512) {
+        if (c.tlog == 13 && rl == 1) { BS_GO(1, 13); return hipGetLastError(); }
+    }
+    if constexpr (E == 8 && NT == 512) {
+        if (c.tlog == 12 && rl == 3) { BS_GO(3, 12); return hipGetLastError(); }
     }
     switch (rl) {
     case 1: BS_GO(1, 0); break;
@@ -1011,57 +884,31 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     return hipGetLastError();
 }
 
-// the direct first pass (and fused producers) for 2^12-record tiles too (512 lanes x 8;
-// FLTEE_BITONIC_DIRECT_SORT8=0 turns it off, A/B)
-static bool direct_sort8() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_DIRECT_SORT8");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-static bool direct_sort() {
-    static bool on = [] {
-        const char *e = getenv("FLTEE_BITONIC_DIRECT_SORT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
                                const SelSink &sink = SelSink{}, uint32_t seg0 = 0) {
     if (c.tiles == 0) return hipSuccess;  // every tile in pad-only stage blocks
     const bool plain = seg0 == 0 && ilog != 0;  // one segment over every row bit
-    if (SORT && wlog == c.tlog && c.tlog > 6 && direct_sort()) {
-        if (c.NT == 1024 && sort32()) return launch_sort_direct<MODE, 32, 512>(as_e32(c), s, data, seed, pbase);
+    if (SORT && wlog == c.tlog && c.tlog > 6) {
         if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
-        if (c.E == 32) return launch_sort_direct<MODE, 32, 512>(c, s, data, seed, pbase);
         if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
-        if (c.NT == 512 && c.E == 8 && direct_sort8()) return launch_sort_direct<MODE, 8, 512>(c, s, data, seed, pbase);
+        if (c.NT == 512 && c.E == 8) return launch_sort_direct<MODE, 8, 512>(c, s, data, seed, pbase);
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
-    if (!SORT && plain && wlog == c.tlog && c.tlog > 6 && direct_merge()) {
+    if (!SORT && plain && wlog == c.tlog && c.tlog > 6) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
-        if (c.E == 32) return launch_direct<MODE, 32, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
         if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
     }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
     if (sink.cnt) return hipErrorNotSupported;  // only the direct contiguous merge selects
-    // strided tiles (W consecutive x 2^R rows), the same first / last round in registers
-    if (!SORT && plain && wlog < c.tlog && c.tlog > 6 && direct_strided() &&
-        (int)(c.tlog - wlog) > (c.E >= 32 ? 5 : 4)) {
-        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
-        if (c.E == 32) return launch_direct<MODE, 32, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
-        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, true>(c, s, data, ilog, wlog, dtile, seed, pbase);
-    }
+    // (strided tiles with the first / last round in registers were slower: 14.64 vs
+    // 14.03 ms at 2^27, the last round's 8-B stores land 2^dtile apart)
     // strided passes of the usual tile sizes, rows of 2^4 .. 2^7 (and, for 2^12 tiles, the
     // planned tiles' 2^8 .. 2^9, whose tails fill the consecutive bits): compile-time rounds
-    if (seg0 && !tail_ct()) seg0 |= 0x80000000u;
-    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && (1u << wlog) <= c.NT && tiles_ct() &&
+    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && (1u << wlog) <= c.NT &&
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
-        (wlog <= 7 || (seg0 && MODE != 2 && tail_ct() && c.NT <= 512))) {
+        (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512))) {
 #define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
     case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0);
         if (c.NT == 1024) {
@@ -1088,11 +935,10 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0)
     if (c.NT == 1024) BT_GO(16, 1024);
-    if (c.E == 32) BT_GO(32, 512);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
     if (c.NT == 64) BT_GO(2, 64);
-    if (!SORT && plain && wlog == c.tlog && c.E == 8 && c.tlog == 12 && tiles_ct())  // contiguous 2^12 merge
+    if (!SORT && plain && wlog == c.tlog && c.E == 8 && c.tlog == 12)  // contiguous 2^12 merge
         return launch_tiles_e<MODE, SORT, 8, 512, 12>(c.grid, c.lds, s, data, c.tlog, ilog, wlog,
                                                       dtile, seed, c.tiles, pbase);
     switch (c.E) {
@@ -1110,19 +956,18 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 // means every stage is one register pass (no tiles).
 static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
     TileCfg c{};
-    const uint32_t tmax = max_tile_log();
+    const uint32_t tmax = kMaxTileLog;
     uint32_t tlog = mlog < tmax ? mlog : tmax;
     if (tlog > slog) tlog = slog;
-    const uint32_t mt = min_tiles_log();
+    const uint32_t mt = kMinTilesLog;
     if (tlog == 14 && mlog - tlog < mt) tlog = 13;
     while (tlog > 11 && tlog <= 13 && (mlog - tlog) < mt) --tlog;  // >= 2^mt tiles
     c.tlog = tlog;
     if (tlog <= 6) return c;
     const uint32_t T = 1u << tlog;
-    if (tlog == 14) {  // FLTEE_BITONIC_TILE32=1: 512 lanes x 32 records (5 steps per round)
-        const bool e32 = tile32();
-        c.E = e32 ? 32 : 16;
-        c.NT = e32 ? 512 : 1024;
+    if (tlog == 14) {  // (512 lanes x 32 records, 5 steps per round: 15.07 vs 14.05 ms at 2^27)
+        c.E = 16;
+        c.NT = 1024;
     } else if (T >= 1024) {
         c.E = T / 512 > 16 ? 16 : T / 512;  // 512 lanes
         c.NT = 512;
@@ -1173,17 +1018,17 @@ static hipError_t stage_steps(uint64_t *data, uint32_t mlog, const TileCfg &c0, 
                               const SelSink &sink = SelSink{}, uint32_t valid = 0) {
     // a register pass of R steps runs M / 2^R lanes: keep >= 2^16 of them (256 lanes per
     // CU) down to R = 4 — at M = 2^20 (C3) R = 6 left 64 blocks of 256 for the whole chip (10.1 us for
-    // that pass; the cap, as FLTEE_BITONIC_MAXR=4 there: 0.1894 vs 0.1916 ms per aggregate)
+    // that pass; the cap, as R = 4 there: 0.1894 vs 0.1916 ms per aggregate)
     const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
-    const int kMaxGlobalR = max_global_r() < rcap ? max_global_r() : rcap;
+    const int kMaxGlobalR = kRegMaxSteps < rcap ? kRegMaxSteps : rcap;
     const uint32_t skip = g_pad_skip ? skip_from(valid, ilog, mlog) : 0u;
     const TileCfg c = live_tiles(c0, skip);
     const uint32_t tlog = c.tlog, T = 1u << tlog;
-    const int rs = (int)tlog - min_w_log();  // global steps per strided LDS pass (W >= 2^min_w_log)
+    const int rs = (int)tlog - kMinWLog;  // global steps per strided LDS pass (W >= 2^kMinWLog)
     const int nglobal = jtop - (int)tlog + 1;  // steps with j >= T
     hipError_t e;
     if (nglobal > 0) {
-        const int per = (strided_passes() && rs > kMaxGlobalR) ? rs : kMaxGlobalR;
+        const int per = rs > kMaxGlobalR ? rs : kMaxGlobalR;
         const int passes = (nglobal + per - 1) / per;
         for (int p = 0; p < passes; ++p) {
             const int left = jtop - (int)tlog + 1;
@@ -1227,13 +1072,8 @@ struct NetPass {
     uint32_t stage = 0;                  // the last stage the launch touches (pad skip)
 };
 
-static bool plan_enabled() {
-    static bool on = knob_on("FLTEE_BITONIC_PLAN");
-    return on;
-}
-
 static std::vector<NetPass> plan_network(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax) {
-    const uint32_t minw = (uint32_t)min_w_log();
+    const uint32_t minw = (uint32_t)kMinWLog;
     uint32_t ntl = 0;
     while ((1u << (ntl + 1)) <= NT) ++ntl;  // log2 NT: W <= NT for strided tiles
     // relative launch costs (MI355X rocprof, `profiles/r02/`): register passes R <= 4 one
@@ -1353,9 +1193,9 @@ static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t 
     // more VALU (the hash multiply), which the planned tile-heavy schedule pays in LDS
     // passes — C4: 10.15 vs 9.78 ms planned, against C5 (mode 0) 14.67 vs 15.34 ms and C3
     // 0.157 vs 0.163 ms (`profiles/r02/ab/network_plan.jsonl`)
-    if (MODE == 2 || !plan_enabled() || c0.tlog <= 6 || mlog <= c0.tlog) return false;
+    if (MODE == 2 || c0.tlog <= 6 || mlog <= c0.tlog) return false;
     const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
-    const int rmax = max_global_r() < rcap ? max_global_r() : rcap;
+    const int rmax = kRegMaxSteps < rcap ? kRegMaxSteps : rcap;
     const std::vector<NetPass> &plan = cached_plan(mlog, c0.tlog, c0.NT, rmax);
     if (plan.empty()) return false;
     e = hipSuccess;
@@ -1479,8 +1319,8 @@ hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t 
 // ------------------------------------------- sorts with a fused producer ---
 // The sort of the padded array that `g` describes (GEN 1: advanced's, 2: nips19's),
 // written into data[0, m): the producer runs inside the first pass's loads.
-// hipErrorNotSupported when that pass is not the direct tile sort (small m, knob
-// off): the caller then builds the array and sorts it.
+// hipErrorNotSupported when that pass is not the direct tile sort (small m, fused
+// init off): the caller then builds the array and sorts it.
 static bool g_fused_init = true;  // fltee_debug_set_fused_init (A/B)
 void set_fused_init(int on) { g_fused_init = on != 0; }
 
@@ -1489,8 +1329,7 @@ void set_fused_init(int on) { g_fused_init = on != 0; }
 static bool last_pass_is_direct_merge(size_t m) {
     const uint32_t mlog = log2_pow2(m);
     const TileCfg c = make_cfg(mlog, mlog);
-    return c.tlog > 6 && mlog > c.tlog && direct_merge() &&
-           (c.NT == 1024 || c.E == 32 || (c.NT == 512 && c.E == 16));
+    return c.tlog > 6 && mlog > c.tlog && (c.NT == 1024 || (c.NT == 512 && c.E == 16));
 }
 
 template <int MODE, int GEN>
@@ -1499,7 +1338,7 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     if (!g_fused_init || m < 2 || m > ((size_t)1 << 29)) return hipErrorNotSupported;
     const uint32_t mlog = log2_pow2(m);
     const TileCfg c0 = make_cfg(mlog, mlog);
-    if (c0.tlog <= 6 || !direct_sort()) return hipErrorNotSupported;
+    if (c0.tlog <= 6) return hipErrorNotSupported;
     if (sink.cnt && !last_pass_is_direct_merge(m)) return hipErrorNotSupported;
     // the padded array's records (advanced: records ++ initial entries; nips19: records ++
     // dummies); past them only (u32::MAX, +0.0) pads
@@ -1512,11 +1351,9 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     gp.pad_begin = (uint32_t)done;
     gp.pad_n = (uint32_t)(m - done);
     hipError_t e;
-    if (c.NT == 1024 && sort32()) e = launch_sort_direct<MODE, 32, 512, GEN>(as_e32(c), s, data, seed, 0u, gp);
-    else if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, gp);
-    else if (c.E == 32) e = launch_sort_direct<MODE, 32, 512, GEN>(c, s, data, seed, 0u, gp);
+    if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, gp);
     else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, gp);
-    else if (c.NT == 512 && c.E == 8 && direct_sort8()) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, gp);
+    else if (c.NT == 512 && c.E == 8) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, gp);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
     if (run_plan<MODE>(data, mlog, c0, seed, 0u, s, sink, valid, e)) return e;
@@ -1597,7 +1434,7 @@ hipError_t bitonic_steps_range(uint64_t *data, size_t m, uint32_t mode, uint32_t
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
     const uint32_t mlog = log2_pow2(m);
     if (jtop >= mlog || jbot > jtop || jtop >= ilog) return hipErrorInvalidValue;
-    const int kMaxGlobalR = max_global_r();
+    const int kMaxGlobalR = kRegMaxSteps;
     int top = (int)jtop;
     while (top >= (int)jbot) {
         const int left = top - (int)jbot + 1;

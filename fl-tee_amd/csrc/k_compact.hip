@@ -157,14 +157,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
 // for 6 waves per SIMD (launch_bounds' 2nd argument = min waves per EU: <= 80 VGPRs).
 // A/B at C5: 497 vs 534 us per middle pass, 499 vs 570 us for the last; the first pass
 // (more live state) spills at that bound (868 vs 751 us), so it keeps 2.
-// FLTEE_COMPACT_BLOCKS=2: two for every pass.
-static int compact_blocks() {
-    static int b = [] {
-        const char *e = getenv("FLTEE_COMPACT_BLOCKS");
-        return e && e[0] == '2' ? 2 : 3;
-    }();
-    return b;
-}
+constexpr int kCompactBlocks = 3;
 // fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB tiles
 // (1024 lanes x 8), 2 = 32 KiB first pass + 64 KiB strided passes (1024 lanes x 8, one
 // block per CU: 6 levels per pass, 4 passes instead of 5 at C5; 512 x 16 spills)
@@ -235,7 +228,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const int fin = last ? (accumulate ? 2 : 1) : 0;
         net_account((uint64_t)(last ? 8 : 16) * L);
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
-        const int blk = j0 == 0 ? 2 : compact_blocks();
+        const int blk = j0 == 0 ? 2 : kCompactBlocks;
         const unsigned res = small ? 256u * (unsigned)blk : 256u;
         const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =

@@ -185,12 +185,6 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 
 size_t fold_context(size_t halo) { return (halo + FS_W - 1) / FS_W * FS_W; }
 
-// A/B knobs (read once per process; 0 = the measured default)
-static int fold_knob(const char *name) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : 0;
-}
-
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
                              uint32_t *status, hipStream_t s) {
@@ -206,21 +200,18 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     // one doubling more while >= 1024 waves remain: less halo re-read (C5: 2048 instead
     // of 1024, 620 vs 643 us; 4096: 700 us, 8192: 1220 us — too few waves in flight)
     if (C >= Hr && span / (64 * 2 * C) >= 1024) C <<= 1;
-    static const int clog = fold_knob("FLTEE_FOLD_CLOG");  // A/B: chunks of 2^clog records
-    if (clog >= 4 && clog <= 20) C = (size_t)1 << clog;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     net_account((uint64_t)16 * span);
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    int depth = blocks <= 256 ? 2 : 1;  // about one wave per CU: latency-bound, prefetch deeper
-    static const int dk = fold_knob("FLTEE_FOLD_DEPTH");
-    if (dk == 1 || dk == 2 || dk == 4) depth = dk;
+    // about one wave per CU: latency-bound, prefetch deeper (2 or 4 stages were no faster
+    // on the large arrays, profiles/r01/ab/fold_chunk_depth*.jsonl)
+    const int depth = blocks <= 256 ? 2 : 1;
 #define FS_GO(D_)                                                                                  \
     hipLaunchKernelGGL(fold_stream_kernel<D_>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,   \
                        (long long)m, (long long)origin, (long long)end, pbase, (long long)fold_len, \
                        (uint32_t)Hr, (uint32_t)C, status)
-    if (depth == 4) FS_GO(4);
-    else if (depth == 2) FS_GO(2);
+    if (depth == 2) FS_GO(2);
     else FS_GO(1);
 #undef FS_GO
     return hipGetLastError();

@@ -226,6 +226,15 @@ class DistRanks:
 
     def __init__(self, rank, world):
         self.rank, self.world = rank, world
+        self._ready = False
+
+    def ensure_init(self):
+        """One full-group collective before the first batched P2P: with RCCL the first
+        batch_isend_irecv of a group must include every rank, and pad skipping leaves
+        the ranges past the live bound out of a pairwise stage."""
+        if not self._ready:
+            dist.barrier()
+            self._ready = True
 
     @staticmethod
     def _run(ops):
@@ -332,6 +341,8 @@ def distributed_network(chunks, world, M, ops, comm, mode=0, seed=0, exchange="t
     clog, mlog = C.bit_length() - 1, M.bit_length() - 1
     assert 1 << clog == C and 1 << mlog == M
     vbound = M if valid is None else min(int(valid), M)
+    if hasattr(comm, "ensure_init"):
+        comm.ensure_init()  # every rank enters here; later stages may skip some ranks
 
     def live_from(stage):
         blk = 1 << stage

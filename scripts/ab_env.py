@@ -1,9 +1,9 @@
-"""A/B of the build-time knobs that are read once per process (FLTEE_BITONIC_* env
-variables): one child process per variant, each timing bench.bench_workload.  The parent
-never touches the GPU.  One JSON line per (workload, variant, repeat).
+"""A/B of library builds: one child process per variant (environment assignments, usually
+FLTEE_LIB=<an A/B build from scripts/ab_build.sh>), each timing bench.bench_workload.  The
+parent never touches the GPU.  One JSON line per (workload, variant, repeat).
 
-    python scripts/ab_env.py c3 'FLTEE_BITONIC_MINTILES_LOG=7' 'FLTEE_BITONIC_MINTILES_LOG=9'
-(the empty variant, the defaults, always runs first and last)."""
+    python scripts/ab_env.py c5 FLTEE_LIB=fl-tee_amd/lib/ab/libfltee_agg_x.so
+(the empty variant, the product library, always runs first and last)."""
 import json
 import os
 import subprocess

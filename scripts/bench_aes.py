@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the AES-128-CTR decrypt kernels in one process per variant
-(FLTEE_AES_TTABLE=1 selects the round-1 T-table kernel, default the bitsliced one).
-Prints one JSON line per shape: kernel ms (HIP events around one decrypt call,
+"""Timing of the AES-128-CTR decrypt kernel (bitsliced, constant time; the library has
+no other variant since round 3 — the round-2 A/B against the T-table kernel is in
+profiles/r02/ab/aes_variants.jsonl).  Prints one JSON line per shape: kernel ms (HIP events around one decrypt call,
 best of K) and GB/s of ciphertext read + records written."""
 import json
 import os
@@ -17,8 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "fl-tee_amd"))
 def main():
     import torch
     from fltee import device as D
-    variant = ("ttable" if os.environ.get("FLTEE_AES_TTABLE", "0") != "0" else
-               "bitsliced32" if os.environ.get("FLTEE_AES_BS") == "32" else "bitsliced4")
+    variant = "bitsliced4"
     shapes = [("ns 100 x 1M dense", 100, 1_000_000), ("c3 100 x 5089 sparse", 100, 5089),
               ("c5 1000 x 100K sparse", 1000, 100_000)]
     for name, n, rpc in shapes:

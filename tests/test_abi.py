@@ -43,9 +43,34 @@ def test_library_exports_every_declared_symbol():
     assert set(names) <= exported
 
 
+def source_hash():
+    """sha256 of fl-tee_amd/csrc/* (file-name order) + include/fltee_agg.h, first 16 hex
+    digits: what fl-tee_amd/Makefile embeds in fltee_version()."""
+    import hashlib
+    csrc = os.path.join(ROOT, "fl-tee_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(csrc)):
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    with open(HEADER, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def test_version_string():
     from fltee import _lib as L
     assert b"gfx950" in L.lib().fltee_version()
+
+
+def test_library_built_from_these_sources():
+    """Provenance: the loaded libfltee_agg.so was built from the tree's own sources (a
+    product build: no A/B tune flags)."""
+    from fltee import _lib as L
+    v = L.lib().fltee_version().decode()
+    if os.environ.get("FLTEE_LIB"):
+        return  # an A/B build loaded on purpose
+    assert f"src={source_hash()} " in v + " ", f"stale library: {v} vs sources {source_hash()}"
+    assert v.endswith("tune="), v
 
 
 def test_device_aes_tables_fips197():

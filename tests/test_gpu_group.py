@@ -148,3 +148,23 @@ def test_group_ragged_payload(enclaves, oracle, alg):
     one = run(enclaves[1], c, alg, enc)
     for w in (2, 8):
         assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, alg, enc).view(np.uint32))
+
+
+@pytest.mark.parametrize("w", [2, 8])
+def test_group_nips19_declined_shape_same_seed(enclaves, oracle, w):
+    """A nips19 shape the group declines (C = M / W < 64: group.hip's fallback to the root
+    path) draws the call's seed once, like one GPU: under fltee_debug_set_seed both eids
+    give the same Laplace counts, shuffle and DP-free sum."""
+    rng = np.random.default_rng(w)
+    n, k, d = 4, 4, 16
+    ids = np.arange(300, 300 + n, dtype=np.uint32)
+    recs = []
+    for _ in range(n):
+        r = np.zeros(k, dtype=oracle.WEIGHT)
+        r["idx"] = rng.permutation(d)[:k]
+        r["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        recs.append(r)
+    enc = oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
+    c = dict(client_ids=ids, d=d, k=k, n=n, name=f"tiny_nips19_{w}")
+    one = run(enclaves[1], c, 2, enc)
+    assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, 2, enc).view(np.uint32))
