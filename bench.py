@@ -114,12 +114,15 @@ def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False):
     net = net_stats(torch, lambda: step(0))
     del recs
     return dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
-                rate=n * kk / kern, bytes=n * kk * 8 + d * 4, nbuf=nbuf, net=net)
+                rate=n * kk / kern, bytes=algorithmic_bytes(w), nbuf=nbuf, net=net)
 
 
-def net_stats(torch, call):
+def net_stats(torch, call, reps=3):
     """Streaming passes one aggregate launches and the bytes they sweep (the library's
-    launch-side accounting: read + write of the array per pass)."""
+    launch-side accounting: read + write of the live part of the array per pass, pad-only
+    blocks excluded), and per kernel: launches, bytes and time, each launch timed live by
+    an event the launcher records on its stream before it (fltee_debug_net_timing; the
+    last launch up to a final event).  Best of `reps` aggregates per kernel."""
     from fltee import _lib as L
     lib = L.lib()
     a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
@@ -127,24 +130,70 @@ def net_stats(torch, call):
     call()
     torch.cuda.synchronize()
     lib.fltee_debug_net_stats(ctypes.byref(a), ctypes.byref(b), 1)
-    return dict(passes=a.value, bytes=b.value)
+    res = dict(passes=a.value, bytes=b.value)
+    best = {}
+    stream = torch.cuda.current_stream()
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        lib.fltee_debug_net_timing(1, None)
+        call()
+        lib.fltee_debug_net_timing(0, ctypes.c_void_p(stream.cuda_stream))
+        torch.cuda.synchronize()
+        per = {}
+        name = ctypes.create_string_buffer(64)
+        nb, ms = ctypes.c_uint64(0), ctypes.c_float(0)
+        n = lib.fltee_debug_net_log(0, None, 0, None, None)
+        for i in range(n):
+            lib.fltee_debug_net_log(i, name, 64, ctypes.byref(nb), ctypes.byref(ms))
+            k = per.setdefault(name.value.decode(), dict(launches=0, bytes=0, ms=0.0))
+            k["launches"] += 1
+            k["bytes"] += nb.value
+            k["ms"] += ms.value
+        for k, v in per.items():
+            if k not in best or v["ms"] < best[k]["ms"]:
+                best[k] = v
+    res["kernels"] = best
+    return res
 
 
-def dominant_kernel(name):
-    """The kernel with the largest total time in the committed rocprofv3 summary of this
-    config (profiles/r02/<name>_kernel_stats.csv), or None."""
+def dominant_kernel(net):
+    """The kernel with the largest total time in one aggregate (live event timing), its
+    bytes per launch (launch-side, pad-aware) and the rate they imply."""
+    if not net.get("kernels"):
+        return None
+    name, k = max(net["kernels"].items(), key=lambda kv: kv[1]["ms"])
+    per_launch_ms = k["ms"] / k["launches"]
+    bpl = k["bytes"] / k["launches"]
+    gbs = bpl / (per_launch_ms * 1e-3) / 1e9
+    return dict(kernel=name, launches=k["launches"], bytes_per_launch=bpl, avg_us=per_launch_ms * 1e3,
+                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS, share_of_aggregate=None)
+
+
+def rocprof_kernel(name, kernel):
+    """Average duration of `kernel` in the committed rocprofv3 summary of this config
+    (profiles/r03/<name>_kernel_stats.csv), for the cross-check, or None."""
     import csv
-    path = os.path.join(ROOT, "profiles", "r02", f"{name}_kernel_stats.csv")
+    path = os.path.join(ROOT, "profiles", "r03", f"{name}_kernel_stats.csv")
     try:
         with open(path) as f:
-            rows = [r for r in csv.DictReader(f) if "fltee::" in r["Name"]]
+            rows = [r for r in csv.DictReader(f) if f"fltee::{kernel}" in r["Name"]]
     except (OSError, KeyError):
         return None
     if not rows:
         return None
-    r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
-    return dict(kernel=r["Name"].split("(")[0], calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
-                source=os.path.relpath(path, ROOT))
+    calls = sum(int(r["Calls"]) for r in rows)
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    return dict(calls=calls, avg_us=tot / calls / 1e3, source=os.path.relpath(path, ROOT))
+
+
+def algorithmic_bytes(w):
+    """n*k*8 + d*4 (advanced and the flat algorithms), nips19 adds the d*floor(T)
+    dummies: (n*k + d*floor(T))*8 + d*4."""
+    n, d, k = w["n"], w["d"], w["k"] or w["d"]
+    if w["alg"] == 2:
+        T = np.float32(2 * k) / np.float32(100.0) * np.float32(np.log(np.float32(d) * np.float32(n)))
+        return (n * k + d * int(T)) * 8 + d * 4
+    return n * k * 8 + d * 4
 
 
 def network_records(w):
@@ -356,6 +405,75 @@ def bench_reference_configs(torch, D, device, steps=3):
     return dict(config="d=50890 (MLP-MNIST), k=5089, n=3000 (num_users=10000, ratio 0.3)", **res)
 
 
+# The reference's headline table: exp/results/exp5.csv column 13 (`execution_time`, the host
+# wall time of one Aggregate ECALL, server.rs:140,184-186), driven by exp/exp5.sh:8-48 (frac
+# 0.3, --local_skip, --secure_agg); means over the csv's rows per configuration (5 runs, path_oram
+# 1-2).  d = the model's parameter count, k = int(alpha * d) (fl_main.py:100-101), n =
+# int(0.3 * num_users) sampled clients.
+EXP5_MODELS = {"mnist": 50890, "purchase100": 44964}  # MLP (models.py:5-30): 784/600-64-10/100
+EXP5_REF_S = {  # (dataset, num_users, alpha) -> {alg: mean execution_time, s}
+    ("mnist", 10, 0.1): dict(advanced=0.07196, baseline=0.05707, non_oblivious=0.001405, path_oram=50.35),
+    ("mnist", 100, 0.1): dict(advanced=0.1513, baseline=0.5099, non_oblivious=0.003197, path_oram=154.8),
+    ("mnist", 1000, 0.1): dict(advanced=2.7725, baseline=5.0185, non_oblivious=0.02831, path_oram=1193.7),
+    ("mnist", 10000, 0.1): dict(advanced=287.11, baseline=52.545, non_oblivious=2.5101, path_oram=11962.5),
+    ("mnist", 10, 0.01): dict(advanced=0.03041, baseline=0.007275, non_oblivious=0.001159, path_oram=39.56),
+    ("mnist", 100, 0.01): dict(advanced=0.06289, baseline=0.05274, non_oblivious=0.001349, path_oram=50.00),
+    ("mnist", 1000, 0.01): dict(advanced=0.13796, baseline=0.50328, non_oblivious=0.003354, path_oram=153.9),
+    ("mnist", 10000, 0.01): dict(advanced=2.6671, baseline=5.1964, non_oblivious=0.03055, path_oram=1233.7),
+    ("purchase100", 100, 0.1): dict(advanced=0.1389, baseline=0.3720, non_oblivious=0.002756, path_oram=139.36),
+    ("purchase100", 100, 0.01): dict(advanced=0.03011, baseline=0.03767, non_oblivious=0.001180, path_oram=44.22),
+}
+EXP5_ALGS = {"advanced": 1, "baseline": 3, "non_oblivious": 4, "path_oram": 5}
+
+
+def bench_exp5(torch, D, device, reps=5):
+    """ecall_secure_aggregation host-inclusive, as exp5 measures it (the host wall time of
+    one ECALL: H2D of the ciphertext, GPU AES-CTR, aggregation, D2H of f32[d]), on every
+    exp5.csv configuration of the MLP models, beside the reference's published mean.
+    Payloads: n clients x k distinct random indices, N(0, 0.01) values, encrypted with the
+    clients' session keys (CTR: the library's own kernel), in pageable host memory."""
+    from fltee.ecalls import Enclave
+    E = Enclave(device.index or 0)
+    rows = []
+    fl = 9000
+    try:
+        for (ds, users, alpha), refs in EXP5_REF_S.items():
+            d = EXP5_MODELS[ds]
+            k = int(alpha * d)
+            n = max(int(0.3 * users), 1)
+            ids = np.arange(1, n + 1, dtype=np.uint32)
+            g = torch.Generator(device=device).manual_seed(users * 7 + k)
+            idx = torch.argsort(torch.rand(n, d, generator=g, device=device), dim=1)[:, :k].to(torch.int64)
+            vals = torch.randn(n, k, generator=g, device=device) * 0.01
+            rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
+            cipher = torch.empty_like(rec)
+            D.decrypt(ids, rec, k * 8, cipher)  # CTR: encryption == decryption
+            host = cipher.cpu().numpy().view(np.uint8)
+            del idx, vals, rec, cipher
+            for alg, ref_s in refs.items():
+                fl += 1
+                a = EXP5_ALGS[alg]
+                assert E.ecall_fl_init(fl, ids, d, k, 1.12, 1.0, alpha, 1.0, a, 0, 0) == (0, 0)
+                walls = []
+                for r in range(reps + 1):
+                    assert E.ecall_start_round(fl, r, n)[:2] == (0, 0)
+                    t0 = time.perf_counter()
+                    st, rv, out, tt = E.ecall_secure_aggregation(fl, r, ids, host, d, k, a)
+                    wall = time.perf_counter() - t0
+                    assert (st, rv) == (0, 0), (alg, st, rv)
+                    if r:  # the first call grows the staging buffers
+                        walls.append(wall)
+                t = float(np.mean(walls))
+                rows.append(dict(dataset=ds, num_users=users, alpha=alpha, n=n, d=d, k=k, alg=alg,
+                                 ms=t * 1e3, ref_ms=ref_s * 1e3, speedup=ref_s / t,
+                                 value=n * k / t, unit="client-params/s"))
+    finally:
+        E.destroy()
+    return dict(metric="execution_time of one Aggregate ECALL (host wall, server.rs:184-186), "
+                       "mean of %d calls after one warm-up" % reps,
+                source="reference: exp/results/exp5.csv col 13 means (exp/exp5.sh:8-48)", rows=rows)
+
+
 def bench_next_rows(torch, D, device, steps=5):
     """SURVEY §8f rows on one GPU, device-resident: the GPU AES-128-CTR decrypt of the
     headline payload (lib.rs:312-343) and the client-side producers (utils.py:327-354,
@@ -514,12 +632,19 @@ def cpu_baseline_configs(gpu_ms):
     ks = k // 8
     Ms = O.next_pow2(n * k + d * int(O.nips19_threshold(d, ks, n)))
     M = O.next_pow2(n * k + d * int(O.nips19_threshold(d, k, n)))
+    # the reference's own shuffle: the running FxHash of heap addresses (nips19.rs:66-105,
+    # fo_shuffle_fxhash); the keyed comparator the GPU and the oracle share is timed beside it
+    t0 = time.perf_counter()
+    O.nips19(ks, w, d, n, seed=7, reference_shuffle=True)
+    ts = time.perf_counter() - t0
     t0 = time.perf_counter()
     O.nips19(ks, w, d, n, seed=7)
-    ts = time.perf_counter() - t0
-    row("c4", n, k, ts * _net_cost(M) / _net_cost(Ms),
-        f"nips19 with request k = {ks} (M = {Ms} instead of {M}): {ts:.2f} s measured, "
-        f"x{_net_cost(M) / _net_cost(Ms):.2f} (compare-exchange ratio)", measured_s=ts, M=M)
+    tk = time.perf_counter() - t0
+    scale = _net_cost(M) / _net_cost(Ms)
+    row("c4", n, k, ts * scale,
+        f"nips19 (the reference's FxHash-of-addresses shuffle network) with request k = {ks} "
+        f"(M = {Ms} instead of {M}): {ts:.2f} s measured, x{scale:.2f} (compare-exchange ratio)",
+        measured_s=ts, M=M, keyed_shuffle_cpu_s=tk * scale, keyed_shuffle_measured_s=tk)
     # configs[4] (C5): advanced, 1000 x 100K over d = 10M (M = 2^27) — 1/16 of d and k
     n, d, k = 1000, 10_000_000, 100_000
     ns_, ds, ks = 1000, d // 16, k // 16
@@ -812,19 +937,29 @@ def main():
                 M = network_records(wl)
                 if M:  # the oblivious paths: their network traffic, not the useful bytes
                     nb = r["net"]["bytes"]
+                    alg_b = algorithmic_bytes(wl)
                     roof = dict(bound="hbm", network_passes=r["net"]["passes"], network_bytes=nb,
                                 network_records=M,
                                 achieved=nb / r["kernel_s"] / 1e9, peak=HBM_PEAK_GBS, unit="GB/s",
                                 frac=nb / r["kernel_s"] / 1e9 / HBM_PEAK_GBS,
-                                algorithmic_bytes=r["bytes"],
-                                note="network bytes = read + write of the array per streaming pass "
-                                     "(launch-side accounting); achieved = those bytes / the "
-                                     "aggregate's event time")
-                    dk = dominant_kernel(name)
+                                algorithmic_bytes=alg_b,
+                                algorithmic_gbs=alg_b / r["kernel_s"] / 1e9,
+                                note="network bytes = read + write of the live (not pad-only) part "
+                                     "of the array per streaming pass (launch-side accounting); "
+                                     "achieved = those bytes / the aggregate's event time; "
+                                     "algorithmic bytes per SURVEY 8(d)")
+                    dk = dominant_kernel(r["net"])
                     if dk:
-                        dk["bytes_per_launch"] = 16 * M
-                        dk["achieved_gbs"] = 16 * M / (dk["avg_us"] * 1e-6) / 1e9
+                        dk["share_of_aggregate"] = dk["avg_us"] * dk["launches"] / (r["kernel_s"] * 1e6)
+                        rp = rocprof_kernel(name, dk["kernel"])
+                        if rp:
+                            dk["rocprof"] = rp
+                        tr = traffic_from_profiles(f"{name}:{dk['kernel']}")
+                        dk["traffic"] = tr
+                        if tr:
+                            dk["traffic_over_launch_bytes"] = tr / dk["bytes_per_launch"]
                         roof["dominant_kernel"] = dk
+                    roof["kernels"] = r["net"]["kernels"]
                     extra[name]["roofline"] = roof
             line["extra"] = extra
             # the metric's literal configuration (100 clients x MLP-MNIST, dense baseline),
@@ -847,6 +982,7 @@ def main():
                 gms = {nm: e["kernel_ms"] for nm, e in extra.items()}
                 line["cpu_baseline_configs"] = cpu_baseline_configs(gms)
             line["reference_configs"] = bench_reference_configs(torch, D, device)
+            line["exp5"] = bench_exp5(torch, D, device)
             line["next_rows"] = bench_next_rows(torch, D, device)
         if sharded is not None:
             with lock:

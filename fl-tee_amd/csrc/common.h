@@ -70,9 +70,12 @@ static inline uint32_t log2_pow2(size_t x) {
 namespace fltee {
 
 // Measurement: HBM bytes the streaming passes of the networks move (algorithmic per
-// launch: read + write of the array they sweep), counted at launch on the host
-// (engine.hip; read by bench.py through fltee_debug_net_stats).
-void net_account(uint64_t bytes);
+// launch: read + write of the live part of the array they sweep — pad-only blocks a
+// launch skips are not counted), counted at launch on the host (engine.hip; read by
+// bench.py through fltee_debug_net_stats).  Called once per launch, before it, with the
+// kernel's name: with fltee_debug_net_timing on, an event recorded there on `s` times
+// each launch (the gap to the next accounted launch or the final event).
+void net_account(uint64_t bytes, const char *kernel, hipStream_t s);
 
 // k_accumulate.hip
 hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,

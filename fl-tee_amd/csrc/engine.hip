@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 #include "engine.h"
@@ -43,9 +44,31 @@ static std::atomic<uint64_t> g_debug_seed{0};
 static std::atomic<uint64_t> g_seed_calls{0};
 
 static std::atomic<uint64_t> g_net_launches{0}, g_net_bytes{0};
-void net_account(uint64_t bytes) {
+struct NetLaunch {
+    const char *kernel;  // nullptr: the final event
+    uint64_t bytes;
+    hipEvent_t ev;
+};
+static std::mutex g_net_mu;
+static std::vector<NetLaunch> g_net_log;
+static std::atomic<bool> g_net_timing{false};
+constexpr size_t kNetLogCap = 16384;
+
+void net_account(uint64_t bytes, const char *kernel, hipStream_t s) {
     g_net_launches.fetch_add(1, std::memory_order_relaxed);
     g_net_bytes.fetch_add(bytes, std::memory_order_relaxed);
+    if (!g_net_timing.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> lk(g_net_mu);
+    if (g_net_log.size() >= kNetLogCap) return;
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    if (hipEventRecord(e, s) != hipSuccess) { (void)hipEventDestroy(e); return; }
+    g_net_log.push_back({kernel, bytes, e});
+}
+
+static void net_log_clear() {
+    for (auto &r : g_net_log) (void)hipEventDestroy(r.ev);
+    g_net_log.clear();
 }
 
 uint64_t next_seed() {
@@ -705,6 +728,47 @@ extern "C" void fltee_debug_net_stats(uint64_t *launches, uint64_t *bytes, int r
         fltee::g_net_launches.store(0);
         fltee::g_net_bytes.store(0);
     }
+}
+
+// measurement hook: per-launch log of the accounted launches.  on = 1 clears the log and
+// starts recording (an event on the launch's stream before each accounted launch); on = 0
+// records the final event on `stream` (after the last launch of the timed call) and stops.
+extern "C" void fltee_debug_net_timing(int on, void *stream) {
+    std::lock_guard<std::mutex> lk(fltee::g_net_mu);
+    if (on) {
+        fltee::net_log_clear();
+        fltee::g_net_timing.store(true);
+        return;
+    }
+    fltee::g_net_timing.store(false);
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) == hipSuccess) {
+        if (hipEventRecord(e, (hipStream_t)stream) == hipSuccess)
+            fltee::g_net_log.push_back({nullptr, 0, e});
+        else
+            (void)hipEventDestroy(e);
+    }
+}
+
+// entry i of the log (the caller has synchronised the stream): kernel name, launch-side
+// bytes and the time to the next entry's event (ms).  Returns the number of launches
+// logged (the final event not counted); i past it fills nothing.
+extern "C" size_t fltee_debug_net_log(size_t i, char *name, size_t name_cap, uint64_t *bytes,
+                                      float *ms) {
+    std::lock_guard<std::mutex> lk(fltee::g_net_mu);
+    const auto &L = fltee::g_net_log;
+    const size_t nl = L.empty() ? 0 : (L.back().kernel ? L.size() : L.size() - 1);
+    if (i < nl) {
+        if (name && name_cap) {
+            std::snprintf(name, name_cap, "%s", L[i].kernel ? L[i].kernel : "");
+        }
+        if (bytes) *bytes = L[i].bytes;
+        if (ms) {
+            *ms = -1.0f;
+            if (i + 1 < L.size()) (void)hipEventElapsedTime(ms, L[i].ev, L[i + 1].ev);
+        }
+    }
+    return nl;
 }
 
 extern "C" fltee_status_t fltee_sum_rows_device(const float *d_rows, size_t nrows, size_t d,

@@ -33,6 +33,19 @@
 
 #include "common.h"
 
+// A/B switches of the tile kernels' code shape (compile time; scripts/ab_build.sh):
+//   FLTEE_CE_BATCH   a step's swap decisions all computed before its selects
+//   FLTEE_LDS_BATCH  groups per batch of a round's LDS reads issued before their
+//                    compare-exchanges and writes (0: all of the lane's groups)
+#ifndef FLTEE_CE_BATCH
+#define FLTEE_CE_BATCH 1
+#endif
+#ifndef FLTEE_LDS_BATCH
+#define FLTEE_LDS_BATCH 0
+#endif
+template <int G>
+constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FLTEE_LDS_BATCH;
+
 namespace fltee {
 
 // cond2 of the compare-exchange at position l (see the header comment)
@@ -49,6 +62,15 @@ __device__ __forceinline__ uint32_t spread(uint32_t g, uint32_t d, uint32_t r) {
     return ((g >> d) << (d + r)) | lo;
 }
 
+// The seed of the keyed comparator, re-defined at the top of each tile iteration: its
+// step keys (a few SALU each, shuffle_step_key) are then computed inside the loop next to
+// their use instead of all being hoisted out of it (the ~100 keys of a first pass held
+// in SGPRs across the loop spilled SGPRs and VGPRs).
+__device__ __forceinline__ uint32_t loop_seed(uint32_t seed) {
+    asm volatile("" : "+s"(seed));
+    return seed;
+}
+
 // Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
 // records held in v[], whose first record sits at global position p0.  The group
 // spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
@@ -60,6 +82,26 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 #pragma unroll
     for (int lv = R - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
+#if FLTEE_CE_BATCH
+        // every swap decision of the step first, then the selects: the compares are
+        // independent, so their mask chains (v_cmp -> s_xor -> v_cndmask) overlap
+        bool sw[(1 << R) / 2];
+#pragma unroll
+        for (int q = 0, k = 0; q < (1 << R); ++q) {
+            if (q & (1 << lv)) continue;
+            const int qm = q | (1 << lv);
+            sw[k++] = asc ^ cond2<MODE>(v[q], v[qm], p0 + ((uint32_t)q << dlog), key);
+        }
+#pragma unroll
+        for (int q = 0, k = 0; q < (1 << R); ++q) {
+            if (q & (1 << lv)) continue;
+            const int qm = q | (1 << lv);
+            const uint64_t a = v[q], c = v[qm];
+            const bool s = sw[k++];
+            v[q] = s ? c : a;
+            v[qm] = s ? a : c;
+        }
+#else
 #pragma unroll
         for (int q = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
@@ -69,6 +111,7 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
         }
+#endif
     }
 }
 
@@ -128,16 +171,28 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t 
     constexpr int G = E >> R;
     const uint32_t dlog = jtop - R + 1;
     const uint32_t dlog_g = dlog >= wlog ? dlog - wlog + dtile : dlog;
+    // every group's records are read before any is written back: the LDS reads of one
+    // group cannot be issued ahead of the previous group's writes otherwise (the
+    // compiler cannot prove they do not alias), which left G - 1 read latencies exposed
+    constexpr int BW = kLdsBatch<G>;
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-        const uint32_t g = threadIdx.x + (uint32_t)h * NT;
-        const uint32_t b = spread(g, dlog, R);
-        uint64_t v[1 << R];
+    for (int h0 = 0; h0 < G; h0 += BW) {
+        uint64_t v[BW][1 << R];
+        uint32_t b[BW];
 #pragma unroll
-        for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << dlog))];
-        group_steps<MODE, R>(v, tile_pos(base, b, wlog, dtile), dlog_g, ilog, seed);
+        for (int h = 0; h < BW; ++h) {
+            b[h] = spread(threadIdx.x + (uint32_t)(h0 + h) * NT, dlog, R);
 #pragma unroll
-        for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << dlog))] = v[q];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = sm[lpad(b[h] + ((uint32_t)q << dlog))];
+        }
+#pragma unroll
+        for (int h = 0; h < BW; ++h)
+            group_steps<MODE, R>(v[h], tile_pos(base, b[h], wlog, dtile), dlog_g, ilog, seed);
+#pragma unroll
+        for (int h = 0; h < BW; ++h) {
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) sm[lpad(b[h] + ((uint32_t)q << dlog))] = v[h][q];
+        }
     }
 }
 
@@ -177,27 +232,41 @@ __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32
                                              uint32_t seed, uint32_t dtile = 0) {
     static_assert(WL == 0 || DLOG >= WL || DLOG + R <= WL, "a round stays on one side of bit WL");
     constexpr int G = E >> R;
+    const uint32_t dg = (WL && DLOG >= WL) ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
+    // all G groups read first, then computed, then written (see lds_round)
+    constexpr int BW = kLdsBatch<G>;
 #pragma unroll
-    for (int h = 0; h < G; ++h) {
-        const uint32_t g = threadIdx.x + (uint32_t)h * NT;
-        const uint32_t b = spread(g, (uint32_t)DLOG, (uint32_t)R);
-        const uint32_t p0 = WL ? tile_pos(base, b, (uint32_t)WL, dtile) : base + b;
-        const uint32_t dg = (WL && DLOG >= WL) ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
-        uint64_t v[1 << R];
+    for (int h0 = 0; h0 < G; h0 += BW) {
+    uint64_t v[BW][1 << R];
+    uint32_t b[BW];
+#pragma unroll
+    for (int h = 0; h < BW; ++h) {
+        b[h] = spread(threadIdx.x + (uint32_t)(h0 + h) * NT, (uint32_t)DLOG, (uint32_t)R);
         if constexpr (DLOG + R >= 4) {
-            uint64_t *row = sm + lpad(b);
+            const uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
-            group_steps<MODE, R>(v, p0, dg, ilog, seed);
-#pragma unroll
-            for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[q];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
         } else {  // a group inside 16 records: the padding slot may fall between its records
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[q] = sm[lpad(b + ((uint32_t)q << DLOG))];
-            group_steps<MODE, R>(v, p0, dg, ilog, seed);
-#pragma unroll
-            for (int q = 0; q < (1 << R); ++q) sm[lpad(b + ((uint32_t)q << DLOG))] = v[q];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = sm[lpad(b[h] + ((uint32_t)q << DLOG))];
         }
+    }
+#pragma unroll
+    for (int h = 0; h < BW; ++h) {
+        const uint32_t p0 = WL ? tile_pos(base, b[h], (uint32_t)WL, dtile) : base + b[h];
+        group_steps<MODE, R>(v[h], p0, dg, ilog, seed);
+    }
+#pragma unroll
+    for (int h = 0; h < BW; ++h) {
+        if constexpr (DLOG + R >= 4) {
+            uint64_t *row = sm + lpad(b[h]);
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[h][q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < (1 << R); ++q) sm[lpad(b[h] + ((uint32_t)q << DLOG))] = v[h][q];
+        }
+    }
     }
 }
 template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0>
@@ -254,6 +323,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
     for (;;) {
+        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = pf[r];
@@ -271,7 +341,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if (!kLate) prefetch();
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
+                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, sk);
         } else {
             // seg0 = (stage << 8) | top: first the last steps top..0 of an earlier stage on
             // the tile's low (consecutive) bits — a stage's tail fused with the next
@@ -286,21 +356,21 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                 // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
                 if constexpr (TL != 0 && WL != 0 && MODE != 2 && NT <= 512) {
                     if ((seg0 & 0xFFu) == (uint32_t)WL - 1u) {
-                        lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
+                        lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, sk, dtile);
                         done = true;
                     }
                 }
                 if (!done)
-                    lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, seed);
+                    lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, sk);
             }
             if (kLate) prefetch();
             if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
-                lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, sk);
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
-                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, sk, dtile);
             } else if (ilog) {  // ilog = 0: no steps on the row bits
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
-                                       wlog < tlog ? (int)wlog : 0, seed);
+                                       wlog < tlog ? (int)wlog : 0, sk);
             }
         }
         {
@@ -358,9 +428,10 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
+        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
     for (;;) {
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
-        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
+        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, sk);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
         __syncthreads();
@@ -371,10 +442,10 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         }
         if constexpr (TL != 0 && !STRIDED)  // tlog == TL (checked by the launcher)
-            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, seed);
+            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, sk);
         else
             lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
-                                   (int)(jbot + RL), seed);
+                                   (int)(jbot + RL), sk);
         constexpr int G = E >> RL;
         if constexpr (SEL && !STRIDED) {
             uint64_t v[E];
@@ -386,7 +457,7 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
             for (int h = 0; h < G; ++h) {
                 uint64_t (&g)[1 << RL] = *reinterpret_cast<uint64_t (*)[1 << RL]>(&v[h << RL]);
                 group_steps<MODE, RL>(g, base + pbase + t * (uint32_t)E + ((uint32_t)h << RL), 0u,
-                                      ilog, seed);
+                                      ilog, sk);
             }
 #pragma unroll
             for (int q = 0; q < E; ++q) c += (uint32_t)v[q] < sel_d;
@@ -421,20 +492,34 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
             tile = next;
             continue;
         }
+        // every group read from LDS first (the fenced stores below would otherwise keep the
+        // next group's reads behind them), then computed, then stored
+        constexpr int BW = kLdsBatch<G>;
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const uint32_t b = spread(t + (uint32_t)h * NT, jbot, RL);
-            uint64_t v[1 << RL];
+        for (int h0 = 0; h0 < G; h0 += BW) {
+        uint64_t vv[BW][1 << RL];
+        uint32_t bb[BW];
+#pragma unroll
+        for (int h = 0; h < BW; ++h) {
+            const uint32_t b = bb[h] = spread(t + (uint32_t)(h0 + h) * NT, jbot, RL);
             if (!STRIDED) {  // b = g << RL: lpad(b + q) = lpad(b) + q + (q >> 4)
                 const uint64_t *row = sm + lpad(b);
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) v[q] = row[q + (q >> 4)];
+                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = row[q + (q >> 4)];
             } else {
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + ((uint32_t)q << jbot))];
+                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = sm[lpad(b + ((uint32_t)q << jbot))];
             }
-            const uint32_t pb = tile_pos(0u, b, wlog, dtile);  // tile-relative position of v[0]
-            group_steps<MODE, RL>(v, base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
+        }
+#pragma unroll
+        for (int h = 0; h < BW; ++h) {
+            const uint32_t pb = tile_pos(0u, bb[h], wlog, dtile);  // tile-relative position of v[0]
+            group_steps<MODE, RL>(vv[h], base + pbase + pb, STRIDED ? dtile : 0u, ilog, sk);
+        }
+#pragma unroll
+        for (int h = 0; h < BW; ++h) {
+            uint64_t (&v)[1 << RL] = vv[h];
+            const uint32_t pb = tile_pos(0u, bb[h], wlog, dtile);
             if (STRIDED) {  // v[q] sits 2^dtile positions after v[q-1]: 8-B stores
 #pragma unroll
                 for (int q = 0; q < (1 << RL); ++q)
@@ -457,6 +542,7 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+        }
         }
         if (next >= ntiles) break;
         __syncthreads();  // the last round's LDS reads retire before the next tile lands
@@ -597,15 +683,16 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             }
         }
     };
+        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
     load(tile);
     for (;;) {
         const uint32_t base = tile << tlog;
         const uint32_t p0 = base + pbase + t * (uint32_t)E;
-        lane_stage<MODE, 1, E>(pf, p0, seed);
-        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, seed);
-        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, seed);
-        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, seed);
-        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, seed);
+        lane_stage<MODE, 1, E>(pf, p0, sk);
+        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, sk);
+        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, sk);
+        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, sk);
+        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, sk);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
         __syncthreads();
@@ -623,32 +710,44 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             // other in the same order, so the network and its output are unchanged.
             constexpr int kLast = RL + R1 - 1;
             if constexpr (LPF == 2 && kLast < TL - 1) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
-                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, sk);
+                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, sk);
                 load(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, seed);
+                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, sk);
             } else if constexpr (LPF != 0) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, sk);
                 load(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, sk);
             } else {
                 load(next < ntiles ? next : tile);
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, sk);
             }
         } else {
             load(next < ntiles ? next : tile);
             for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
-            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
+                lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, sk);
+            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, sk);
         }
         constexpr int G = E >> RL;
+        // every group read from LDS first, then computed, then stored (the fenced stores
+        // would otherwise hold the next group's reads behind them)
+        constexpr int BW = kLdsBatch<G>;
 #pragma unroll
-        for (int h = 0; h < G; ++h) {
-            const uint32_t b = (t + (uint32_t)h * NT) << RL;
-            uint64_t v[1 << RL];
+        for (int h0 = 0; h0 < G; h0 += BW) {
+        uint64_t vv[BW][1 << RL];
 #pragma unroll
-            for (int q = 0; q < (1 << RL); ++q) v[q] = sm[lpad(b + (uint32_t)q)];
-            group_steps<MODE, RL>(v, base + pbase + b, 0u, tlog, seed);
+        for (int h = 0; h < BW; ++h) {
+            const uint32_t b = (t + (uint32_t)(h0 + h) * NT) << RL;
+#pragma unroll
+            for (int q = 0; q < (1 << RL); ++q) vv[h][q] = sm[lpad(b + (uint32_t)q)];
+        }
+#pragma unroll
+        for (int h = 0; h < BW; ++h)
+            group_steps<MODE, RL>(vv[h], base + pbase + ((t + (uint32_t)(h0 + h) * NT) << RL), 0u, tlog, sk);
+#pragma unroll
+        for (int h = 0; h < BW; ++h) {
+            const uint32_t b = (t + (uint32_t)(h0 + h) * NT) << RL;
+            uint64_t (&v)[1 << RL] = vv[h];
 #pragma unroll
             for (int q = 0; q < (1 << RL); q += 2) {
                 const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
@@ -662,6 +761,7 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
                 asm volatile("s_nop 1" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
             }
+        }
         }
         if (next >= ntiles) break;
         __syncthreads();  // the last round's LDS reads retire before the next tile lands
@@ -706,7 +806,7 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
     if (live_groups && live_groups < ngroups) ngroups = live_groups;
     if (ngroups == 0) return hipSuccess;
     const unsigned blocks = (ngroups + 255) / 256;
-    net_account((uint64_t)16 * ngroups << R);
+    net_account((uint64_t)16 * ngroups << R, "bitonic_global", s);
     switch (R) {
     case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
     case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
@@ -753,7 +853,7 @@ static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uin
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    net_account((uint64_t)16 * tiles << tlog);
+    net_account((uint64_t)16 * tiles << tlog, "bitonic_tiles", s);
     hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF>), dim3(grid), dim3(NT), lds, s,
                        data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
     return hipGetLastError();
@@ -795,7 +895,8 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     const int rest = (int)c.tlog - (int)(STRIDED ? wlog : 0u) - R1;  // steps after the register round
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
-    net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog);  // the select pass writes ~nothing
+    // the select pass writes ~nothing
+    net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog, "bitonic_merge_direct", s);
 #define BD_GO1(RL_, SEL_, TL_)                                                                     \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -841,15 +942,23 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
                                      uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{}) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
-    net_account((uint64_t)16 * c.tiles << c.tlog);
     SortGen gg = g;
     unsigned grid = c.grid;
+    // the live tiles' read + write (GEN: the read is the client records; the initial
+    // entries, dummies and pads are made in registers) ...
+    uint64_t bytes = (uint64_t)16 * c.tiles << c.tlog;
+    if (GEN) {
+        const uint64_t live = (uint64_t)c.tiles << c.tlog;
+        const uint64_t rd = g.nrec > pbase ? (uint64_t)g.nrec - pbase : 0u;
+        bytes = 8 * live + 8 * (rd < live ? rd : live);
+    }
     if (gg.pad_n) {  // + store-only blocks for the pad tiles, about 8 stores per lane
         gg.grid_live = c.grid;
         uint32_t nb = (gg.pad_n / 2u + NT * 8u - 1u) / (NT * 8u);
         grid += nb < 1024u ? nb : 1024u;
-        net_account((uint64_t)8 * gg.pad_n);
+        bytes += (uint64_t)8 * gg.pad_n;  // ... + the pad tiles' stores
     }
+    net_account(bytes, "bitonic_sort_direct", s);
 #define BS_GO_PF(RL_, TL_, LPF_)                                                                   \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -1460,7 +1569,7 @@ hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, ui
     const uint32_t lower = pos_mine < pos_theirs;
     const uint32_t pos_lo = lower ? pos_mine : pos_theirs;
     const uint32_t key = mode == 2 ? shuffle_step_key(seed, ilog, jlog) : 0u;
-    net_account((uint64_t)24 * m);
+    net_account((uint64_t)24 * m, "bitonic_exchange_kernel", s);
 #define BX_GO(MD)                                                                                  \
     hipLaunchKernelGGL((bitonic_exchange_kernel<MD>), dim3((unsigned)blocks), dim3(256), 0, s,     \
                        (uint4 *)mine, (const uint4 *)theirs, m2, pos_lo, lower, ilog, key)

@@ -226,7 +226,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         if (ntiles == 0 || ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
-        net_account((uint64_t)(last ? 8 : 16) * L);
+        net_account((uint64_t)(last ? 8 : 16) * L, "compact_pass", s);
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
         const int blk = j0 == 0 ? 2 : kCompactBlocks;
         const unsigned res = small ? 256u * (unsigned)blk : 256u;
@@ -492,7 +492,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);
     const size_t lds = (Hr + CAP + 1) * 8;
-    net_account((uint64_t)(last ? 8 : 16) * L);
+    net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
     const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr <= 512)
     const int F = !last ? 0 : (accumulate ? 2 : 1);
     hipError_t e;

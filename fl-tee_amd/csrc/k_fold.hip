@@ -202,7 +202,7 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     if (C >= Hr && span / (64 * 2 * C) >= 1024) C <<= 1;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
-    net_account((uint64_t)16 * span);
+    net_account((uint64_t)16 * span, "fold_stream_kernel", s);
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
     // about one wave per CU: latency-bound, prefetch deeper (2 or 4 stages were no faster
     // on the large arrays, profiles/r01/ab/fold_chunk_depth*.jsonl)

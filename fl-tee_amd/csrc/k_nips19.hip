@@ -202,7 +202,7 @@ __global__ __launch_bounds__(SEL_NT) void select_write_kernel(const uint2 *__res
 hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t *cnt,
                                uint32_t *base, hipStream_t s) {
     const size_t nb = select_tiles(m);
-    net_account((uint64_t)8 * m);
+    net_account((uint64_t)8 * m, "select_count_kernel", s);
     const bool vec = ((uintptr_t)src & 15) == 0;
     const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
     if (vec)
@@ -218,7 +218,7 @@ hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t
 hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const uint32_t *base,
                                uint64_t *dst, hipStream_t s) {
     const size_t nb = select_tiles(m);
-    net_account((uint64_t)8 * m);
+    net_account((uint64_t)8 * m, "select_write_kernel", s);
     const bool vec = ((uintptr_t)src & 15) == 0;
     const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
     if (vec)

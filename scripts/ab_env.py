@@ -15,16 +15,30 @@ import json, sys, torch
 sys.path.insert(0, {root!r}); sys.path.insert(0, {root!r} + "/fl-tee_amd")
 import bench
 from fltee import device as D
-r = bench.bench_workload(torch, D, {w!r}, steps={steps}, warmup=5, device=torch.device("cuda", 0))
-print("RESULT " + json.dumps(dict(kernel_ms=r["kernel_s"] * 1e3, passes=r["net"]["passes"])))
+import hashlib, numpy as np
+from fltee import _lib as L
+dev = torch.device("cuda", 0)
+r = bench.bench_workload(torch, D, {w!r}, steps={steps}, warmup=5, device=dev)
+# the output's bits, to check that the variants compute the same aggregate
+wl = bench.WORKLOADS[{w!r}]
+rec = bench.make_records(torch, wl["n"], wl["d"], wl["k"], 1000, dev)
+kw = dict(dense=wl["k"] is None)
+if wl.get("dp"):
+    kw.update(seed=7)
+out = D.aggregate(wl["alg"], rec, wl["n"], wl["k"] or wl["d"], wl["d"], **kw).cpu().numpy()
+h = hashlib.sha256(out.view(np.uint32).tobytes()).hexdigest()[:16]
+print("RESULT " + json.dumps(dict(kernel_ms=r["kernel_s"] * 1e3, passes=r["net"]["passes"], out_sha=h,
+      build=L.lib().fltee_version().decode(),
+      kernels={{k: round(v["ms"] / v["launches"] * 1e3, 1) for k, v in r["net"]["kernels"].items()}})))
 """
 
 
 def main():
     w = sys.argv[1]
     steps = {"c3": 300, "c1": 300, "mnist100": 300}.get(w, 10)
+    reps = int(os.environ.get("AB_REPS", "2"))
     variants = [""] + sys.argv[2:] + [""]
-    for rep in range(2):
+    for rep in range(reps):
         for v in variants:
             env = dict(os.environ)
             for kv in v.split():

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun job that regenerates the round's GPU evidence (run under gpurun from the
-# repo root):  TAG=r02 [TESTS=1] [BENCH=1] [PROFILE="ns c1 c3 c4 mnist100"] [PMC="ns"] \
-#              bash scripts/gpu_evidence.sh
+# repo root):  TAG=r03 [TESTS=1] [BENCH=1] [PROFILE="ns c1 c3 c4 mnist100"] [PMC="ns"] \
+#              [SQ="c4 c5"] bash scripts/gpu_evidence.sh
 # Every GPU step has its own time limit and the steps stop at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
@@ -32,6 +32,18 @@ for w in ${PMC}; do
       -- python3 bench.py --workload "$w" --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
       --no-e2e > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
   echo "pmc $w"
+done
+# SQ counters per kernel (one pass of <= 8 SQ counters each, its own run)
+SQ1=${SQ1:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT}
+SQ2=${SQ2:-SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR}
+for w in ${SQ}; do
+  timeout -s KILL 150 rocprofv3 --pmc ${SQ1} --output-format csv -d "$OUT/sq1_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/sq1_$w.log" 2>&1 || exit 18
+  timeout -s KILL 150 rocprofv3 --pmc ${SQ2} --output-format csv -d "$OUT/sq2_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/sq2_$w.log" 2>&1 || exit 19
+  echo "sq $w"
 done
 if [ "${AESPROF:-0}" = 1 ]; then  # the constant-time AES-CTR kernel (scripts/bench_aes.py shapes)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_aes" -o run \
