@@ -41,10 +41,30 @@
 #define FLTEE_CE_BATCH 1
 #endif
 #ifndef FLTEE_LDS_BATCH
-#define FLTEE_LDS_BATCH 0
+#define FLTEE_LDS_BATCH 2
+#endif
+//   FLTEE_KEY_AFTER_DATA  the keyed comparator's step keys computed after each round's loads
+#ifndef FLTEE_KEY_AFTER_DATA
+#define FLTEE_KEY_AFTER_DATA 1
+#endif
+//   FLTEE_KEYED_SPLIT  the keyed comparator as one per-lane product per step + a scalar
+#ifndef FLTEE_KEYED_SPLIT
+#define FLTEE_KEYED_SPLIT 1
 #endif
 template <int G>
 constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FLTEE_LDS_BATCH;
+//   FLTEE_LDS_READ1   LDS reads as single ds_read_b64 (no ds_read2_b64 pairing)
+#ifndef FLTEE_LDS_READ1
+#define FLTEE_LDS_READ1 0
+#endif
+//   FLTEE_TID_FRESH   the lane id re-read per LDS round (see lane_tid)
+#ifndef FLTEE_TID_FRESH
+#define FLTEE_TID_FRESH 1
+#endif
+//   FLTEE_WAVE_LOCAL  the first pass's stages inside a wave's records without block barriers
+#ifndef FLTEE_WAVE_LOCAL
+#define FLTEE_WAVE_LOCAL 1
+#endif
 
 namespace fltee {
 
@@ -62,13 +82,23 @@ __device__ __forceinline__ uint32_t spread(uint32_t g, uint32_t d, uint32_t r) {
     return ((g >> d) << (d + r)) | lo;
 }
 
-// The seed of the keyed comparator, re-defined at the top of each tile iteration: its
-// step keys (a few SALU each, shuffle_step_key) are then computed inside the loop next to
-// their use instead of all being hoisted out of it (the ~100 keys of a first pass held
-// in SGPRs across the loop spilled SGPRs and VGPRs).
-__device__ __forceinline__ uint32_t loop_seed(uint32_t seed) {
-    asm volatile("" : "+s"(seed));
-    return seed;
+// The same value, made to depend on a loaded record (an SGPR the compiler cannot see
+// through): the keyed comparator's step keys and swap decisions depend on positions only,
+// so without this hipcc computes those of a whole tile up front and spills them.
+__device__ __forceinline__ uint32_t after_data(uint32_t s, uint32_t v) {
+    asm volatile("; after_data %1" : "+s"(s) : "v"(v));
+    return s;
+}
+
+// The keyed comparator (MODE 2) split into a per-lane and a wave-uniform part.  For a
+// group whose first position p0 has zero bits where dq = q << dlog has ones, l = p0 + dq
+// = p0 ^ dq, so l ^ key = x ^ dq = x + dq - 2 (key & dq) with x = p0 ^ key, and
+//   (l ^ key) * K = x * K + (dq - 2 (key & dq)) * K   (mod 2^32):
+// the top bit cond2<2> takes is the sign of X + C(dq), X = x * K once per group and step,
+// C(dq) computed by the scalar unit.  One v_add per compare instead of an add, a xor and
+// a v_mul_lo_u32; the same bits.
+__device__ __forceinline__ uint32_t keyed_c(uint32_t key, uint32_t dq) {
+    return (dq - 2u * (key & dq)) * 0x9E3779B1u;
 }
 
 // Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
@@ -78,10 +108,17 @@ __device__ __forceinline__ uint32_t loop_seed(uint32_t seed) {
 template <int MODE, int R>
 __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, uint32_t dlog,
                                             uint32_t ilog, uint32_t seed) {
+    if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
     const bool asc = (p0 & (1u << ilog)) == 0;
 #pragma unroll
     for (int lv = R - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
+        const uint32_t X = (MODE == 2 && FLTEE_KEYED_SPLIT) ? (p0 ^ key) * 0x9E3779B1u : 0u;
+        auto decide = [&](int q, int qm) -> bool {
+            if constexpr (MODE == 2 && FLTEE_KEYED_SPLIT)
+                return asc ^ ((int32_t)(X + keyed_c(key, (uint32_t)q << dlog)) < 0);
+            return asc ^ cond2<MODE>(v[q], v[qm], p0 + ((uint32_t)q << dlog), key);
+        };
 #if FLTEE_CE_BATCH
         // every swap decision of the step first, then the selects: the compares are
         // independent, so their mask chains (v_cmp -> s_xor -> v_cndmask) overlap
@@ -89,8 +126,7 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
 #pragma unroll
         for (int q = 0, k = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
-            const int qm = q | (1 << lv);
-            sw[k++] = asc ^ cond2<MODE>(v[q], v[qm], p0 + ((uint32_t)q << dlog), key);
+            sw[k++] = decide(q, q | (1 << lv));
         }
 #pragma unroll
         for (int q = 0, k = 0; q < (1 << R); ++q) {
@@ -107,13 +143,42 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
             const uint64_t a = v[q], c = v[qm];
-            const bool sw = asc ^ cond2<MODE>(a, c, p0 + ((uint32_t)q << dlog), key);
+            const bool sw = decide(q, qm);
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
         }
 #endif
     }
 }
+
+// An 8-B LDS read the compiler does not pair into ds_read2_b64: on gfx950 that form takes
+// 8 LDS cycles for two 512-B wave accesses, two ds_read_b64 take 4 (MI355X_MICROARCH.md
+// LDS table).  A volatile access is never merged (FLTEE_LDS_READ1).
+__device__ __forceinline__ uint64_t lds_ld(const uint64_t *p) {
+#if FLTEE_LDS_READ1
+    typedef __attribute__((address_space(3))) const volatile uint64_t lds_cv_u64;
+    return *(lds_cv_u64 *)p;
+#else
+    return *p;
+#endif
+}
+
+// The lane id, re-defined where it is read (FLTEE_TID_FRESH): a round's per-lane LDS
+// addresses are then computed in the round (a few VALU) instead of being hoisted out of
+// the tile loop as loop invariants and spilled (a spill's reload waits vmcnt(0), i.e. for
+// the previous tile's stores and the prefetch in flight).
+// Only the 1024-lane kernels (held to 128 VGPRs) need it: at 512 lanes the recomputation
+// costs more than it saves (C3 0.1518 vs 0.1484 ms, `profiles/r03/ab/`).
+template <int NT>
+__device__ __forceinline__ uint32_t lane_tid() {
+    uint32_t t = threadIdx.x;
+    if constexpr (FLTEE_TID_FRESH && NT >= 1024) asm volatile("; lane_tid" : "+v"(t));
+    return t;
+}
+
+// One wave's LDS accesses stay in program order (the LDS executes a wave's DS
+// instructions in issue order): a compiler-only barrier suffices between wave-local rounds.
+__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_wave_barrier(); }
 
 // Raw buffer access: byte offset = soffset (wave-uniform, SGPR) + voffset (per lane).
 typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
@@ -181,9 +246,9 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t 
         uint32_t b[BW];
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            b[h] = spread(threadIdx.x + (uint32_t)(h0 + h) * NT, dlog, R);
+            b[h] = spread(lane_tid<NT>() + (uint32_t)(h0 + h) * NT, dlog, R);
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[h][q] = sm[lpad(b[h] + ((uint32_t)q << dlog))];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = lds_ld(&sm[lpad(b[h] + ((uint32_t)q << dlog))]);
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h)
@@ -227,10 +292,21 @@ __device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t 
 // first position from tile_pos, its global distance 2^(DLOG - WL + dtile) for the rounds
 // on the row bits (>= WL) and 2^DLOG for those on the consecutive bits (< WL: a stage's
 // tail fused into the tile, plan_network).
-template <int MODE, int R, int E, int NT, int DLOG, int WL = 0>
+// WB > 0: a wave-local round (every group inside the wave's own 2^WB = 64 * E records:
+// the wave's 64 lanes x G groups x 2^R records are tile positions wave * 2^WB + [0, 2^WB)),
+// so it needs no block barrier before or after it, only the wave's own LDS order.
+template <int G>
+__device__ __forceinline__ uint32_t round_group(uint32_t t, int h, int NT, int WB) {
+    constexpr int gl = G >= 32 ? 5 : (G >= 16 ? 4 : (G >= 8 ? 3 : (G >= 4 ? 2 : (G >= 2 ? 1 : 0))));
+    if (!WB) return t + (uint32_t)h * (uint32_t)NT;
+    return (t & 63u) | ((uint32_t)h << 6) | ((t >> 6) << (6 + gl));
+}
+
+template <int MODE, int R, int E, int NT, int DLOG, int WL = 0, int WB = 0>
 __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     static_assert(WL == 0 || DLOG >= WL || DLOG + R <= WL, "a round stays on one side of bit WL");
+    static_assert(WB == 0 || (WL == 0 && DLOG + R <= WB && (64 * E) == (1 << WB)), "wave-local round");
     constexpr int G = E >> R;
     const uint32_t dg = (WL && DLOG >= WL) ? (uint32_t)(DLOG - WL) + dtile : (uint32_t)DLOG;
     // all G groups read first, then computed, then written (see lds_round)
@@ -241,14 +317,14 @@ __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32
     uint32_t b[BW];
 #pragma unroll
     for (int h = 0; h < BW; ++h) {
-        b[h] = spread(threadIdx.x + (uint32_t)(h0 + h) * NT, (uint32_t)DLOG, (uint32_t)R);
+        b[h] = spread(round_group<G>(lane_tid<NT>(), h0 + h, NT, WB), (uint32_t)DLOG, (uint32_t)R);
         if constexpr (DLOG + R >= 4) {
             const uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[h][q] = row[(q << DLOG) + ((q << DLOG) >> 4)];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = lds_ld(&row[(q << DLOG) + ((q << DLOG) >> 4)]);
         } else {  // a group inside 16 records: the padding slot may fall between its records
 #pragma unroll
-            for (int q = 0; q < (1 << R); ++q) v[h][q] = sm[lpad(b[h] + ((uint32_t)q << DLOG))];
+            for (int q = 0; q < (1 << R); ++q) v[h][q] = lds_ld(&sm[lpad(b[h] + ((uint32_t)q << DLOG))]);
         }
     }
 #pragma unroll
@@ -269,23 +345,39 @@ __device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32
     }
     }
 }
-template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0>
+// WB > 0: wave-local rounds (see round_group), ordered by the wave's own LDS order
+// (a compiler-only barrier between them) instead of block barriers
+template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0, int WB = 0>
 __device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     if constexpr (JTOP >= JBOT) {
         constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
         constexpr int r = JTOP - JBOT + 1 < rmax ? JTOP - JBOT + 1 : rmax;
-        lds_round_ct<MODE, r, E, NT, JTOP - r + 1, WL>(sm, base, ilog, seed, dtile);
-        __syncthreads();
-        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT, WL>(sm, base, ilog, seed, dtile);
+        lds_round_ct<MODE, r, E, NT, JTOP - r + 1, WL, WB>(sm, base, ilog, seed, dtile);
+        if constexpr (WB) wave_lds_order();
+        else __syncthreads();
+        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT, WL, WB>(sm, base, ilog, seed, dtile);
     }
 }
 
-// stages IL..TL-1 in full and stage TL down to step RL (bitonic_sort_direct's LDS part)
+// stages IL..TL-1 in full and stage TL down to step RL (bitonic_sort_direct's LDS part).
+// With FLTEE_WAVE_LOCAL the stages up to log2(64 E) (every step inside the wave's own
+// records) run as wave-local rounds — no block barrier, so the waves drift apart and one
+// wave's LDS traffic overlaps another's compare-exchanges — and one block barrier
+// precedes the first stage that crosses waves.  The caller orders the LDS writes in front
+// of the first round (a block barrier, or the wave's own order when WAVE_FIRST).
+template <int E>
+constexpr int kWaveLog = E >= 32 ? 11 : (E >= 16 ? 10 : (E >= 8 ? 9 : (E >= 4 ? 8 : 7)));
 template <int MODE, int E, int NT, int IL, int TL, int RL>
 __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
+    constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
     if constexpr (IL < TL) {
-        lds_steps_ct<MODE, E, NT, IL - 1, 0>(sm, base, (uint32_t)IL, seed);
+        if constexpr (WB && IL <= WB) {
+            lds_steps_ct<MODE, E, NT, IL - 1, 0, 0, WB>(sm, base, (uint32_t)IL, seed);
+            if constexpr (IL == WB) __syncthreads();  // the next stage crosses waves
+        } else {
+            lds_steps_ct<MODE, E, NT, IL - 1, 0>(sm, base, (uint32_t)IL, seed);
+        }
         sort_stages_ct<MODE, E, NT, IL + 1, TL, RL>(sm, base, seed);
     } else {
         lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base, (uint32_t)TL, seed);
@@ -323,7 +415,6 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
     for (;;) {
-        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = pf[r];
@@ -341,7 +432,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if (!kLate) prefetch();
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, sk);
+                lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
         } else {
             // seg0 = (stage << 8) | top: first the last steps top..0 of an earlier stage on
             // the tile's low (consecutive) bits — a stage's tail fused with the next
@@ -356,27 +447,27 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                 // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
                 if constexpr (TL != 0 && WL != 0 && MODE != 2 && NT <= 512) {
                     if ((seg0 & 0xFFu) == (uint32_t)WL - 1u) {
-                        lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, sk, dtile);
+                        lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
                         done = true;
                     }
                 }
                 if (!done)
-                    lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, sk);
+                    lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, st, (int)(seg0 & 0xFFu), 0, seed);
             }
             if (kLate) prefetch();
             if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
-                lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, sk);
+                lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
-                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, sk, dtile);
+                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
             } else if (ilog) {  // ilog = 0: no steps on the row bits
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
-                                       wlog < tlog ? (int)wlog : 0, sk);
+                                       wlog < tlog ? (int)wlog : 0, seed);
             }
         }
         {
             const uint32_t sb = base * 8u;
 #pragma unroll
-            for (int r = 0; r < E; ++r) bt_store<kTileCP>(rs, voff, sb + (uint32_t)r * rstride, sm[lpad(threadIdx.x + r * NT)]);
+            for (int r = 0; r < E; ++r) bt_store<kTileCP>(rs, voff, sb + (uint32_t)r * rstride, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
@@ -428,10 +519,9 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
-        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
     for (;;) {
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
-        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, sk);
+        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
         __syncthreads();
@@ -442,22 +532,22 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
             for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
         }
         if constexpr (TL != 0 && !STRIDED)  // tlog == TL (checked by the launcher)
-            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, sk);
+            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, seed);
         else
             lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
-                                   (int)(jbot + RL), sk);
+                                   (int)(jbot + RL), seed);
         constexpr int G = E >> RL;
         if constexpr (SEL && !STRIDED) {
             uint64_t v[E];
             const uint64_t *own = sm + lpad(t * (uint32_t)E);  // E >= 16: lpad splits
 #pragma unroll
-            for (int q = 0; q < E; ++q) v[q] = own[q + (q >> 4)];
+            for (int q = 0; q < E; ++q) v[q] = lds_ld(&own[q + (q >> 4)]);
             uint32_t c = 0;
 #pragma unroll
             for (int h = 0; h < G; ++h) {
                 uint64_t (&g)[1 << RL] = *reinterpret_cast<uint64_t (*)[1 << RL]>(&v[h << RL]);
                 group_steps<MODE, RL>(g, base + pbase + t * (uint32_t)E + ((uint32_t)h << RL), 0u,
-                                      ilog, sk);
+                                      ilog, seed);
             }
 #pragma unroll
             for (int q = 0; q < E; ++q) c += (uint32_t)v[q] < sel_d;
@@ -501,20 +591,20 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         uint32_t bb[BW];
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            const uint32_t b = bb[h] = spread(t + (uint32_t)(h0 + h) * NT, jbot, RL);
+            const uint32_t b = bb[h] = spread(lane_tid<NT>() + (uint32_t)(h0 + h) * NT, jbot, RL);
             if (!STRIDED) {  // b = g << RL: lpad(b + q) = lpad(b) + q + (q >> 4)
                 const uint64_t *row = sm + lpad(b);
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = row[q + (q >> 4)];
+                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = lds_ld(&row[q + (q >> 4)]);
             } else {
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = sm[lpad(b + ((uint32_t)q << jbot))];
+                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = lds_ld(&sm[lpad(b + ((uint32_t)q << jbot))]);
             }
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
             const uint32_t pb = tile_pos(0u, bb[h], wlog, dtile);  // tile-relative position of v[0]
-            group_steps<MODE, RL>(vv[h], base + pbase + pb, STRIDED ? dtile : 0u, ilog, sk);
+            group_steps<MODE, RL>(vv[h], base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
@@ -555,18 +645,31 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 template <int MODE, int IL, int E>
 __device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32_t seed) {
     constexpr int B = 1 << IL;
+    if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
 #pragma unroll
     for (int lv = IL - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, IL, (uint32_t)lv) : 0u;
+        // p0 is a multiple of E: l = p0 + q = p0 ^ q (keyed_c)
+        const uint32_t X = (MODE == 2 && FLTEE_KEYED_SPLIT) ? (p0 ^ key) * 0x9E3779B1u : 0u;
+        bool sw[E / 2];
 #pragma unroll
-        for (int q = 0; q < E; ++q) {
+        for (int q = 0, k = 0; q < E; ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
             const bool asc = ((p0 + (uint32_t)(q & ~(B - 1))) & (1u << IL)) == 0;
+            if constexpr (MODE == 2 && FLTEE_KEYED_SPLIT)
+                sw[k++] = asc ^ ((int32_t)(X + keyed_c(key, (uint32_t)q)) < 0);
+            else
+                sw[k++] = asc ^ cond2<MODE>(v[q], v[qm], p0 + (uint32_t)q, key);
+        }
+#pragma unroll
+        for (int q = 0, k = 0; q < E; ++q) {
+            if (q & (1 << lv)) continue;
+            const int qm = q | (1 << lv);
             const uint64_t a = v[q], c = v[qm];
-            const bool sw = asc ^ cond2<MODE>(a, c, p0 + (uint32_t)q, key);
-            v[q] = sw ? c : a;
-            v[qm] = sw ? a : c;
+            const bool s = sw[k++];
+            v[q] = s ? c : a;
+            v[qm] = s ? a : c;
         }
     }
 }
@@ -645,57 +748,84 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
                                                 0x00020000)
             : rs;
     const uint32_t voff = t * (uint32_t)E * 8u;
+    // GEN: a 16-B load that straddles the end of rec (nloc odd) returns zeros whole: its
+    // first record, the last client record, is read once up front and put back in
+    // finish() (a select, no branch)
+    uint64_t last_rec = 0;
+    if (GEN && (nloc & 1u)) last_rec = g.rec[nloc - 1u];
+    // GEN 2: the Laplace counts the lane's dummies read, r[gi] and r[gi + 1] (the E
+    // entries of a lane span at most two counts when tf >= E), as range-checked buffer
+    // loads (index >= d: 0, an entry that is a pad anyway)
+    const __amdgpu_buffer_rsrc_t lr =
+        GEN == 2 ? __builtin_amdgcn_make_buffer_rsrc((void *)g.r, (short)0, (int)(g.d * 4u), 0x00020000) : rs;
     uint64_t pf[E];
-    auto load = [&](uint32_t tl) {
+    uint32_t lap[2] = {0u, 0u};
+    // issue(): the next tile's loads only — nothing here waits for them (a use of the
+    // loaded values would make the compiler wait right after the loads and the prefetch
+    // would no longer overlap the LDS rounds); finish(): the producer, on arrival
+    auto first_entry = [&](uint32_t tl, uint32_t &gi, uint32_t &gj) {
+        const uint32_t p0 = pbase + (tl << tlog) + t * (uint32_t)E;
+        const uint32_t e0 = p0 > g.nrec ? p0 - g.nrec : 0u;
+        gi = g.tf ? e0 / g.tf : 0u;
+        gj = e0 - gi * g.tf;
+    };
+    auto issue = [&](uint32_t tl) {
         const uint32_t sb = (tl << tlog) * 8u;
-        // GEN 2: the lane's E positions are consecutive, so dummy e = p - nrec of the first
-        // one is divided by tf once and (i, j) = (e / tf, e % tf) advance with p
-        uint32_t gi = 0, gj = 0;
-        if (GEN == 2) {
-            const uint32_t p0 = pbase + (tl << tlog) + t * (uint32_t)E;
-            const uint32_t e0 = p0 > g.nrec ? p0 - g.nrec : 0u;
-            gi = g.tf ? e0 / g.tf : 0u;
-            gj = e0 - gi * g.tf;
-        }
 #pragma unroll
         for (int r = 0; r < E; r += 2) {
             const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ls, (int)(voff + (uint32_t)r * 8u),
                                                                       (int)sb, kTileCP);
             pf[r] = ((uint64_t)x.y << 32) | x.x;
             pf[r + 1] = ((uint64_t)x.w << 32) | x.z;
-            if (GEN) {
-                const uint32_t xl = (tl << tlog) + t * (uint32_t)E + (uint32_t)r;  // local index of pf[r]
-                if (xl + 1u == nloc)  // the 16-B load straddles the end of rec: reload 8 B
-                    pf[r] = bt_load<kTileCP>(ls, voff + (uint32_t)r * 8u, sb);
-                if (GEN == 1) {
-                    pf[r] = gen_entry<GEN>(g, pbase + xl, pf[r]);
-                    pf[r + 1] = gen_entry<GEN>(g, pbase + xl + 1u, pf[r + 1]);
-                } else {
+        }
+        if constexpr (GEN == 2) {
+            uint32_t gi, gj;
+            first_entry(tl, gi, gj);
+            lap[0] = __builtin_amdgcn_raw_buffer_load_b32(lr, (int)(gi * 4u), 0, 0);
+            lap[1] = __builtin_amdgcn_raw_buffer_load_b32(lr, (int)(gi * 4u + 4u), 0, 0);
+        }
+    };
+    auto finish = [&](uint32_t tl) {
+        if constexpr (GEN != 0) {
+            const uint32_t x0 = (tl << tlog) + t * (uint32_t)E;  // local index of pf[0]
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        if (pbase + xl + (uint32_t)u >= g.nrec) {  // entry (i, j): (r_i < j) ? i : MAX
-                            pf[r + u] = (g.tf == 0 || gi >= g.d || g.r[gi] >= gj) ? 0xFFFFFFFFull
-                                                                                  : (uint64_t)gi;
-                            if (++gj == g.tf) { gj = 0; ++gi; }
-                        }
+            for (int r = 0; r < E; r += 2)
+                pf[r] = (x0 + (uint32_t)r + 1u == nloc) ? last_rec : pf[r];
+            if constexpr (GEN == 1) {
+#pragma unroll
+                for (int q = 0; q < E; ++q) pf[q] = gen_entry<GEN>(g, pbase + x0 + (uint32_t)q, pf[q]);
+            } else {
+                uint32_t gi, gj;
+                first_entry(tl, gi, gj);
+                const uint32_t gi0 = gi;
+                const bool two = g.tf >= (uint32_t)E;  // uniform: the prefetched counts cover the lane
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    if (pbase + x0 + (uint32_t)q >= g.nrec) {  // entry (i, j): (r_i < j) ? i : MAX
+                        const uint32_t ri = two ? (gi == gi0 ? lap[0] : lap[1]) : (gi < g.d ? g.r[gi] : 0u);
+                        pf[q] = (g.tf == 0 || gi >= g.d || ri >= gj) ? 0xFFFFFFFFull : (uint64_t)gi;
+                        if (++gj == g.tf) { gj = 0; ++gi; }
                     }
                 }
             }
         }
     };
-        const uint32_t sk = MODE == 2 ? loop_seed(seed) : seed;
-    load(tile);
+    issue(tile);
     for (;;) {
+        finish(tile);
         const uint32_t base = tile << tlog;
         const uint32_t p0 = base + pbase + t * (uint32_t)E;
-        lane_stage<MODE, 1, E>(pf, p0, sk);
-        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, sk);
-        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, sk);
-        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, sk);
-        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, sk);
+        lane_stage<MODE, 1, E>(pf, p0, seed);
+        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, seed);
+        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, seed);
+        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, seed);
+        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, seed);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
-        __syncthreads();
+        // the lane's records are positions tE .. tE + E - 1: the wave's own 64 E records,
+        // which its wave-local first rounds read back (TL != 0 with FLTEE_WAVE_LOCAL)
+        if constexpr (TL != 0 && FLTEE_WAVE_LOCAL && R1 + 1 <= kWaveLog<E>) wave_lds_order();
+        else __syncthreads();
         const uint32_t next = tile + stride;
         if constexpr (TL != 0) {  // tlog == TL (launcher)
             // the next tile's loads go out before the LAST stage's rounds, not before the
@@ -710,23 +840,23 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             // other in the same order, so the network and its output are unchanged.
             constexpr int kLast = RL + R1 - 1;
             if constexpr (LPF == 2 && kLast < TL - 1) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, sk);
-                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, sk);
-                load(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, sk);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, seed);
+                issue(next < ntiles ? next : tile);
+                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, seed);
             } else if constexpr (LPF != 0) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, sk);
-                load(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, sk);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                issue(next < ntiles ? next : tile);
+                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, seed);
             } else {
-                load(next < ntiles ? next : tile);
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, sk);
+                issue(next < ntiles ? next : tile);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
             }
         } else {
-            load(next < ntiles ? next : tile);
+            issue(next < ntiles ? next : tile);
             for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
-                lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, sk);
-            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, sk);
+                lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, il, (int)il - 1, 0, seed);
+            lds_steps<MODE, E, NT>(sm, base + pbase, tlog, tlog, tlog, (int)tlog - 1, RL, seed);
         }
         constexpr int G = E >> RL;
         // every group read from LDS first, then computed, then stored (the fenced stores
@@ -735,18 +865,19 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += BW) {
         uint64_t vv[BW][1 << RL];
+        const uint32_t tf = lane_tid<NT>();
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            const uint32_t b = (t + (uint32_t)(h0 + h) * NT) << RL;
+            const uint32_t b = (tf + (uint32_t)(h0 + h) * NT) << RL;
 #pragma unroll
-            for (int q = 0; q < (1 << RL); ++q) vv[h][q] = sm[lpad(b + (uint32_t)q)];
+            for (int q = 0; q < (1 << RL); ++q) vv[h][q] = lds_ld(&sm[lpad(b + (uint32_t)q)]);
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h)
-            group_steps<MODE, RL>(vv[h], base + pbase + ((t + (uint32_t)(h0 + h) * NT) << RL), 0u, tlog, sk);
+            group_steps<MODE, RL>(vv[h], base + pbase + ((tf + (uint32_t)(h0 + h) * NT) << RL), 0u, tlog, seed);
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            const uint32_t b = (t + (uint32_t)(h0 + h) * NT) << RL;
+            const uint32_t b = (tf + (uint32_t)(h0 + h) * NT) << RL;
             uint64_t (&v)[1 << RL] = vv[h];
 #pragma unroll
             for (int q = 0; q < (1 << RL); q += 2) {
@@ -830,15 +961,16 @@ constexpr uint32_t kMinTilesLog = 8;
 // 14.03 ms at 2^27, W = 4: 14.66, W = 2: 16.37).
 constexpr int kMinWLog = 4;
 // The first pass's prefetch of the next tile: 0 = before the first LDS round, 1 = before
-// the last stage's rounds, 2 = before that stage's last round.  2 for the sorts by key
-// (C5 14.25 -> 14.21 ms), 1 for the keyed shuffle (C4 9.34 vs 9.38 ms with 2;
-// `profiles/r02/ab/sort_late_prefetch.jsonl`).  Overridable at build time for A/B
-// libraries only (scripts/ab_build.sh).
+// the last stage's rounds, 2 = before that stage's last round.  Round 2 kept it late (2
+// for the sorts by key, 1 for the keyed shuffle) because the kernels spilled; without
+// spills (lane_tid, the producer moved out of the prefetch) the earliest is fastest: C5
+// 13.69 vs 13.77 ms (2), C4 9.34 vs 9.35 ms (1) (`profiles/r03/ab/ab4_*.jsonl`).
+// Overridable at build time for A/B libraries only (scripts/ab_build.sh).
 #ifndef FLTEE_SORT_LATEPF_KEY
-#define FLTEE_SORT_LATEPF_KEY 2
+#define FLTEE_SORT_LATEPF_KEY 0
 #endif
 #ifndef FLTEE_SORT_LATEPF_SHUFFLE
-#define FLTEE_SORT_LATEPF_SHUFFLE 1
+#define FLTEE_SORT_LATEPF_SHUFFLE 0
 #endif
 template <int MODE>
 constexpr int kSortLatePf = MODE == 2 ? FLTEE_SORT_LATEPF_SHUFFLE : FLTEE_SORT_LATEPF_KEY;
