@@ -176,7 +176,8 @@ def rocprof_kernel(name, kernel):
     path = os.path.join(ROOT, "profiles", "r03", f"{name}_kernel_stats.csv")
     try:
         with open(path) as f:
-            rows = [r for r in csv.DictReader(f) if f"fltee::{kernel}" in r["Name"]]
+            rows = [r for r in csv.DictReader(f) if f"fltee::{kernel}<" in r["Name"] and
+                    not (kernel == "bitonic_merge_direct" and ", false, true, " in r["Name"])]
     except (OSError, KeyError):
         return None
     if not rows:

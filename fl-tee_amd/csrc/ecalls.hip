@@ -603,6 +603,21 @@ extern "C" fltee_status_t fltee_client_clip_device(void *d_records, size_t n, si
     return FLTEE_SUCCESS;
 }
 
+// CPU self-test hook: the clients' round keys by the AES-NI schedule (when the CPU has
+// it) or by the portable bitsliced one (portable != 0); returns 1 when AES-NI was used.
+namespace fltee {
+void aes128_session_round_keys_portable(const uint32_t *ids, size_t n, uint32_t *rk);
+bool host_has_aesni();
+}
+extern "C" int fltee_debug_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk, int portable) {
+    if (portable || !fltee::host_has_aesni()) {
+        fltee::aes128_session_round_keys_portable(ids, n, rk);
+        return 0;
+    }
+    fltee::aes128_session_round_keys(ids, n, rk);
+    return 1;
+}
+
 // CPU self-test hook: one AES-128 block with the library's tables (no GPU).
 namespace fltee { void aes128_encrypt_block_host(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]); }
 extern "C" void fltee_debug_aes_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {

@@ -143,12 +143,19 @@ static void expand_keys8(const uint8_t (*key)[16], int nk, uint32_t *rk) {
     }
 }
 
+// host_aesni.cpp: the same schedules with AES-NI (the ECALL's per-client key expansion)
+bool host_has_aesni();
+void aes128_expand_key_aesni(const uint8_t key[16], uint32_t rk[44]);
+void aes128_session_round_keys_aesni(const uint32_t *ids, size_t n, uint32_t *rk);
+
 void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]) {
+    if (host_has_aesni()) return aes128_expand_key_aesni(key, rk);
     expand_keys8(reinterpret_cast<const uint8_t (*)[16]>(key), 1, rk);
 }
 
 // session_key_store.rs:17-32: 16 zero bytes with bytes[4..8] = client_id big-endian
-void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk) {
+// (portable: the bitsliced circuit, 8 keys per pass)
+void aes128_session_round_keys_portable(const uint32_t *ids, size_t n, uint32_t *rk) {
     for (size_t c0 = 0; c0 < n; c0 += 8) {
         const int nk = (int)(n - c0 < 8 ? n - c0 : 8);
         uint8_t key[8][16] = {};
@@ -156,6 +163,11 @@ void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk) {
             for (int b = 0; b < 4; ++b) key[k][4 + b] = (uint8_t)(ids[c0 + k] >> (24 - 8 * b));
         expand_keys8(key, nk, rk + 44 * c0);
     }
+}
+
+void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk) {
+    if (host_has_aesni()) return aes128_session_round_keys_aesni(ids, n, rk);
+    aes128_session_round_keys_portable(ids, n, rk);
 }
 
 // host-side single block, for the CPU self-test (no GPU needed): slice 0 of the planes

@@ -57,6 +57,18 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_LDS_READ1
 #define FLTEE_LDS_READ1 0
 #endif
+//   FLTEE_TILE_HEADREG  a strided tile's first row round on its prefetch registers
+#ifndef FLTEE_TILE_HEADREG
+#define FLTEE_TILE_HEADREG 1
+#endif
+//   FLTEE_TAIL_CT_1024  compile-time tail rounds in the 1024-lane strided tiles too
+#ifndef FLTEE_TAIL_CT_1024
+#define FLTEE_TAIL_CT_1024 0
+#endif
+//   FLTEE_PLAN_SHUFFLE  the keyed shuffle (mode 2) on the planned schedule too
+#ifndef FLTEE_PLAN_SHUFFLE
+#define FLTEE_PLAN_SHUFFLE 0
+#endif
 //   FLTEE_TID_FRESH   the lane id re-read per LDS round (see lane_tid)
 #ifndef FLTEE_TID_FRESH
 #define FLTEE_TID_FRESH 1
@@ -414,8 +426,20 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
     }
+    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    // a strided tile with no fused tail (seg0 == 0) starts with the stage's top row steps:
+    // element t + r * NT of lane t differs from its other records in the top log2(E) row
+    // bits only, so that first round runs on the prefetch registers before they go to LDS
+    // (one LDS write + read of the tile less, as in bitonic_merge_direct)
+    constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && (TL - R1) >= WL;
     for (;;) {
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
+        const bool head_reg = kHeadReg && seg0 == 0;
+        if constexpr (kHeadReg) {
+            if (head_reg)
+                group_steps<MODE, R1>(pf, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
+                                      (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
+        }
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = pf[r];
         __syncthreads();
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                 // (2^12 tiles of 512 lanes; the 1024-lane 2^14 tiles are held to 128 VGPRs
                 // and spill with the tail unrolled: C5 14.82 -> 15.44 ms, so they keep
                 // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
-                if constexpr (TL != 0 && WL != 0 && MODE != 2 && NT <= 512) {
+                if constexpr (TL != 0 && WL != 0 && MODE != 2 && (NT <= 512 || FLTEE_TAIL_CT_1024)) {
                     if ((seg0 & 0xFFu) == (uint32_t)WL - 1u) {
                         lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
                         done = true;
@@ -458,7 +482,14 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
             if constexpr (TL != 0 && WL == 0) {  // contiguous merge, tlog == TL (launcher)
                 lds_steps_ct<MODE, E, NT, TL - 1, 0>(sm, base + pbase, ilog, seed);
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
-                lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                if constexpr (kHeadReg) {
+                    if (head_reg)
+                        lds_steps_ct<MODE, E, NT, TL - R1 - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                    else
+                        lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                } else {
+                    lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                }
             } else if (ilog) {  // ilog = 0: no steps on the row bits
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)tlog - 1,
                                        wlog < tlog ? (int)wlog : 0, seed);
@@ -1028,7 +1059,8 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
     if (rl == 0) return hipErrorInvalidValue;
     // the select pass writes ~nothing
-    net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog, "bitonic_merge_direct", s);
+    net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog,
+                sink.cnt ? "bitonic_merge_direct(select)" : "bitonic_merge_direct", s);
 #define BD_GO1(RL_, SEL_, TL_)                                                                     \
     do {                                                                                           \
         static bool attr = false;                                                                  \
@@ -1434,7 +1466,7 @@ static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t 
     // more VALU (the hash multiply), which the planned tile-heavy schedule pays in LDS
     // passes — C4: 10.15 vs 9.78 ms planned, against C5 (mode 0) 14.67 vs 15.34 ms and C3
     // 0.157 vs 0.163 ms (`profiles/r02/ab/network_plan.jsonl`)
-    if (MODE == 2 || c0.tlog <= 6 || mlog <= c0.tlog) return false;
+    if ((MODE == 2 && !FLTEE_PLAN_SHUFFLE) || c0.tlog <= 6 || mlog <= c0.tlog) return false;
     const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
     const int rmax = kRegMaxSteps < rcap ? kRegMaxSteps : rcap;
     const std::vector<NetPass> &plan = cached_plan(mlog, c0.tlog, c0.NT, rmax);

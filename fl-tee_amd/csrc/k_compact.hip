@@ -62,7 +62,14 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
     constexpr uint32_t CAP = (uint32_t)NT * PER;
     __shared__ uint64_t sm[CAP];
     const uint32_t W = 1u << logW, H = (1u << G) - 1;
-    const uint32_t t = threadIdx.x;
+    // the lane id re-defined where it is used: per-record positions are recomputed (a few
+    // VALU) instead of being hoisted out of the tile loop and spilled — a spill's reload
+    // waits vmcnt(0), i.e. for the prefetch in flight (k_bitonic.hip lane_tid)
+    auto tid = [] {
+        uint32_t x = threadIdx.x;
+        asm volatile("; compact tid" : "+v"(x));
+        return x;
+    };
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)src, (short)0, (int)(L * 8u), 0x00020000);
     uint32_t tile = blockIdx.x;
@@ -73,25 +80,27 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         return ((uint64_t)(band * S + (f >> logW)) << j0) + (grp << logW) + (f & (W - 1));
     };
     uint64_t pf[PER];
+    // the loads only: the dummy for slots past L is selected when the tile lands (a use of
+    // the loaded value here would make the compiler wait for the prefetch right away)
     auto prefetch = [&](uint32_t tl) {
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
-            const uint64_t p = pos_of(tl, t + i * NT);
+            const uint64_t p = pos_of(tl, tid() + i * NT);
             const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
                 rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
-            pf[i] = p < L ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
+            pf[i] = ((uint64_t)x.y << 32) | x.x;
         }
     };
     prefetch(tile);
     for (;;) {
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
-            uint64_t v = pf[i];
+            uint64_t v = pos_of(tile, tid() + i * NT) < L ? pf[i] : CP_DUMMY;
             if (FIRST) {  // key -> shift c = p - idx (u32::MAX when not selected)
-                const uint32_t p = (uint32_t)pos_of(tile, t + i * NT), idx = (uint32_t)v;
+                const uint32_t p = (uint32_t)pos_of(tile, tid() + i * NT), idx = (uint32_t)v;
                 v = (v & 0xFFFFFFFF00000000ull) | (idx < d ? (uint64_t)(p - idx) : CP_DUMMY);
             }
-            sm[t + i * NT] = v;
+            sm[tid() + i * NT] = v;
         }
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             if (two) {
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
-                    const uint32_t f = t + i * NT;
+                    const uint32_t f = tid() + i * NT;
                     if (f < lim) {
                         const uint64_t y0 = cp_pick(sm[f], sm[f + stepf], j);
                         const uint64_t y2 = cp_pick(sm[f + 2 * stepf], sm[f + 3 * stepf], j);
@@ -120,14 +129,14 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             } else {
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
-                    const uint32_t f = t + i * NT;
+                    const uint32_t f = tid() + i * NT;
                     if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], j);
                 }
             }
             __syncthreads();
 #pragma unroll
             for (uint32_t i = 0; i < PER; ++i) {
-                const uint32_t f = t + i * NT;
+                const uint32_t f = tid() + i * NT;
                 if (f < lim) sm[f] = nv[i];
             }
             __syncthreads();
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         const uint32_t nout = S << logW;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
-            const uint32_t f = t + i * NT;
+            const uint32_t f = tid() + i * NT;
             if (f < nout) {
                 const uint64_t p = pos_of(tile, f);
                 if (FINAL == 0) {
@@ -157,7 +166,17 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
 // for 6 waves per SIMD (launch_bounds' 2nd argument = min waves per EU: <= 80 VGPRs).
 // A/B at C5: 497 vs 534 us per middle pass, 499 vs 570 us for the last; the first pass
 // (more live state) spills at that bound (868 vs 751 us), so it keeps 2.
-constexpr int kCompactBlocks = 3;
+// Round 3: the kernels no longer spill (54 VGPRs, the lane id re-read where used), so the
+// first pass may take as many blocks as the later ones (FLTEE_COMPACT_FIRST_BLOCKS), and 4
+// blocks (8 waves per SIMD, <= 64 VGPRs) fit too (FLTEE_COMPACT_BLOCKS; A/B builds).
+#ifndef FLTEE_COMPACT_BLOCKS
+#define FLTEE_COMPACT_BLOCKS 3
+#endif
+#ifndef FLTEE_COMPACT_FIRST_BLOCKS
+#define FLTEE_COMPACT_FIRST_BLOCKS 3
+#endif
+constexpr int kCompactBlocks = FLTEE_COMPACT_BLOCKS;
+constexpr int kCompactFirstBlocks = FLTEE_COMPACT_FIRST_BLOCKS;
 // fltee_debug_set_compact_variant (A/B): 1 = 32 KiB tiles (default), 0 = 64 KiB tiles
 // (1024 lanes x 8), 2 = 32 KiB first pass + 64 KiB strided passes (1024 lanes x 8, one
 // block per CU: 6 levels per pass, 4 passes instead of 5 at C5; 512 x 16 spills)
@@ -228,11 +247,15 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const int fin = last ? (accumulate ? 2 : 1) : 0;
         net_account((uint64_t)(last ? 8 : 16) * L, "compact_pass", s);
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
-        const int blk = j0 == 0 ? 2 : kCompactBlocks;
+        const int blk = j0 == 0 ? kCompactFirstBlocks : kCompactBlocks;
         const unsigned res = small ? 256u * (unsigned)blk : 256u;
         const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =
-            small ? (blk == 3
+            small ? (blk >= 4
+                         ? launch_pass<512, 8, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                                                  (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
+                                                  out, (uint32_t)ntiles)
+                     : blk == 3
                          ? launch_pass<512, 8, 6>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
                                                   out, (uint32_t)ntiles)

@@ -104,6 +104,7 @@ EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_set_nips19_fused_select": (None, [ctypes.c_int]),
     "fltee_debug_net_stats": (None, [_P, _P, ctypes.c_int]),
     "fltee_debug_net_timing": (None, [ctypes.c_int, _P]),
+    "fltee_debug_session_round_keys": (ctypes.c_int, [_P, _S, _P, ctypes.c_int]),
     "fltee_debug_net_log": (_S, [_S, ctypes.c_char_p, _S, _P, _P]),
     "fltee_debug_set_fold_compact": (None, [ctypes.c_int]),
     "fltee_debug_set_pad_skip": (None, [ctypes.c_int]),

@@ -36,6 +36,8 @@ done
 # SQ counters per kernel (one pass of <= 8 SQ counters each, its own run)
 SQ1=${SQ1:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT}
 SQ2=${SQ2:-SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR}
+SQ3=${SQ3:-SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC SQ_IFETCH SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES}
+SQC=${SQC:-SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ}
 for w in ${SQ}; do
   timeout -s KILL 150 rocprofv3 --pmc ${SQ1} --output-format csv -d "$OUT/sq1_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
@@ -43,6 +45,12 @@ for w in ${SQ}; do
   timeout -s KILL 150 rocprofv3 --pmc ${SQ2} --output-format csv -d "$OUT/sq2_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
       --no-e2e > "$OUT/sq2_$w.log" 2>&1 || exit 19
+  timeout -s KILL 150 rocprofv3 --pmc ${SQ3} --output-format csv -d "$OUT/sq3_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/sq3_$w.log" 2>&1 || exit 20
+  timeout -s KILL 150 rocprofv3 --pmc ${SQC} --output-format csv -d "$OUT/sqc_$w" -o run \
+      -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
+      --no-e2e > "$OUT/sqc_$w.log" 2>&1 || exit 21
   echo "sq $w"
 done
 if [ "${AESPROF:-0}" = 1 ]; then  # the constant-time AES-CTR kernel (scripts/bench_aes.py shapes)

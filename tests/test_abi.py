@@ -117,3 +117,23 @@ def test_pack_records_roundtrip():
     # byte layout == Weight (parameters.rs:9): [u32 LE idx][f32 LE val]
     w = np.frombuffer(r.tobytes(), dtype=[("idx", "<u4"), ("val", "<f4")])
     assert np.array_equal(w["idx"], idx)
+
+
+def test_session_round_keys_aesni_equals_portable():
+    """The ECALL's per-client AES-128 key schedules: the AES-NI path (host_aesni.cpp) and
+    the portable bitsliced circuit (k_aes.hip) give the same 44 round-key words, and the
+    first four are the session key of session_key_store.rs:17-32 (id big-endian in bytes
+    4..8)."""
+    from fltee import _lib as L
+    lib = L.lib()
+    rng = np.random.default_rng(7)
+    ids = np.concatenate([[0, 1, 0xFFFF, 0xFFFFFFFF], rng.integers(0, 2 ** 32, 60)]).astype(np.uint32)
+    n = len(ids)
+    a = np.zeros(n * 44, np.uint32)
+    b = np.zeros(n * 44, np.uint32)
+    used = lib.fltee_debug_session_round_keys(ids.ctypes.data, n, a.ctypes.data, 0)
+    lib.fltee_debug_session_round_keys(ids.ctypes.data, n, b.ctypes.data, 1)
+    assert np.array_equal(a, b), f"AES-NI path used: {used}"
+    w = a.reshape(n, 44)
+    assert (w[:, 0] == 0).all() and (w[:, 2] == 0).all() and (w[:, 3] == 0).all()
+    assert np.array_equal(w[:, 1], ids)
