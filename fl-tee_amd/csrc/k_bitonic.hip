@@ -63,11 +63,11 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #endif
 //   FLTEE_TAIL_CT_1024  compile-time tail rounds in the 1024-lane strided tiles too
 #ifndef FLTEE_TAIL_CT_1024
-#define FLTEE_TAIL_CT_1024 0
+#define FLTEE_TAIL_CT_1024 1
 #endif
 //   FLTEE_PLAN_SHUFFLE  the keyed shuffle (mode 2) on the planned schedule too
 #ifndef FLTEE_PLAN_SHUFFLE
-#define FLTEE_PLAN_SHUFFLE 0
+#define FLTEE_PLAN_SHUFFLE 1
 #endif
 //   FLTEE_TID_FRESH   the lane id re-read per LDS round (see lane_tid)
 #ifndef FLTEE_TID_FRESH

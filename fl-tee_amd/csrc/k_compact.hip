@@ -170,10 +170,10 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
 // first pass may take as many blocks as the later ones (FLTEE_COMPACT_FIRST_BLOCKS), and 4
 // blocks (8 waves per SIMD, <= 64 VGPRs) fit too (FLTEE_COMPACT_BLOCKS; A/B builds).
 #ifndef FLTEE_COMPACT_BLOCKS
-#define FLTEE_COMPACT_BLOCKS 3
+#define FLTEE_COMPACT_BLOCKS 4
 #endif
 #ifndef FLTEE_COMPACT_FIRST_BLOCKS
-#define FLTEE_COMPACT_FIRST_BLOCKS 3
+#define FLTEE_COMPACT_FIRST_BLOCKS 4
 #endif
 constexpr int kCompactBlocks = FLTEE_COMPACT_BLOCKS;
 constexpr int kCompactFirstBlocks = FLTEE_COMPACT_FIRST_BLOCKS;
