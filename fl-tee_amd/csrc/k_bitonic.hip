@@ -48,8 +48,10 @@
 #define FLTEE_KEY_AFTER_DATA 1
 #endif
 //   FLTEE_KEYED_SPLIT  the keyed comparator as one per-lane product per step + a scalar
+//                      (off: it moves the cost to the scalar unit, C4 8.93 vs 9.01 ms with
+//                      it, `profiles/r03/ab/ab6_c4.jsonl`)
 #ifndef FLTEE_KEYED_SPLIT
-#define FLTEE_KEYED_SPLIT 1
+#define FLTEE_KEYED_SPLIT 0
 #endif
 template <int G>
 constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FLTEE_LDS_BATCH;
