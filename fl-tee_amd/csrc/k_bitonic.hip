@@ -222,6 +222,43 @@ __device__ __forceinline__ void bt_store(__amdgpu_buffer_rsrc_t rs, uint32_t vof
 // tile sort (spills at 1024 lanes; ~12 VALU per record per cross-lane step).
 constexpr int kTileCP = 0;
 
+// Block-swizzled physical layout (round 3) of the 2^14-tile networks (C4, C5): between
+// its first and its last pass a full sort keeps logical position p at physical slot
+//   phys(p) = p ^ (((h ^ (h >> 10)) << 4) & 0x3FF0),  h = p >> 14,
+// i.e. the 128-B blocks (16 records) inside each aligned 2^14-record block are permuted
+// by a function of the block's position bits >= 14.  A strided tile's rows (W = 16..128
+// consecutive records, 2^dtile apart) otherwise sit at power-of-two strides that map one
+// wave's rows onto the same HBM channels (MI355X: W = 16 rows 2^14 apart stream at 3.5
+// TB/s, swizzled 5.1, `profiles/r03/microbench_tiles_*.jsonl`).  Properties used:
+//  * bits >= 14 are unchanged, so a contiguous 2^14 tile occupies its own block in either
+//    layout (the first pass reads logical and writes physical, the last pass the other
+//    way round, both in place) and whole pad blocks are the same in both;
+//  * bits 0..3 are unchanged, so every 16-record row segment stays contiguous;
+//  * it is GF(2)-linear: phys(a ^ b) = phys(a) ^ phys(b), so for an address made of
+//    bit-disjoint fields (tile base | lane part | row part) the per-lane and the uniform
+//    parts are swizzled separately and combined with one XOR.
+// Only addresses change: positions (directions, keys) stay logical — the same network.
+constexpr uint32_t kSwzMask = 0x3FF0u;
+__device__ __forceinline__ uint32_t swz_x(uint32_t p) {
+    const uint32_t h = p >> 14;
+    return ((h ^ (h >> 10)) << 4) & kSwzMask;
+}
+__device__ __forceinline__ uint32_t phys(uint32_t p) { return p ^ swz_x(p); }
+
+// A tile record's HBM access: lane part `vl` (bytes; SW: phys(lane part) * 8) and uniform
+// record index `u` (the tile base plus the record's row part, bit-disjoint from the lane
+// part).  !SW: voffset + soffset as before; SW: one XOR into the voffset.
+template <bool SW>
+__device__ __forceinline__ uint64_t tl_load(__amdgpu_buffer_rsrc_t rs, uint32_t vl, uint32_t u) {
+    if constexpr (SW) return bt_load<kTileCP>(rs, vl ^ (phys(u) * 8u), 0u);
+    return bt_load<kTileCP>(rs, vl, u * 8u);
+}
+template <bool SW>
+__device__ __forceinline__ void tl_store(__amdgpu_buffer_rsrc_t rs, uint32_t vl, uint32_t u, uint64_t v) {
+    if constexpr (SW) bt_store<kTileCP>(rs, vl ^ (phys(u) * 8u), 0u, v);
+    else bt_store<kTileCP>(rs, vl, u * 8u, v);
+}
+
 // ------------------------------------------------------------- LDS tile ----
 __device__ __forceinline__ uint32_t lpad(uint32_t e) { return e + (e >> 4); }
 
@@ -409,7 +446,7 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 // around each prefetch load makes hipcc branch and wait vmcnt(0) per load
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
-template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true>
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true, bool SW = false>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase,
@@ -419,14 +456,18 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     if (tile >= ntiles) return;
     // record r of this lane is tile element threadIdx.x + r*NT at position
     // base + p_off + r*rstride (W <= NT for strided tiles, W = T for contiguous ones)
-    const uint32_t voff = tile_pos(0u, threadIdx.x, wlog, dtile) * 8u;  // per-lane bytes
-    const uint32_t rstride = ((uint32_t)NT << (dtile - wlog)) * 8u;     // bytes, uniform
+    // SW (static_assert: middle passes only, read and written in the swizzled layout):
+    // the lane part swizzled once, each record's uniform part (tile base + row) per access
+    static_assert(!SW || !SORT, "the first pass is bitonic_sort_direct");
+    const uint32_t lpos = tile_pos(0u, threadIdx.x, wlog, dtile);
+    const uint32_t voff = (SW ? phys(lpos) : lpos) * 8u;          // per-lane bytes
+    const uint32_t rrow = (uint32_t)NT << (dtile - wlog);         // records, uniform
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t pf[E];
     {
-        const uint32_t sb = tile_base(tile, tlog, wlog, dtile) * 8u;
+        const uint32_t sb = tile_base(tile, tlog, wlog, dtile);
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+        for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
     }
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     // a strided tile with no fused tail (seg0 == 0) starts with the stage's top row steps:
@@ -448,9 +489,9 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
         auto prefetch = [&]() {
-            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) * 8u;
+            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile);
 #pragma unroll
-            for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+            for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
         // registers are then not live through the tail)
@@ -497,11 +538,9 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                                        wlog < tlog ? (int)wlog : 0, seed);
             }
         }
-        {
-            const uint32_t sb = base * 8u;
 #pragma unroll
-            for (int r = 0; r < E; ++r) bt_store<kTileCP>(rs, voff, sb + (uint32_t)r * rstride, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
-        }
+        for (int r = 0; r < E; ++r)
+            tl_store<SW>(rs, voff, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
         tile = next;
@@ -523,7 +562,10 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
 // gives lane t the E consecutive records t*E .. t*E+E-1 (groups t*G .. t*G+G-1), so
 // one block-wide exclusive scan of the lanes' counts orders the tile's entries.  The
 // tile was read into LDS before, so the in-place writes are safe.
-template <int MODE, int E, int NT, int RL, bool STRIDED, bool SEL = false, int TL = 0>
+// SWI / SWO: the tile is read / written in the block-swizzled layout (kSwzMask; the
+// contiguous merges only: a middle merge both, the last merge of a sort SWI alone).
+template <int MODE, int E, int NT, int RL, bool STRIDED, bool SEL = false, int TL = 0,
+          bool SWI = false, bool SWO = false>
 __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict__ data,
                                                            uint32_t tlog, uint32_t ilog,
                                                            uint32_t wlog, uint32_t dtile,
@@ -541,16 +583,19 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     // contiguous: wlog = dtile = tlog.  strided: W = 2^wlog consecutive positions x T/W
     // rows at stride 2^dtile (W <= NT), as in bitonic_tiles
-    const uint32_t voff = tile_pos(0u, t, wlog, dtile) * 8u;
-    const uint32_t rstride = ((uint32_t)NT << (dtile - wlog)) * 8u;
+    static_assert(!(STRIDED && (SWI || SWO)), "swizzled layout: contiguous merges only");
+    static_assert(!(SEL && SWO), "the selection is written in position order");
+    const uint32_t lpos = tile_pos(0u, t, wlog, dtile);
+    const uint32_t voff = (SWI ? phys(lpos) : lpos) * 8u;
+    const uint32_t rrow = (uint32_t)NT << (dtile - wlog);  // records
     const uint32_t dlog1 = tlog - (uint32_t)R1;  // == log2 NT: the first round's tile-local distance
     const uint32_t dlog1_g = STRIDED ? dlog1 - wlog + dtile : dlog1;
     const uint32_t jbot = STRIDED ? wlog : 0u;  // the tile's lowest step
     uint64_t pf[E];
     {
-        const uint32_t sb = tile_base(tile, tlog, wlog, dtile) * 8u;
+        const uint32_t sb = tile_base(tile, tlog, wlog, dtile);
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+        for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
     }
     for (;;) {
         const uint32_t base = tile_base(tile, tlog, wlog, dtile);
@@ -560,9 +605,9 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         {
-            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile) * 8u;
+            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile);
 #pragma unroll
-            for (int r = 0; r < E; ++r) pf[r] = bt_load<kTileCP>(rs, voff, sb + (uint32_t)r * rstride);
+            for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
         }
         if constexpr (TL != 0 && !STRIDED)  // tlog == TL (checked by the launcher)
             lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, seed);
@@ -618,6 +663,9 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         // every group read from LDS first (the fenced stores below would otherwise keep the
         // next group's reads behind them), then computed, then stored
         constexpr int BW = kLdsBatch<G>;
+        // SWO: a contiguous tile stays in its own 2^14 block, so its records' physical
+        // offsets inside the block are (tile offset ^ swz_x(base)): one uniform XOR
+        const uint32_t sxb = SWO ? swz_x(base) : 0u;
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += BW) {
         uint64_t vv[BW][1 << RL];
@@ -653,12 +701,15 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                 // store has read them (measured: nondeterministic output); the explicit
                 // "s_nop 1" fenced by sched_barriers gives the two wait states the hazard needs
                 // (cdna_hip_programming.md §5.7: dwordx3/x4 stores end with s_nop 1).
+                // (pb is a multiple of 2^RL and sxb of 16: (pb ^ sxb) + q is the physical
+                // offset of record pb + q)
+                const uint32_t pbs = SWO ? (pb ^ sxb) : pb;
 #pragma unroll
                 for (int q = 0; q < (1 << RL); q += 2) {
                     const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
                                         (uint32_t)(v[q + 1] >> 32)};
                     __builtin_amdgcn_sched_barrier(0);
-                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((pb + (uint32_t)q) * 8u),
+                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((pbs + (uint32_t)q) * 8u),
                                                            (int)(base * 8u), kTileCP);
                     __builtin_amdgcn_sched_barrier(0);
                     asm volatile("s_nop 1" ::: "memory");
@@ -740,7 +791,9 @@ __device__ __forceinline__ uint64_t gen_entry(const SortGen &g, uint32_t p, uint
 // 1..log2 E on them without LDS, and writes them to LDS; the LDS rounds run stages
 // log2 E + 1 .. tlog; the last round of stage tlog (groups of 2^RL consecutive records)
 // stores straight to HBM (16-B stores fenced with s_nop 1, see bitonic_merge_direct).
-template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0, int LPF = 1>
+// SWO: the sorted tiles are written in the block-swizzled layout (kSwzMask; the loads
+// are logical), for a sort whose later passes run swizzled.
+template <int MODE, int E, int NT, int RL, int GEN = 0, int TL = 0, int LPF = 1, bool SWO = false>
 __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__ data,
                                                           uint32_t tlog, uint32_t seed,
                                                           uint32_t ntiles, uint32_t pbase,
@@ -895,6 +948,7 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
         // every group read from LDS first, then computed, then stored (the fenced stores
         // would otherwise hold the next group's reads behind them)
         constexpr int BW = kLdsBatch<G>;
+        const uint32_t sxb = SWO ? swz_x(base) : 0u;  // the tile's block swizzle (merge_direct)
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += BW) {
         uint64_t vv[BW][1 << RL];
@@ -910,7 +964,7 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             group_steps<MODE, RL>(vv[h], base + pbase + ((tf + (uint32_t)(h0 + h) * NT) << RL), 0u, tlog, seed);
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            const uint32_t b = (tf + (uint32_t)(h0 + h) * NT) << RL;
+            const uint32_t b = ((tf + (uint32_t)(h0 + h) * NT) << RL) ^ sxb;  // physical offset
             uint64_t (&v)[1 << RL] = vv[h];
 #pragma unroll
             for (int q = 0; q < (1 << RL); q += 2) {
@@ -942,7 +996,9 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
 // compare-exchanges (R = 6: ~290 VGPRs, one wave per SIMD).  Byte offsets are 32-bit:
 // M <= 2^29 (checked by the callers).
 
-template <int MODE, int R>
+// SW: the array is in the block-swizzled layout (a middle pass of a swizzled sort): the
+// group's first record swizzled per lane, record q's uniform part per access (one XOR).
+template <int MODE, int R, bool SW = false>
 __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
                                                       uint32_t jtop, uint32_t seed,
                                                       uint32_t ngroups, uint32_t pbase) {
@@ -950,14 +1006,23 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
     if (t >= ngroups) return;
     const uint32_t dlog = jtop - R + 1;
     const uint32_t b = spread(t, dlog, R);
-    const uint32_t voff = b * 8u;
+    const uint32_t voff = (SW ? phys(b) : b) * 8u;
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t v[1 << R];
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) v[q] = bt_load(rs, voff, (uint32_t)q << (dlog + 3));
+    for (int q = 0; q < (1 << R); ++q) {
+        if constexpr (SW) v[q] = bt_load(rs, voff ^ (phys((uint32_t)q << dlog) * 8u), 0u);
+        else v[q] = bt_load(rs, voff, (uint32_t)q << (dlog + 3));
+    }
     group_steps<MODE, R>(v, b + pbase, dlog, ilog, seed);
+    // the store addresses recomputed (one XOR each) rather than 2^R of them kept live
+    uint32_t vst = voff;
+    if constexpr (SW) asm volatile("; global swz" : "+v"(vst));
 #pragma unroll
-    for (int q = 0; q < (1 << R); ++q) bt_store(rs, voff, (uint32_t)q << (dlog + 3), v[q]);
+    for (int q = 0; q < (1 << R); ++q) {
+        if constexpr (SW) bt_store(rs, vst ^ (phys((uint32_t)q << dlog) * 8u), 0u, v[q]);
+        else bt_store(rs, voff, (uint32_t)q << (dlog + 3), v[q]);
+    }
 }
 
 // live_groups (0 = all): only the first live_groups groups run — the rest lie in stage
@@ -965,20 +1030,28 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
 template <int MODE>
 static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jtop,
                                 int R, uint32_t seed, hipStream_t s, uint32_t pbase,
-                                uint32_t live_groups = 0) {
+                                uint32_t live_groups = 0, bool sw = false) {
     uint32_t ngroups = 1u << (mlog - R);
     if (live_groups && live_groups < ngroups) ngroups = live_groups;
     if (ngroups == 0) return hipSuccess;
     const unsigned blocks = (ngroups + 255) / 256;
     net_account((uint64_t)16 * ngroups << R, "bitonic_global", s);
+#define BG_GO(R_)                                                                                  \
+    do {                                                                                           \
+        if (sw) hipLaunchKernelGGL((bitonic_global<MODE, R_, true>), dim3(blocks), dim3(256), 0, s, \
+                                   data, ilog, jtop, seed, ngroups, pbase);                        \
+        else hipLaunchKernelGGL((bitonic_global<MODE, R_>), dim3(blocks), dim3(256), 0, s, data,    \
+                                ilog, jtop, seed, ngroups, pbase);                                 \
+    } while (0)
     switch (R) {
-    case 1: hipLaunchKernelGGL((bitonic_global<MODE, 1>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
-    case 2: hipLaunchKernelGGL((bitonic_global<MODE, 2>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
-    case 3: hipLaunchKernelGGL((bitonic_global<MODE, 3>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
-    case 4: hipLaunchKernelGGL((bitonic_global<MODE, 4>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
-    case 5: hipLaunchKernelGGL((bitonic_global<MODE, 5>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
-    default: hipLaunchKernelGGL((bitonic_global<MODE, 6>), dim3(blocks), dim3(256), 0, s, data, ilog, jtop, seed, ngroups, pbase); break;
+    case 1: BG_GO(1); break;
+    case 2: BG_GO(2); break;
+    case 3: BG_GO(3); break;
+    case 4: BG_GO(4); break;
+    case 5: BG_GO(5); break;
+    default: BG_GO(6); break;
     }
+#undef BG_GO
     return hipGetLastError();
 }
 
@@ -989,7 +1062,10 @@ constexpr uint32_t kMaxTileLog = 14;  // 16384 records = 128 KB (+1/16 padding) 
 // Steps per register-blocked global pass: 6 (64 records / lane; fastest at M = 2^24, 2^27).
 constexpr int kRegMaxSteps = 6;
 // Smaller tiles until there are at least 2^8 of them (one per CU).
-constexpr uint32_t kMinTilesLog = 8;
+#ifndef FLTEE_MIN_TILES_LOG
+#define FLTEE_MIN_TILES_LOG 8
+#endif
+constexpr uint32_t kMinTilesLog = FLTEE_MIN_TILES_LOG;
 // Narrowest strided-tile row, log2: 16 records = 128-B row segments (W = 8: 14.09 vs
 // 14.03 ms at 2^27, W = 4: 14.66, W = 2: 16.37).
 constexpr int kMinWLog = 4;
@@ -1008,26 +1084,44 @@ constexpr int kMinWLog = 4;
 template <int MODE>
 constexpr int kSortLatePf = MODE == 2 ? FLTEE_SORT_LATEPF_SHUFFLE : FLTEE_SORT_LATEPF_KEY;
 
-template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
-static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
-                                   uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                   uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0) {
+template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF, bool SW>
+static hipError_t launch_tiles_sw(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog, "bitonic_tiles", s);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF>), dim3(grid), dim3(NT), lds, s,
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>), dim3(grid), dim3(NT), lds, s,
                        data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
     return hipGetLastError();
+}
+
+// sw: the pass reads and writes the block-swizzled layout (2^14 tiles of 1024 lanes only)
+template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
+static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                   uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                   uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0,
+                                   bool sw) {
+    if constexpr (!SORT && NT == 1024 && E == 16) {
+        if (sw)
+            return launch_tiles_sw<MODE, SORT, E, NT, TL, WL, LPF, true>(grid, lds, s, data, tlog, ilog,
+                                                                         wlog, dtile, seed, tiles, pbase, seg0);
+    } else {
+        if (sw) return hipErrorInvalidValue;
+    }
+    return launch_tiles_sw<MODE, SORT, E, NT, TL, WL, LPF, false>(grid, lds, s, data, tlog, ilog, wlog,
+                                                                  dtile, seed, tiles, pbase, seg0);
 }
 
 template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                 uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0) {
+                                 uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0,
+                                 bool sw = false) {
     // the compile-time strided tiles' prefetch goes after their fused tail, except for the
     // tiles with a tail on rows of 2^5 (their 9 row steps cover the load less well: 514 ->
     // 553 us at C5 with it late, while every other shape gains,
@@ -1035,11 +1129,16 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
     if constexpr (TL != 0 && WL == 5 && !SORT) {
         if (seg0 != 0)
             return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, false>(grid, lds, s, data, tlog, ilog, wlog,
-                                                                      dtile, seed, tiles, pbase, seg0);
+                                                                      dtile, seed, tiles, pbase, seg0, sw);
     }
     return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, true>(grid, lds, s, data, tlog, ilog, wlog, dtile,
-                                                             seed, tiles, pbase, seg0);
+                                                             seed, tiles, pbase, seg0, sw);
 }
+
+// The block-swizzled layout (kSwzMask) of a pass's input and output
+struct Swz {
+    bool in = false, out = false;
+};
 
 struct TileCfg {
     uint32_t tlog, E, NT;
@@ -1055,7 +1154,7 @@ struct SelSink {
 template <int MODE, int E, int NT, bool STRIDED>
 static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                 uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
-                                const SelSink &sink = SelSink{}) {
+                                const SelSink &sink = SelSink{}, Swz sw = Swz{}) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rest = (int)c.tlog - (int)(STRIDED ? wlog : 0u) - R1;  // steps after the register round
     const int rl = rest <= 0 ? 0 : (rest - 1) % R1 + 1;  // lds_steps' greedy split leaves this last
@@ -1063,20 +1162,21 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     // the select pass writes ~nothing
     net_account((uint64_t)(sink.cnt ? 8 : 16) * c.tiles << c.tlog,
                 sink.cnt ? "bitonic_merge_direct(select)" : "bitonic_merge_direct", s);
-#define BD_GO1(RL_, SEL_, TL_)                                                                     \
+#define BD_GO2(RL_, SEL_, TL_, SWI_, SWO_)                                                         \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
             (void)hipFuncSetAttribute(                                                             \
-                (const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_>,          \
+                (const void *)bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_, SWI_, SWO_>, \
                 hipFuncAttributeMaxDynamicSharedMemorySize,                                        \
                 160 * 1024 - (SEL_ ? 256 : 0)); /* static wtot[] counts against the 160 KB */      \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_>),           \
+        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_, SWI_, SWO_>), \
                            dim3(c.grid), dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, \
                            c.tiles, pbase, sink.d, sink.cnt);                                      \
     } while (0)
+#define BD_GO1(RL_, SEL_, TL_) BD_GO2(RL_, SEL_, TL_, false, false)
 #define BD_GO(RL_, TL_)                                                                            \
     do {                                                                                           \
         if (!STRIDED && sink.cnt) BD_GO1(RL_, true, TL_);                                          \
@@ -1085,12 +1185,20 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     // contiguous tiles of the usual sizes: the LDS rounds unrolled at compile time
     if constexpr (!STRIDED) {
         if constexpr (E == 16 && NT == 1024) {
-            if (c.tlog == 14 && rl == 2) { BD_GO(2, 14); return hipGetLastError(); }
+            if (c.tlog == 14 && rl == 2) {
+                if (sw.in && sw.out && !sink.cnt) BD_GO2(2, false, 14, true, true);  // a middle merge
+                else if (sw.in && !sw.out && sink.cnt) BD_GO2(2, true, 14, true, false);  // the last
+                else if (sw.in && !sw.out) BD_GO2(2, false, 14, true, false);
+                else if (sw.out) return hipErrorInvalidValue;
+                else BD_GO(2, 14);
+                return hipGetLastError();
+            }
         }
         if constexpr (E == 16 && NT == 512) {
             if (c.tlog == 13 && rl == 1) { BD_GO(1, 13); return hipGetLastError(); }
         }
     }
+    if (sw.in || sw.out) return hipErrorInvalidValue;  // swizzled: 2^14 contiguous tiles only
     switch (rl) {
     case 1: BD_GO(1, 0); break;
     case 2: if constexpr (R1 >= 2) BD_GO(2, 0); break;
@@ -1100,12 +1208,14 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     }
 #undef BD_GO
 #undef BD_GO1
+#undef BD_GO2
     return hipGetLastError();
 }
 
 template <int MODE, int E, int NT, int GEN = 0>
 static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
-                                     uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{}) {
+                                     uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{},
+                                     bool swo = false) {
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     const int rl = ((int)c.tlog - 1) % R1 + 1;  // lds_steps' greedy split of stage tlog
     SortGen gg = g;
@@ -1125,22 +1235,28 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
         bytes += (uint64_t)8 * gg.pad_n;  // ... + the pad tiles' stores
     }
     net_account(bytes, "bitonic_sort_direct", s);
-#define BS_GO_PF(RL_, TL_, LPF_)                                                                   \
+#define BS_GO_SW(RL_, TL_, LPF_, SWO_)                                                             \
     do {                                                                                           \
         static bool attr = false;                                                                  \
         if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_>, \
+            (void)hipFuncSetAttribute((const void *)bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_, SWO_>, \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_>), dim3(grid),    \
+        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_, SWO_>), dim3(grid), \
                            dim3(NT), c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);            \
     } while (0)
+#define BS_GO_PF(RL_, TL_, LPF_) BS_GO_SW(RL_, TL_, LPF_, false)
 #define BS_GO(RL_, TL_) BS_GO_PF(RL_, TL_, ((TL_) != 0 ? kSortLatePf<MODE> : 1))
     // the usual tile sizes: every stage's LDS rounds unrolled at compile time
     if constexpr (E == 16 && NT == 1024) {
-        if (c.tlog == 14 && rl == 2) { BS_GO(2, 14); return hipGetLastError(); }
+        if (c.tlog == 14 && rl == 2) {
+            if (swo) BS_GO_SW(2, 14, kSortLatePf<MODE>, true);
+            else BS_GO(2, 14);
+            return hipGetLastError();
+        }
     }
+    if (swo) return hipErrorInvalidValue;  // swizzled: 2^14 tiles of 1024 lanes only
     if constexpr (E == 16 && NT == 512) {
         if (c.tlog == 13 && rl == 1) { BS_GO(1, 13); return hipGetLastError(); }
     }
@@ -1156,27 +1272,35 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     }
 #undef BS_GO
 #undef BS_GO_PF
+#undef BS_GO_SW
     return hipGetLastError();
 }
 
+// sw: the block-swizzled layout of the pass's input / output (2^14 tiles of 1024 lanes:
+// the first pass writes it, the middle passes read and write it, the last reads it)
 template <int MODE, bool SORT>
 static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, uint32_t ilog,
                                uint32_t wlog, uint32_t dtile, uint32_t seed, uint32_t pbase,
-                               const SelSink &sink = SelSink{}, uint32_t seg0 = 0) {
+                               const SelSink &sink = SelSink{}, uint32_t seg0 = 0, Swz sw = Swz{}) {
     if (c.tiles == 0) return hipSuccess;  // every tile in pad-only stage blocks
     const bool plain = seg0 == 0 && ilog != 0;  // one segment over every row bit
     if (SORT && wlog == c.tlog && c.tlog > 6) {
-        if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase);
+        if (sw.in) return hipErrorInvalidValue;
+        if (c.NT == 1024) return launch_sort_direct<MODE, 16, 1024>(c, s, data, seed, pbase, SortGen{}, sw.out);
+        if (sw.out) return hipErrorInvalidValue;
         if (c.NT == 512 && c.E == 16) return launch_sort_direct<MODE, 16, 512>(c, s, data, seed, pbase);
         if (c.NT == 512 && c.E == 8) return launch_sort_direct<MODE, 8, 512>(c, s, data, seed, pbase);
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
     if (!SORT && plain && wlog == c.tlog && c.tlog > 6) {
-        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
-        if (c.NT == 512 && c.E == 16) return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
+        if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink, sw);
+        if (c.NT == 512 && c.E == 16 && !sw.in && !sw.out)
+            return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
     }  // (E <= 8 tiles, M <= 2^20: measured no faster, 175 vs 169 us at 2^20)
     if (sink.cnt) return hipErrorNotSupported;  // only the direct contiguous merge selects
+    // the other tile passes are in place: a swizzled one reads and writes that layout
+    if (sw.in != sw.out || (sw.in && (SORT || c.NT != 1024 || c.E != 16))) return hipErrorInvalidValue;
     // (strided tiles with the first / last round in registers were slower: 14.64 vs
     // 14.03 ms at 2^27, the last round's 8-B stores land 2^dtile apart)
     // strided passes of the usual tile sizes, rows of 2^4 .. 2^7 (and, for 2^12 tiles, the
@@ -1185,7 +1309,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
         (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512))) {
 #define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
-    case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0);
+    case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in);
         if (c.NT == 1024) {
             switch (wlog) {
                 BT_ST_CASE(16, 1024, 14, 4) BT_ST_CASE(16, 1024, 14, 5) BT_ST_CASE(16, 1024, 14, 6)
@@ -1208,7 +1332,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 #undef BT_ST_CASE
     }
 #define BT_GO(E_, NT_) \
-    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0)
+    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in)
     if (c.NT == 1024) BT_GO(16, 1024);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
@@ -1460,34 +1584,55 @@ size_t debug_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax, uint32_t 
     return plan.size();
 }
 
-// stages tlog+1 .. mlog of a full sort by the planned launches (false: no plan, use stage_steps)
+// the planned schedule of a full sort (empty: none, the per-stage one runs)
 template <int MODE>
-static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t seed, uint32_t pbase,
-                     hipStream_t s, const SelSink &sink, uint32_t valid, hipError_t &e) {
-    // the keyed shuffle (mode 2) keeps the per-stage schedule: its compare-exchanges cost
-    // more VALU (the hash multiply), which the planned tile-heavy schedule pays in LDS
-    // passes — C4: 10.15 vs 9.78 ms planned, against C5 (mode 0) 14.67 vs 15.34 ms and C3
-    // 0.157 vs 0.163 ms (`profiles/r02/ab/network_plan.jsonl`)
-    if ((MODE == 2 && !FLTEE_PLAN_SHUFFLE) || c0.tlog <= 6 || mlog <= c0.tlog) return false;
+static const std::vector<NetPass> *plan_for(uint32_t mlog, const TileCfg &c0) {
+    // (the keyed shuffle planned too since round 3: FLTEE_PLAN_SHUFFLE, `profiles/r03/ab`)
+    if ((MODE == 2 && !FLTEE_PLAN_SHUFFLE) || c0.tlog <= 6 || mlog <= c0.tlog) return nullptr;
     const int rcap = (int)mlog - 16 < 4 ? 4 : (int)mlog - 16;
     const int rmax = kRegMaxSteps < rcap ? kRegMaxSteps : rcap;
     const std::vector<NetPass> &plan = cached_plan(mlog, c0.tlog, c0.NT, rmax);
-    if (plan.empty()) return false;
+    return plan.empty() ? nullptr : &plan;
+}
+
+// Whether a full sort runs in the block-swizzled layout (kSwzMask): planned, 2^14 tiles of
+// 1024 lanes, its last launch the contiguous merge (plan_network always ends with it).
+static bool g_swizzle = true;  // fltee_debug_set_swizzle (A/B)
+void set_swizzle(int on) { g_swizzle = on != 0; }
+static bool swizzled(const std::vector<NetPass> *plan, const TileCfg &c0) {
+    if (!g_swizzle || !plan || c0.tlog != 14 || c0.NT != 1024 || c0.E != 16) return false;
+    const NetPass &l = plan->back();
+    return !l.reg && l.ilogA && !l.ilogB && l.aTop == c0.tlog - 1;
+}
+
+// stages tlog+1 .. mlog of a full sort by the planned launches (false: no plan, use
+// stage_steps).  sw: the first pass wrote the block-swizzled layout; the middle launches
+// read and write it and the last one (the contiguous merge) writes positions in order.
+template <int MODE>
+static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t seed, uint32_t pbase,
+                     hipStream_t s, const SelSink &sink, uint32_t valid, hipError_t &e,
+                     bool sw = false) {
+    const std::vector<NetPass> *pl = plan_for<MODE>(mlog, c0);
+    if (!pl) return false;
+    const std::vector<NetPass> &plan = *pl;
     e = hipSuccess;
     for (size_t k = 0; k < plan.size() && e == hipSuccess; ++k) {
         const NetPass &p = plan[k];
+        const bool last = k + 1 == plan.size();
+        const Swz io{sw, sw && !last};
         const uint32_t skip = g_pad_skip ? skip_from(valid, p.stage, mlog) : 0u;
         if (p.reg) {
-            e = launch_global<MODE>(data, mlog, p.ilog, p.jtop, (int)p.R, seed, s, pbase, skip >> p.R);
+            if (io.in != io.out) { e = hipErrorInvalidValue; break; }
+            e = launch_global<MODE>(data, mlog, p.ilog, p.jtop, (int)p.R, seed, s, pbase, skip >> p.R, sw);
             continue;
         }
         const TileCfg c = live_tiles(c0, skip);
         if (p.ilogA && !p.ilogB && p.aTop == c0.tlog - 1)  // a whole contiguous merge
             e = launch_tiles<MODE, false>(c, s, data, p.ilogA, c0.tlog, c0.tlog, seed, pbase,
-                                          k + 1 == plan.size() ? sink : SelSink{});
+                                          last ? sink : SelSink{}, 0u, io);
         else
             e = launch_tiles<MODE, false>(c, s, data, p.ilogB, p.wlog, p.dtile, seed, pbase, SelSink{},
-                                          p.ilogA ? ((p.ilogA << 8) | p.aTop) : 0u);
+                                          p.ilogA ? ((p.ilogA << 8) | p.aTop) : 0u, io);
     }
     return true;
 }
@@ -1512,10 +1657,12 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
         }
         return hipSuccess;
     }
+    // a full sort on the planned schedule runs in the block-swizzled layout where it can
+    const bool sw = slog == mlog && swizzled(plan_for<MODE>(mlog, c), c);
     e = launch_tiles<MODE, true>(live_tiles(c, skip_from(valid, c.tlog, mlog)), s, data, 0u, c.tlog,
-                                 c.tlog, seed, pbase);
+                                 c.tlog, seed, pbase, SelSink{}, 0u, Swz{false, sw});
     if (e != hipSuccess) return e;
-    if (slog == mlog && run_plan<MODE>(data, mlog, c, seed, pbase, s, SelSink{}, valid, e)) return e;
+    if (slog == mlog && run_plan<MODE>(data, mlog, c, seed, pbase, s, SelSink{}, valid, e, sw)) return e;
     for (uint32_t ilog = c.tlog + 1; ilog <= slog; ++ilog) {
         e = stage_steps<MODE>(data, mlog, c, ilog, (int)ilog - 1, seed, pbase, s, SelSink{}, valid);
         if (e != hipSuccess) return e;
@@ -1626,12 +1773,13 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     gp.pad_begin = (uint32_t)done;
     gp.pad_n = (uint32_t)(m - done);
     hipError_t e;
-    if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, gp);
+    const bool sw = swizzled(plan_for<MODE>(mlog, c0), c0);  // (pad blocks: whole 2^14 blocks)
+    if (c.NT == 1024) e = launch_sort_direct<MODE, 16, 1024, GEN>(c, s, data, seed, 0u, gp, sw);
     else if (c.NT == 512 && c.E == 16) e = launch_sort_direct<MODE, 16, 512, GEN>(c, s, data, seed, 0u, gp);
     else if (c.NT == 512 && c.E == 8) e = launch_sort_direct<MODE, 8, 512, GEN>(c, s, data, seed, 0u, gp);
     else return hipErrorNotSupported;
     if (e != hipSuccess) return e;
-    if (run_plan<MODE>(data, mlog, c0, seed, 0u, s, sink, valid, e)) return e;
+    if (run_plan<MODE>(data, mlog, c0, seed, 0u, s, sink, valid, e, sw)) return e;
     for (uint32_t ilog = c0.tlog + 1; ilog <= mlog; ++ilog) {
         e = stage_steps<MODE>(data, mlog, c0, ilog, (int)ilog - 1, seed, 0u, s,
                               ilog == mlog ? sink : SelSink{}, valid);

@@ -534,6 +534,37 @@ def test_pad_skip_bit_identical(dev, oracle, alg, n, d, k):
         assert st == 0 and bits_equal(outs[0], ref)
 
 
+@pytest.mark.parametrize("alg,n,d,k", [(1, 40, 1_000_000, 60_000), (1, 300, 44964, 14000),
+                                       (2, 300, 44964, 4496), (4, 64, 1 << 24, 65536),
+                                       (1, 1000, 10_000_000, 100_000)])
+def test_swizzled_layout_bit_identical(dev, oracle, alg, n, d, k):
+    """The 2^14-tile networks keep the array in the block-swizzled layout between their
+    first and last pass (k_bitonic.hip kSwzMask): addresses only, the same bits as the
+    plain layout — advanced (mode 0) at 2^22 and at C5's 2^27, nips19's keyed shuffle
+    (mode 2, with the selection sink) at C4's 2^27, non_oblivious's composite sort (mode
+    1) at 2^22 — and, where the oracle finishes in seconds, the oracle's bits."""
+    from fltee import _lib as L
+    rng = np.random.default_rng(n * 11 + d)
+    if n * k > 10_000_000:
+        idx = ((rng.integers(0, d, n)[:, None] + np.arange(k)[None, :]) % d).reshape(-1).astype(np.uint32)
+        val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    else:
+        idx, val = rand_sparse(rng, n, d, k)
+    rec = cuda_records(dev, idx, val)
+    outs = []
+    for on in (1, 0):
+        L.lib().fltee_debug_set_swizzle(on)
+        try:
+            outs.append(dev.aggregate(alg, rec, n, k, d, seed=91).cpu().numpy())
+        finally:
+            L.lib().fltee_debug_set_swizzle(1)
+        assert dev.status() == 0
+    assert bits_equal(outs[0], outs[1])
+    if n * k <= 4_200_000 and alg == 1:
+        ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+        assert st == 0 and bits_equal(outs[0], ref)
+
+
 @pytest.mark.parametrize("n,d,k,repeat", [(100, 50890, 5089, False), (1000, 200000, 2000, False),
                                           (3, 1000, 1000, False), (30, 3000, 400, True),
                                           (3000, 30000, 16, False), (5000, 20000, 20, False)])
