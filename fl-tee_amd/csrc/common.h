@@ -10,6 +10,19 @@
 // One record of the wire / HBM layout: parameters.rs:3-10 Weight(u32 idx, f32 val),
 // little-endian, 8 bytes.  Kept as a u64 in registers: low word = idx, high = val bits.
 __device__ __forceinline__ uint32_t rec_idx(uint64_t r) { return (uint32_t)r; }
+
+// Block-swizzled physical layout of the large record arrays between the passes of a
+// network (k_bitonic.hip: the 2^14-tile sorts): logical
+// position p lives at phys(p) = p ^ swz_x(p), the 128-B blocks (16 records) of each
+// aligned 2^14-record block permuted by the block's position bits >= 14, so that rows at
+// power-of-two strides do not land on the same HBM channels.  Bits >= 14 and bits 0..3
+// are unchanged; GF(2)-linear: phys(a ^ b) = phys(a) ^ phys(b).
+constexpr uint32_t kSwzMask = 0x3FF0u;
+__device__ __forceinline__ uint32_t swz_x(uint32_t p) {
+    const uint32_t h = p >> 14;
+    return ((h ^ (h >> 10)) << 4) & kSwzMask;
+}
+__device__ __forceinline__ uint32_t phys(uint32_t p) { return p ^ swz_x(p); }
 __device__ __forceinline__ float rec_val(uint64_t r) { return __uint_as_float((uint32_t)(r >> 32)); }
 __device__ __forceinline__ uint64_t make_rec(uint32_t idx, float val) {
     return ((uint64_t)__float_as_uint(val) << 32) | idx;

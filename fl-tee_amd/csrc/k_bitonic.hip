@@ -222,8 +222,9 @@ __device__ __forceinline__ void bt_store(__amdgpu_buffer_rsrc_t rs, uint32_t vof
 // tile sort (spills at 1024 lanes; ~12 VALU per record per cross-lane step).
 constexpr int kTileCP = 0;
 
-// Block-swizzled physical layout (round 3) of the 2^14-tile networks (C4, C5): between
-// its first and its last pass a full sort keeps logical position p at physical slot
+// Block-swizzled physical layout (round 3, common.h phys) of the 2^14-tile networks (C4,
+// C5): between its first and its last pass a full sort keeps logical position p at
+// physical slot
 //   phys(p) = p ^ (((h ^ (h >> 10)) << 4) & 0x3FF0),  h = p >> 14,
 // i.e. the 128-B blocks (16 records) inside each aligned 2^14-record block are permuted
 // by a function of the block's position bits >= 14.  A strided tile's rows (W = 16..128
@@ -238,13 +239,6 @@ constexpr int kTileCP = 0;
 //    bit-disjoint fields (tile base | lane part | row part) the per-lane and the uniform
 //    parts are swizzled separately and combined with one XOR.
 // Only addresses change: positions (directions, keys) stay logical — the same network.
-constexpr uint32_t kSwzMask = 0x3FF0u;
-__device__ __forceinline__ uint32_t swz_x(uint32_t p) {
-    const uint32_t h = p >> 14;
-    return ((h ^ (h >> 10)) << 4) & kSwzMask;
-}
-__device__ __forceinline__ uint32_t phys(uint32_t p) { return p ^ swz_x(p); }
-
 // A tile record's HBM access: lane part `vl` (bytes; SW: phys(lane part) * 8) and uniform
 // record index `u` (the tile base plus the record's row part, bit-disjoint from the lane
 // part).  !SW: voffset + soffset as before; SW: one XOR into the voffset.

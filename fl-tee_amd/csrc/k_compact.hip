@@ -495,8 +495,13 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const size_t Hr = fold_context(halo);
     // A/B in one process (scripts/ab_fold_compact.py, profiles/r02/ab/fold_compact.jsonl):
     // C3 (Hr = 112): 0.211 vs 0.214 ms with the separate fold; C5 (Hr = 1008, windows 25 %
-    // wider than the tile): 17.66 vs 17.48 ms.  Fused while the halo is under 1/8 of the tile.
-    if (!g_fold_compact || d == 0 || L <= d || Hr > 512 || M >= ((size_t)1 << 29) || L > M)
+    // wider than the tile): 17.66 vs 17.48 ms in round 2, when it stayed separate; round 3
+    // (spill-free compaction): C5 13.22 vs 13.32 ms fused (`profiles/r03/ab/ab10_*`), so the
+    // fold is fused whenever the halo fits two window slots per lane (Hr < 1024).
+    // (Tried in round 3 and not kept: batched branch-free level rounds, 505.6 -> 517 us per
+    // pass; the block-swizzled layout between the passes, 508 -> 503 us, `ab12_*`, `ab13_*`;
+    // 64 KiB tiles, 3 passes of 6 levels, as slow as 4 of 5, `ab11_*`.)
+    if (!g_fold_compact || d == 0 || L <= d || Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
         return hipErrorNotSupported;
     const uint32_t nlev = bitlen(L - d);
     const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1;
