@@ -107,7 +107,6 @@ hipError_t bitonic_sort(uint64_t *data, size_t m, uint32_t mode, uint32_t seed, 
                         size_t valid = 0);
 void set_pad_skip(int on);
 void set_swizzle(int on);
-void set_shuffle_index(int on);
 bool pad_skip_enabled();
 size_t debug_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax, uint32_t *out, size_t cap);
 // stages up to log2(seg) only: aligned segments of seg records sorted, alternating

@@ -801,7 +801,6 @@ extern "C" void fltee_debug_set_fold_compact(int on) { fltee::set_fold_compact(o
 // A/B hook: 0 runs the networks over the pad-only stage blocks too
 extern "C" void fltee_debug_set_pad_skip(int on) { fltee::set_pad_skip(on); }
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
-extern "C" void fltee_debug_set_shuffle_index(int on) { fltee::set_shuffle_index(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes
 extern "C" void fltee_debug_set_nips19_fused_select(int on) { fltee::g_nips19_fused_select = on != 0; }

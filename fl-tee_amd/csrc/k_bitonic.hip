@@ -119,10 +119,8 @@ __device__ __forceinline__ uint32_t keyed_c(uint32_t key, uint32_t dq) {
 // records held in v[], whose first record sits at global position p0.  The group
 // spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
 // is the same for every compare-exchange of the group: computed once.
-// T: the element — an 8-B record, or (the keyed shuffle's index networks, whose swap
-// decisions do not read the data) a u32 tile slot index.
-template <int MODE, int R, typename T = uint64_t>
-__device__ __forceinline__ void group_steps(T (&v)[1 << R], uint32_t p0, uint32_t dlog,
+template <int MODE, int R>
+__device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, uint32_t dlog,
                                             uint32_t ilog, uint32_t seed) {
     if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
     const bool asc = (p0 & (1u << ilog)) == 0;
@@ -148,7 +146,7 @@ __device__ __forceinline__ void group_steps(T (&v)[1 << R], uint32_t p0, uint32_
         for (int q = 0, k = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const T a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool s = sw[k++];
             v[q] = s ? c : a;
             v[qm] = s ? a : c;
@@ -158,7 +156,7 @@ __device__ __forceinline__ void group_steps(T (&v)[1 << R], uint32_t p0, uint32_
         for (int q = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const T a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool sw = decide(q, qm);
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
@@ -178,7 +176,6 @@ __device__ __forceinline__ uint64_t lds_ld(const uint64_t *p) {
     return *p;
 #endif
 }
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *p; }
 
 // The lane id, re-defined where it is read (FLTEE_TID_FRESH): a round's per-lane LDS
 // addresses are then computed in the round (a few VALU) instead of being hoisted out of
@@ -350,8 +347,8 @@ __device__ __forceinline__ uint32_t round_group(uint32_t t, int h, int NT, int W
     return (t & 63u) | ((uint32_t)h << 6) | ((t >> 6) << (6 + gl));
 }
 
-template <int MODE, int R, int E, int NT, int DLOG, int WL = 0, int WB = 0, typename T = uint64_t>
-__device__ __forceinline__ void lds_round_ct(T *sm, uint32_t base, uint32_t ilog,
+template <int MODE, int R, int E, int NT, int DLOG, int WL = 0, int WB = 0>
+__device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     static_assert(WL == 0 || DLOG >= WL || DLOG + R <= WL, "a round stays on one side of bit WL");
     static_assert(WB == 0 || (WL == 0 && DLOG + R <= WB && (64 * E) == (1 << WB)), "wave-local round");
@@ -361,13 +358,13 @@ __device__ __forceinline__ void lds_round_ct(T *sm, uint32_t base, uint32_t ilog
     constexpr int BW = kLdsBatch<G>;
 #pragma unroll
     for (int h0 = 0; h0 < G; h0 += BW) {
-    T v[BW][1 << R];
+    uint64_t v[BW][1 << R];
     uint32_t b[BW];
 #pragma unroll
     for (int h = 0; h < BW; ++h) {
         b[h] = spread(round_group<G>(lane_tid<NT>(), h0 + h, NT, WB), (uint32_t)DLOG, (uint32_t)R);
         if constexpr (DLOG + R >= 4) {
-            const T *row = sm + lpad(b[h]);
+            const uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) v[h][q] = lds_ld(&row[(q << DLOG) + ((q << DLOG) >> 4)]);
         } else {  // a group inside 16 records: the padding slot may fall between its records
@@ -383,7 +380,7 @@ __device__ __forceinline__ void lds_round_ct(T *sm, uint32_t base, uint32_t ilog
 #pragma unroll
     for (int h = 0; h < BW; ++h) {
         if constexpr (DLOG + R >= 4) {
-            T *row = sm + lpad(b[h]);
+            uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[h][q];
         } else {
@@ -395,16 +392,16 @@ __device__ __forceinline__ void lds_round_ct(T *sm, uint32_t base, uint32_t ilog
 }
 // WB > 0: wave-local rounds (see round_group), ordered by the wave's own LDS order
 // (a compiler-only barrier between them) instead of block barriers
-template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0, int WB = 0, typename T = uint64_t>
-__device__ __forceinline__ void lds_steps_ct(T *sm, uint32_t base, uint32_t ilog,
+template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0, int WB = 0>
+__device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     if constexpr (JTOP >= JBOT) {
         constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
         constexpr int r = JTOP - JBOT + 1 < rmax ? JTOP - JBOT + 1 : rmax;
-        lds_round_ct<MODE, r, E, NT, JTOP - r + 1, WL, WB, T>(sm, base, ilog, seed, dtile);
+        lds_round_ct<MODE, r, E, NT, JTOP - r + 1, WL, WB>(sm, base, ilog, seed, dtile);
         if constexpr (WB) wave_lds_order();
         else __syncthreads();
-        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT, WL, WB, T>(sm, base, ilog, seed, dtile);
+        lds_steps_ct<MODE, E, NT, JTOP - r, JBOT, WL, WB>(sm, base, ilog, seed, dtile);
     }
 }
 
@@ -416,19 +413,19 @@ __device__ __forceinline__ void lds_steps_ct(T *sm, uint32_t base, uint32_t ilog
 // of the first round (a block barrier, or the wave's own order when WAVE_FIRST).
 template <int E>
 constexpr int kWaveLog = E >= 32 ? 11 : (E >= 16 ? 10 : (E >= 8 ? 9 : (E >= 4 ? 8 : 7)));
-template <int MODE, int E, int NT, int IL, int TL, int RL, typename T = uint64_t>
-__device__ __forceinline__ void sort_stages_ct(T *sm, uint32_t base, uint32_t seed) {
+template <int MODE, int E, int NT, int IL, int TL, int RL>
+__device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
     constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
     if constexpr (IL < TL) {
         if constexpr (WB && IL <= WB) {
-            lds_steps_ct<MODE, E, NT, IL - 1, 0, 0, WB, T>(sm, base, (uint32_t)IL, seed);
+            lds_steps_ct<MODE, E, NT, IL - 1, 0, 0, WB>(sm, base, (uint32_t)IL, seed);
             if constexpr (IL == WB) __syncthreads();  // the next stage crosses waves
         } else {
-            lds_steps_ct<MODE, E, NT, IL - 1, 0, 0, 0, T>(sm, base, (uint32_t)IL, seed);
+            lds_steps_ct<MODE, E, NT, IL - 1, 0>(sm, base, (uint32_t)IL, seed);
         }
-        sort_stages_ct<MODE, E, NT, IL + 1, TL, RL, T>(sm, base, seed);
+        sort_stages_ct<MODE, E, NT, IL + 1, TL, RL>(sm, base, seed);
     } else {
-        lds_steps_ct<MODE, E, NT, TL - 1, RL, 0, 0, T>(sm, base, (uint32_t)TL, seed);
+        lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base, (uint32_t)TL, seed);
     }
 }
 
@@ -723,8 +720,8 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 
 // Stage IL (< log2 E) on a lane's E consecutive records at positions p0..p0+E-1: the
 // records form E / 2^IL whole stage blocks, each with its own direction.
-template <int MODE, int IL, int E, typename T = uint64_t>
-__device__ __forceinline__ void lane_stage(T (&v)[E], uint32_t p0, uint32_t seed) {
+template <int MODE, int IL, int E>
+__device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32_t seed) {
     constexpr int B = 1 << IL;
     if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
 #pragma unroll
@@ -747,7 +744,7 @@ __device__ __forceinline__ void lane_stage(T (&v)[E], uint32_t p0, uint32_t seed
         for (int q = 0, k = 0; q < E; ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const T a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool s = sw[k++];
             v[q] = s ? c : a;
             v[qm] = s ? a : c;
@@ -984,160 +981,6 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
     }
 }
 
-// The keyed shuffle's first pass (MODE 2) as an INDEX network.  Its swap decisions read
-// positions only (cond2<2>), so the network is a fixed permutation of each tile: it runs
-// on u32 tile slot indices (two v_cndmask per compare-exchange instead of four, 4-B LDS
-// elements instead of 8) while the tile's records wait in registers; then every lane
-// reads the final index of its E output positions, the records go to LDS at their input
-// slots and each output position gathers its record.  The same compare-exchanges in the
-// same order: the same permutation, bit for bit.  LDS: the index network (68 KB) and then
-// the records (136 KB) in the same space.  The next tile's loads go out before the
-// network (the records of the current tile are already in `cur`).
-template <int E, int NT, int TL, int GEN = 0, bool SWO = false>
-__global__ __launch_bounds__(NT) void bitonic_shuffle_direct(uint64_t *__restrict__ data,
-                                                             uint32_t tlog, uint32_t seed,
-                                                             uint32_t ntiles, uint32_t pbase,
-                                                             SortGen g) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
-    uint32_t *si = reinterpret_cast<uint32_t *>(sm);
-    constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
-    static_assert((1 << R1) == E && TL > R1, "tile shape");
-    const uint32_t t = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
-    if (g.pad_n && blockIdx.x >= g.grid_live) {  // store-only blocks (whole pad tiles)
-        const uint32_t nb = gridDim.x - g.grid_live;
-        const bt_u32x4 pad = {0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u};
-        for (uint32_t i = (blockIdx.x - g.grid_live) * (uint32_t)NT + t; i < g.pad_n / 2u;
-             i += nb * (uint32_t)NT) {
-            __builtin_amdgcn_raw_buffer_store_b128(pad, rs, (int)(i * 16u), (int)(g.pad_begin * 8u),
-                                                   kTileCP);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 1" ::: "memory");  // dwordx4 store data hazard (bitonic_merge_direct)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return;
-    }
-    const uint32_t stride = g.pad_n ? g.grid_live : gridDim.x;
-    uint32_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    // the producer (GEN) exactly as in bitonic_sort_direct
-    uint32_t nloc = 0;
-    if (GEN) {
-        nloc = g.nrec > pbase ? g.nrec - pbase : 0u;
-        const uint32_t m = ntiles << tlog;
-        if (nloc > m) nloc = m;
-    }
-    const uint64_t lbytes = (uint64_t)nloc * 8u;
-    const __amdgpu_buffer_rsrc_t ls =
-        GEN ? __builtin_amdgcn_make_buffer_rsrc((void *)g.rec, (short)0,
-                                                (int)(lbytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)lbytes),
-                                                0x00020000)
-            : rs;
-    const uint32_t voff = t * (uint32_t)E * 8u;
-    uint64_t last_rec = 0;
-    if (GEN && (nloc & 1u)) last_rec = g.rec[nloc - 1u];
-    const __amdgpu_buffer_rsrc_t lr =
-        GEN == 2 ? __builtin_amdgcn_make_buffer_rsrc((void *)g.r, (short)0, (int)(g.d * 4u), 0x00020000) : rs;
-    uint64_t pf[E];
-    uint32_t lap[2] = {0u, 0u};
-    auto first_entry = [&](uint32_t tl, uint32_t &gi, uint32_t &gj) {
-        const uint32_t p0 = pbase + (tl << tlog) + t * (uint32_t)E;
-        const uint32_t e0 = p0 > g.nrec ? p0 - g.nrec : 0u;
-        gi = g.tf ? e0 / g.tf : 0u;
-        gj = e0 - gi * g.tf;
-    };
-    auto issue = [&](uint32_t tl) {
-        const uint32_t sb = (tl << tlog) * 8u;
-#pragma unroll
-        for (int r = 0; r < E; r += 2) {
-            const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(ls, (int)(voff + (uint32_t)r * 8u),
-                                                                      (int)sb, kTileCP);
-            pf[r] = ((uint64_t)x.y << 32) | x.x;
-            pf[r + 1] = ((uint64_t)x.w << 32) | x.z;
-        }
-        if constexpr (GEN == 2) {
-            uint32_t gi, gj;
-            first_entry(tl, gi, gj);
-            lap[0] = __builtin_amdgcn_raw_buffer_load_b32(lr, (int)(gi * 4u), 0, 0);
-            lap[1] = __builtin_amdgcn_raw_buffer_load_b32(lr, (int)(gi * 4u + 4u), 0, 0);
-        }
-    };
-    auto finish = [&](uint32_t tl) {
-        if constexpr (GEN != 0) {
-            const uint32_t x0 = (tl << tlog) + t * (uint32_t)E;
-#pragma unroll
-            for (int r = 0; r < E; r += 2)
-                pf[r] = (x0 + (uint32_t)r + 1u == nloc) ? last_rec : pf[r];
-            if constexpr (GEN == 1) {
-#pragma unroll
-                for (int q = 0; q < E; ++q) pf[q] = gen_entry<GEN>(g, pbase + x0 + (uint32_t)q, pf[q]);
-            } else {
-                uint32_t gi, gj;
-                first_entry(tl, gi, gj);
-                const uint32_t gi0 = gi;
-                const bool two = g.tf >= (uint32_t)E;
-#pragma unroll
-                for (int q = 0; q < E; ++q) {
-                    if (pbase + x0 + (uint32_t)q >= g.nrec) {
-                        const uint32_t ri = two ? (gi == gi0 ? lap[0] : lap[1]) : (gi < g.d ? g.r[gi] : 0u);
-                        pf[q] = (g.tf == 0 || gi >= g.d || ri >= gj) ? 0xFFFFFFFFull : (uint64_t)gi;
-                        if (++gj == g.tf) { gj = 0; ++gi; }
-                    }
-                }
-            }
-        }
-    };
-    issue(tile);
-    for (;;) {
-        finish(tile);
-        uint64_t cur[E];
-#pragma unroll
-        for (int q = 0; q < E; ++q) cur[q] = pf[q];
-        const uint32_t next = tile + stride;
-        issue(next < ntiles ? next : tile);  // in flight through the whole index network
-        const uint32_t base = tile << tlog;
-        const uint32_t p0 = base + pbase + t * (uint32_t)E;
-        uint32_t ix[E];
-#pragma unroll
-        for (int q = 0; q < E; ++q) ix[q] = t * (uint32_t)E + (uint32_t)q;
-        lane_stage<2, 1, E>(ix, p0, seed);
-        if constexpr (R1 >= 2) lane_stage<2, (R1 >= 2 ? 2 : 1), E>(ix, p0, seed);
-        if constexpr (R1 >= 3) lane_stage<2, (R1 >= 3 ? 3 : 1), E>(ix, p0, seed);
-        if constexpr (R1 >= 4) lane_stage<2, (R1 >= 4 ? 4 : 1), E>(ix, p0, seed);
-        if constexpr (R1 >= 5) lane_stage<2, (R1 >= 5 ? 5 : 1), E>(ix, p0, seed);
-#pragma unroll
-        for (int q = 0; q < E; ++q) si[lpad(t * (uint32_t)E + (uint32_t)q)] = ix[q];
-        if constexpr (FLTEE_WAVE_LOCAL && R1 + 1 <= kWaveLog<E>) wave_lds_order();
-        else __syncthreads();
-        sort_stages_ct<2, E, NT, R1 + 1, TL, 0, uint32_t>(si, base + pbase, seed);  // ends in a barrier
-        // the permutation: output position t*E + q takes the record of input slot pm[q]
-        uint32_t pm[E];
-#pragma unroll
-        for (int q = 0; q < E; ++q) pm[q] = si[lpad(t * (uint32_t)E + (uint32_t)q)];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < E; ++q) sm[lpad(t * (uint32_t)E + (uint32_t)q)] = cur[q];
-        __syncthreads();
-        // gather and store: the lane's E consecutive output records as 16-B stores (SWO:
-        // at their block-swizzled slots, a multiple-of-16 XOR of the tile offset)
-        const uint32_t b = (t * (uint32_t)E) ^ (SWO ? swz_x(base) : 0u);
-#pragma unroll
-        for (int q = 0; q < E; q += 2) {
-            const uint64_t v0 = sm[lpad(pm[q])], v1 = sm[lpad(pm[q + 1])];
-            const bt_u32x4 x = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)};
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u), (int)(base * 8u),
-                                                   kTileCP);
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_nop 1" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (next >= ntiles) break;
-        __syncthreads();  // the gathers retire before the next tile's index network
-        tile = next;
-    }
-}
-
 // --------------------------------------------------------- global pass -----
 // Steps jtop..jtop-R+1 of stage ilog straight from HBM: lane t owns group t.
 // Record q of a group sits at byte (q << dlog) * 8 + b * 8: a wave-uniform part and
@@ -1363,10 +1206,6 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
     return hipGetLastError();
 }
 
-// the keyed shuffle's first pass as an index network (fltee_debug_set_shuffle_index, A/B)
-static bool g_shuffle_index = true;
-void set_shuffle_index(int on) { g_shuffle_index = on != 0; }
-
 template <int MODE, int E, int NT, int GEN = 0>
 static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
                                      uint32_t seed, uint32_t pbase, const SortGen &g = SortGen{},
@@ -1403,26 +1242,6 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
     } while (0)
 #define BS_GO_PF(RL_, TL_, LPF_) BS_GO_SW(RL_, TL_, LPF_, false)
 #define BS_GO(RL_, TL_) BS_GO_PF(RL_, TL_, ((TL_) != 0 ? kSortLatePf<MODE> : 1))
-    // the keyed shuffle's 2^14 tiles: the index network (bitonic_shuffle_direct)
-    if constexpr (MODE == 2 && E == 16 && NT == 1024) {
-        if (c.tlog == 14 && g_shuffle_index) {
-#define BX_GO(SWO_)                                                                                \
-    do {                                                                                           \
-        static bool attr = false;                                                                  \
-        if (!attr) {                                                                               \
-            (void)hipFuncSetAttribute((const void *)bitonic_shuffle_direct<E, NT, 14, GEN, SWO_>,   \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
-            attr = true;                                                                           \
-        }                                                                                          \
-        hipLaunchKernelGGL((bitonic_shuffle_direct<E, NT, 14, GEN, SWO_>), dim3(grid), dim3(NT),   \
-                           c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);                      \
-    } while (0)
-            if (swo) BX_GO(true);
-            else BX_GO(false);
-#undef BX_GO
-            return hipGetLastError();
-        }
-    }
     // the usual tile sizes: every stage's LDS rounds unrolled at compile time
     if constexpr (E == 16 && NT == 1024) {
         if (c.tlog == 14 && rl == 2) {

@@ -109,7 +109,6 @@ EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_set_fold_compact": (None, [ctypes.c_int]),
     "fltee_debug_set_pad_skip": (None, [ctypes.c_int]),
     "fltee_debug_set_swizzle": (None, [ctypes.c_int]),
-    "fltee_debug_set_shuffle_index": (None, [ctypes.c_int]),
     "fltee_debug_sort_fused": (_U32, [_U32, _P, _S, _P, _S, _P, _S, _S,
                                        _U32, _P]),
 }

@@ -565,29 +565,6 @@ def test_swizzled_layout_bit_identical(dev, oracle, alg, n, d, k):
         assert st == 0 and bits_equal(outs[0], ref)
 
 
-@pytest.mark.parametrize("n,d,k,dp", [(300, 44964, 4496, True), (10, 16000, 1000, False),
-                                      (20, 20000, 2000, True)])
-def test_shuffle_index_network_bit_identical(dev, n, d, k, dp):
-    """The keyed shuffle's first pass runs as an index network (k_bitonic.hip
-    bitonic_shuffle_direct: the swap decisions read positions only): the same permutation,
-    hence the same nips19 aggregate bits, as the record network — at C4's 2^27 and at
-    2^22 / 2^24 (the oracle's own bits there: test_nips19_fused_selection_bit_exact)."""
-    from fltee import _lib as L
-    rng = np.random.default_rng(n * 13 + k)
-    idx, val = rand_sparse(rng, n, d, k)
-    rec = cuda_records(dev, idx, val)
-    kw = dict(seed=5, dp=dp, sigma=1.0, clipping=1.0)
-    outs = []
-    for on in (1, 0):
-        L.lib().fltee_debug_set_shuffle_index(on)
-        try:
-            outs.append(dev.aggregate(2, rec, n, k, d, **kw).cpu().numpy())
-        finally:
-            L.lib().fltee_debug_set_shuffle_index(1)
-        assert dev.status() == 0
-    assert bits_equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("n,d,k,repeat", [(100, 50890, 5089, False), (1000, 200000, 2000, False),
                                           (3, 1000, 1000, False), (30, 3000, 400, True),
                                           (3000, 30000, 16, False), (5000, 20000, 20, False)])
