@@ -109,6 +109,8 @@ void set_pad_skip(int on);
 void set_swizzle(int on);
 bool pad_skip_enabled();
 size_t debug_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax, uint32_t *out, size_t cap);
+void debug_pad_units(uint32_t mode, uint32_t valid, uint32_t mlog, uint32_t pbase, uint32_t ilog,
+                     uint32_t jstep, uint32_t sblog, uint32_t uplog, uint32_t out[3]);
 // stages up to log2(seg) only: aligned segments of seg records sorted, alternating
 // ascending (even segments) / descending (odd segments)
 hipError_t bitonic_sort_segments(uint64_t *data, size_t m, size_t seg, uint32_t mode,

@@ -720,6 +720,13 @@ extern "C" size_t fltee_debug_network_plan(uint32_t mlog, uint32_t tlog, uint32_
     return fltee::debug_plan(mlog, tlog, nt, rmax, out, cap);
 }
 
+// the pad-only units a network launch skips (k_bitonic.hip pad_units): {live, hole_at, hole_len}
+extern "C" void fltee_debug_pad_units(uint32_t mode, uint32_t valid, uint32_t mlog, uint32_t pbase,
+                                      uint32_t ilog, uint32_t jstep, uint32_t sblog, uint32_t uplog,
+                                      uint32_t *out) {
+    fltee::debug_pad_units(mode, valid, mlog, pbase, ilog, jstep, sblog, uplog, out);
+}
+
 // measurement hook: streaming passes launched and the bytes they sweep since the last reset
 extern "C" void fltee_debug_net_stats(uint64_t *launches, uint64_t *bytes, int reset) {
     if (launches) *launches = fltee::g_net_launches.load();

@@ -270,6 +270,12 @@ __device__ __forceinline__ uint32_t tile_pos(uint32_t base, uint32_t e, uint32_t
     return base + (e & ((1u << wlog) - 1u)) + ((e >> wlog) << dtile);
 }
 
+// Tile / group t of a launch that skips the hole_len pad-only units from hole_at on
+// (pad_map): units are numbered in position order, the live ones run as 0 .. n-1.
+__device__ __forceinline__ uint32_t past_hole(uint32_t t, uint32_t hole_at, uint32_t hole_len) {
+    return t >= hole_at ? t + hole_len : t;
+}
+
 // One LDS round: steps at tile-local bits jtop..jtop-R+1 of stage ilog over the whole
 // tile of T = E * NT records.  Lane t handles the G = E >> R groups t + h*NT (R <=
 // log2 E, so every lane is busy).  A round never straddles bit wlog, so the group's
@@ -444,10 +450,11 @@ template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF =
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase,
-                                                    uint32_t seg0) {
+                                                    uint32_t seg0, uint32_t hole_at, uint32_t hole_len) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
+    // ntiles live tiles; the hole_len tiles from hole_at on hold pads alone (pad_map)
     // record r of this lane is tile element threadIdx.x + r*NT at position
     // base + p_off + r*rstride (W <= NT for strided tiles, W = T for contiguous ones)
     // SW (static_assert: middle passes only, read and written in the swizzled layout):
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t pf[E];
     {
-        const uint32_t sb = tile_base(tile, tlog, wlog, dtile);
+        const uint32_t sb = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
     }
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     // (one LDS write + read of the tile less, as in bitonic_merge_direct)
     constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && (TL - R1) >= WL;
     for (;;) {
-        const uint32_t base = tile_base(tile, tlog, wlog, dtile);
+        const uint32_t base = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
         const bool head_reg = kHeadReg && seg0 == 0;
         if constexpr (kHeadReg) {
             if (head_reg)
@@ -483,7 +490,8 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
         auto prefetch = [&]() {
-            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile);
+            const uint32_t sb = tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog,
+                                          wlog, dtile);
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
         };
@@ -565,7 +573,8 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                                                            uint32_t wlog, uint32_t dtile,
                                                            uint32_t seed, uint32_t ntiles,
                                                            uint32_t pbase, uint32_t sel_d,
-                                                           uint32_t *__restrict__ sel_cnt) {
+                                                           uint32_t *__restrict__ sel_cnt,
+                                                           uint32_t hole_at, uint32_t hole_len) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sm[];
     __shared__ uint32_t wtot[SEL ? NT / 64 : 1];
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
@@ -587,19 +596,21 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
     const uint32_t jbot = STRIDED ? wlog : 0u;  // the tile's lowest step
     uint64_t pf[E];
     {
-        const uint32_t sb = tile_base(tile, tlog, wlog, dtile);
+        const uint32_t sb = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
 #pragma unroll
         for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
     }
     for (;;) {
-        const uint32_t base = tile_base(tile, tlog, wlog, dtile);
+        const uint32_t ptile = past_hole(tile, hole_at, hole_len);
+        const uint32_t base = tile_base(ptile, tlog, wlog, dtile);
         group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
 #pragma unroll
         for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         {
-            const uint32_t sb = tile_base(next < ntiles ? next : tile, tlog, wlog, dtile);
+            const uint32_t sb = tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog,
+                                          wlog, dtile);
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
         }
@@ -648,7 +659,7 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                     ++o;
                 }
             }
-            if (t == NT - 1) sel_cnt[tile] = tot;
+            if (t == NT - 1) sel_cnt[ptile] = tot;
             if (next >= ntiles) break;
             __syncthreads();  // wtot and the last round's LDS reads retire
             tile = next;
@@ -995,11 +1006,12 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
 template <int MODE, int R, bool SW = false>
 __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ data, uint32_t ilog,
                                                       uint32_t jtop, uint32_t seed,
-                                                      uint32_t ngroups, uint32_t pbase) {
+                                                      uint32_t ngroups, uint32_t pbase,
+                                                      uint32_t hole_at, uint32_t hole_len) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     if (t >= ngroups) return;
     const uint32_t dlog = jtop - R + 1;
-    const uint32_t b = spread(t, dlog, R);
+    const uint32_t b = spread(past_hole(t, hole_at, hole_len), dlog, R);
     const uint32_t voff = (SW ? phys(b) : b) * 8u;
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t v[1 << R];
@@ -1024,18 +1036,21 @@ __global__ __launch_bounds__(256) void bitonic_global(uint64_t *__restrict__ dat
 template <int MODE>
 static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, uint32_t jtop,
                                 int R, uint32_t seed, hipStream_t s, uint32_t pbase,
-                                uint32_t live_groups = 0, bool sw = false) {
+                                uint32_t live_groups = 0, bool sw = false, uint32_t hole_at = 0,
+                                uint32_t hole_len = 0) {
     uint32_t ngroups = 1u << (mlog - R);
     if (live_groups && live_groups < ngroups) ngroups = live_groups;
+    if (hole_len >= ngroups || hole_at >= ngroups) hole_at = hole_len = 0;
+    ngroups -= hole_len;
     if (ngroups == 0) return hipSuccess;
     const unsigned blocks = (ngroups + 255) / 256;
     net_account((uint64_t)16 * ngroups << R, "bitonic_global", s);
 #define BG_GO(R_)                                                                                  \
     do {                                                                                           \
         if (sw) hipLaunchKernelGGL((bitonic_global<MODE, R_, true>), dim3(blocks), dim3(256), 0, s, \
-                                   data, ilog, jtop, seed, ngroups, pbase);                        \
+                                   data, ilog, jtop, seed, ngroups, pbase, hole_at, hole_len);     \
         else hipLaunchKernelGGL((bitonic_global<MODE, R_>), dim3(blocks), dim3(256), 0, s, data,    \
-                                ilog, jtop, seed, ngroups, pbase);                                 \
+                                ilog, jtop, seed, ngroups, pbase, hole_at, hole_len);              \
     } while (0)
     switch (R) {
     case 1: BG_GO(1); break;
@@ -1081,7 +1096,8 @@ constexpr int kSortLatePf = MODE == 2 ? FLTEE_SORT_LATEPF_SHUFFLE : FLTEE_SORT_L
 template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF, bool SW>
 static hipError_t launch_tiles_sw(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                   uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
-                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0) {
+                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0,
+                                  uint32_t hole_at, uint32_t hole_len) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>,
@@ -1090,7 +1106,7 @@ static hipError_t launch_tiles_sw(unsigned grid, size_t lds, hipStream_t s, uint
     }
     net_account((uint64_t)16 * tiles << tlog, "bitonic_tiles", s);
     hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>), dim3(grid), dim3(NT), lds, s,
-                       data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0);
+                       data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0, hole_at, hole_len);
     return hipGetLastError();
 }
 
@@ -1099,23 +1115,25 @@ template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF>
 static hipError_t launch_tiles_lpf(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                    uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                    uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0,
-                                   bool sw) {
+                                   bool sw, uint32_t hole_at, uint32_t hole_len) {
     if constexpr (!SORT && NT == 1024 && E == 16) {
         if (sw)
             return launch_tiles_sw<MODE, SORT, E, NT, TL, WL, LPF, true>(grid, lds, s, data, tlog, ilog,
-                                                                         wlog, dtile, seed, tiles, pbase, seg0);
+                                                                         wlog, dtile, seed, tiles, pbase, seg0,
+                                                                         hole_at, hole_len);
     } else {
         if (sw) return hipErrorInvalidValue;
     }
     return launch_tiles_sw<MODE, SORT, E, NT, TL, WL, LPF, false>(grid, lds, s, data, tlog, ilog, wlog,
-                                                                  dtile, seed, tiles, pbase, seg0);
+                                                                  dtile, seed, tiles, pbase, seg0, hole_at,
+                                                                  hole_len);
 }
 
 template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0>
 static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0 = 0,
-                                 bool sw = false) {
+                                 bool sw = false, uint32_t hole_at = 0, uint32_t hole_len = 0) {
     // the compile-time strided tiles' prefetch goes after their fused tail, except for the
     // tiles with a tail on rows of 2^5 (their 9 row steps cover the load less well: 514 ->
     // 553 us at C5 with it late, while every other shape gains,
@@ -1123,10 +1141,11 @@ static hipError_t launch_tiles_e(unsigned grid, size_t lds, hipStream_t s, uint6
     if constexpr (TL != 0 && WL == 5 && !SORT) {
         if (seg0 != 0)
             return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, false>(grid, lds, s, data, tlog, ilog, wlog,
-                                                                      dtile, seed, tiles, pbase, seg0, sw);
+                                                                      dtile, seed, tiles, pbase, seg0, sw,
+                                                                      hole_at, hole_len);
     }
     return launch_tiles_lpf<MODE, SORT, E, NT, TL, WL, true>(grid, lds, s, data, tlog, ilog, wlog, dtile,
-                                                             seed, tiles, pbase, seg0, sw);
+                                                             seed, tiles, pbase, seg0, sw, hole_at, hole_len);
 }
 
 // The block-swizzled layout (kSwzMask) of a pass's input and output
@@ -1136,8 +1155,9 @@ struct Swz {
 
 struct TileCfg {
     uint32_t tlog, E, NT;
-    unsigned tiles, grid;
+    unsigned tiles, grid;  // tiles: the live tiles a launch runs (the hole excluded)
     size_t lds;
+    unsigned hole_at = 0, hole_len = 0;  // pad-only tiles skipped inside the range (pad_map)
 };
 // the selection sink of the last pass (see bitonic_merge_direct SEL)
 struct SelSink {
@@ -1168,7 +1188,7 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
         }                                                                                          \
         hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_, SWI_, SWO_>), \
                            dim3(c.grid), dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, \
-                           c.tiles, pbase, sink.d, sink.cnt);                                      \
+                           c.tiles, pbase, sink.d, sink.cnt, c.hole_at, c.hole_len);               \
     } while (0)
 #define BD_GO1(RL_, SEL_, TL_) BD_GO2(RL_, SEL_, TL_, false, false)
 #define BD_GO(RL_, TL_)                                                                            \
@@ -1303,7 +1323,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
         (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512))) {
 #define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
-    case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in);
+    case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in, c.hole_at, c.hole_len);
         if (c.NT == 1024) {
             switch (wlog) {
                 BT_ST_CASE(16, 1024, 14, 4) BT_ST_CASE(16, 1024, 14, 5) BT_ST_CASE(16, 1024, 14, 6)
@@ -1326,14 +1346,15 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
 #undef BT_ST_CASE
     }
 #define BT_GO(E_, NT_) \
-    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in)
+    return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in, c.hole_at, c.hole_len)
     if (c.NT == 1024) BT_GO(16, 1024);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
     if (c.NT == 64) BT_GO(2, 64);
     if (!SORT && plain && wlog == c.tlog && c.E == 8 && c.tlog == 12)  // contiguous 2^12 merge
         return launch_tiles_e<MODE, SORT, 8, 512, 12>(c.grid, c.lds, s, data, c.tlog, ilog, wlog,
-                                                      dtile, seed, c.tiles, pbase);
+                                                      dtile, seed, c.tiles, pbase, 0u, false, c.hole_at,
+                                                      c.hole_len);
     switch (c.E) {
     case 2: BT_GO(2, 512);
     case 4: BT_GO(4, 512);
@@ -1397,9 +1418,89 @@ static TileCfg live_tiles(const TileCfg &c, uint32_t skip) {
     if (l.grid > l.tiles) l.grid = l.tiles;
     return l;
 }
-static bool g_pad_skip = true;  // fltee_debug_set_pad_skip (A/B)
-void set_pad_skip(int on) { g_pad_skip = on != 0; }
-bool pad_skip_enabled() { return g_pad_skip; }
+// fltee_debug_set_pad_skip (A/B): 0 off, 1 pad-only stage blocks, 2 (default) also the pad-only
+// units inside a stage's mixed block on the planned schedule (pad_map)
+static int g_pad_skip = 2;
+void set_pad_skip(int on) { g_pad_skip = on < 0 ? 0 : (on > 2 ? 2 : on); }
+bool pad_skip_enabled() { return g_pad_skip != 0; }
+
+// Pads inside a stage's mixed block.  Sorting by key (MODE 0 / 1), the pads are the largest
+// keys, so a compare-exchange of a pad with a record always leaves the pad on the side its
+// direction sends the larger key to, and one of two pads with another pad: the set of
+// positions holding pads after every step depends on `valid` alone (public), not on the
+// data.  At stage ilog one aligned 2^ilog block holds `valid` (the mixed block: below it no
+// pads, above it pads alone).  Its two halves come sorted in opposite directions, so the
+// block is bitonic and each step's half-cleaner sends min(p, half) of its p pads to the
+// half its direction fills with the larger keys (the 0-1 principle): one half is then
+// clean (pads alone, or none) and the other holds the rest.  Pads alone fill
+//   ascending block:  [end, M)                  (a suffix, growing down from the top)
+//   descending block: [hlo, hhi) and [end, M)   (growing up from the block's start)
+// at the start of step 2^jstep (steps ilog-1 .. jstep+1 done).  A unit of a launch (tile or
+// register group) whose positions all lie there holds pads alone and its compare-exchanges
+// pair pads with pads: skipping it leaves the array as it is.  (A record whose key equals
+// the pads' — idx u32::MAX — shares their key: the positions holding that key still follow
+// the same map (monotone in the set: a superset of it), only records of that key may end
+// in another order among themselves; none of them has idx < d, so no output changes.)
+// The keyed shuffle (MODE 2) moves pads by a secret permutation: stage blocks only.
+struct PadMap {
+    uint64_t end, hlo, hhi;
+};
+static PadMap pad_map(uint64_t valid, uint32_t mlog, uint32_t ilog, uint32_t jstep, uint32_t pbase,
+                      bool fine) {
+    const uint64_t M = (uint64_t)1 << mlog;
+    PadMap r{M, 0, 0};
+    if (valid == 0 || valid >= M || ilog > mlog) return r;
+    const uint64_t B = (uint64_t)1 << ilog;
+    const uint64_t a = valid & ~(B - 1), bend = a + B;  // the block holding position `valid`
+    if (a == valid) { r.end = valid; return r; }        // aligned: whole pad blocks from valid on
+    r.end = bend;
+    if (!fine) return r;
+    const bool asc = ((((uint64_t)pbase + a) >> ilog) & 1u) == 0;
+    uint64_t lo = a, size = B, p = bend - valid, padlo = bend, padhi = a;
+    for (int k = (int)ilog - 1; k > (int)jstep && p != 0 && p != size; --k) {
+        const uint64_t half = (uint64_t)1 << k;
+        if (p >= half) {  // the half taking the larger keys is pads alone
+            if (asc) padlo = lo + half;
+            else { padhi = lo + half; lo += half; }
+            p -= half;
+        } else if (asc) {
+            lo += half;  // the lower half has none left: the upper one holds all p
+        }
+        size = half;
+    }
+    if (p == size) {  // the rest of the block is pads too
+        if (asc) padlo = lo;
+        else padhi = lo + size;
+    }
+    if (asc) r.end = padlo;
+    else { r.hlo = a; r.hhi = padhi; }
+    return r;
+}
+
+// The live units of a launch whose units (2^uplog per aligned superblock of 2^sblog
+// positions, numbered in position order) start at step 2^jstep of stage ilog: every unit
+// before `live` runs except the hole_len units from hole_at on.
+struct PadUnits {
+    uint32_t live, hole_at, hole_len;
+};
+template <int MODE>
+static PadUnits pad_units(uint32_t valid, uint32_t mlog, uint32_t pbase, uint32_t ilog, uint32_t jstep,
+                          uint32_t sblog, uint32_t uplog) {
+    const uint64_t nunits = ((uint64_t)1 << (mlog - sblog)) << uplog;
+    PadUnits u{(uint32_t)nunits, 0u, 0u};
+    if (!g_pad_skip || valid == 0) return u;
+    const PadMap pm = pad_map(valid, mlog, ilog, jstep, pbase, MODE != 2 && g_pad_skip >= 2);
+    const uint64_t sb = (uint64_t)1 << sblog;
+    auto up = [&](uint64_t x) { return ((x + sb - 1) >> sblog) << uplog; };
+    auto dn = [&](uint64_t x) { return (x >> sblog) << uplog; };
+    const uint64_t live = up(pm.end);
+    u.live = (uint32_t)(live < nunits ? live : nunits);
+    if (pm.hhi > pm.hlo) {
+        const uint64_t h0 = up(pm.hlo), h1 = dn(pm.hhi);
+        if (h1 > h0 && h1 <= u.live) { u.hole_at = (uint32_t)h0; u.hole_len = (uint32_t)(h1 - h0); }
+    }
+    return u;
+}
 
 // Steps jtop..0 of stage ilog (ilog > c.tlog) over the m = 2^mlog records at global
 // positions pbase..pbase+m-1: the steps with j >= T in register passes (up to 6 steps)
@@ -1566,6 +1667,17 @@ static const std::vector<NetPass> &cached_plan(uint32_t mlog, uint32_t tlog, uin
     return it->second;
 }
 
+// test hook (fltee_debug_pad_units): pad_units of a sort by key (mode 0/1) or the keyed
+// shuffle (mode 2) at the current pad-skip level: {live, hole_at, hole_len}
+void debug_pad_units(uint32_t mode, uint32_t valid, uint32_t mlog, uint32_t pbase, uint32_t ilog,
+                     uint32_t jstep, uint32_t sblog, uint32_t uplog, uint32_t out[3]) {
+    const PadUnits u = mode == 2 ? pad_units<2>(valid, mlog, pbase, ilog, jstep, sblog, uplog)
+                                 : pad_units<0>(valid, mlog, pbase, ilog, jstep, sblog, uplog);
+    out[0] = u.live;
+    out[1] = u.hole_at;
+    out[2] = u.hole_len;
+}
+
 // test hook: the plan as rows of 8 words {reg, ilog, jtop, R, ilogA, aTop, ilogB, wlog|dtile<<8}
 size_t debug_plan(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax, uint32_t *out, size_t cap) {
     const std::vector<NetPass> &plan = cached_plan(mlog, tlog, NT, rmax);
@@ -1614,13 +1726,26 @@ static bool run_plan(uint64_t *data, uint32_t mlog, const TileCfg &c0, uint32_t 
         const NetPass &p = plan[k];
         const bool last = k + 1 == plan.size();
         const Swz io{sw, sw && !last};
-        const uint32_t skip = g_pad_skip ? skip_from(valid, p.stage, mlog) : 0u;
-        if (p.reg) {
+        if (p.reg) {  // groups of 2^R: 2^(jtop+1-R) per superblock of 2^(jtop+1)
             if (io.in != io.out) { e = hipErrorInvalidValue; break; }
-            e = launch_global<MODE>(data, mlog, p.ilog, p.jtop, (int)p.R, seed, s, pbase, skip >> p.R, sw);
+            const PadUnits u = pad_units<MODE>(valid, mlog, pbase, p.ilog, p.jtop, p.jtop + 1, p.jtop + 1 - p.R);
+            if (u.live == u.hole_len) continue;  // pads alone
+            e = launch_global<MODE>(data, mlog, p.ilog, p.jtop, (int)p.R, seed, s, pbase, u.live, sw,
+                                    u.hole_at, u.hole_len);
             continue;
         }
-        const TileCfg c = live_tiles(c0, skip);
+        // tiles: contiguous ones one per 2^tlog; strided ones 2^(dtile-wlog) per superblock of
+        // 2^(dtile+rows); the launch starts with segment A's top step (else segment B's)
+        const uint32_t rows = c0.tlog - p.wlog;
+        const bool contig = p.wlog == c0.tlog;
+        const PadUnits u = pad_units<MODE>(valid, mlog, pbase, p.ilogA ? p.ilogA : p.ilogB,
+                                           p.ilogA ? p.aTop : p.dtile + rows - 1,
+                                           contig ? c0.tlog : p.dtile + rows, contig ? 0u : p.dtile - p.wlog);
+        TileCfg c = c0;
+        c.tiles = u.live - u.hole_len;
+        c.hole_at = u.hole_at;
+        c.hole_len = u.hole_len;
+        if (c.grid > c.tiles) c.grid = c.tiles;
         if (p.ilogA && !p.ilogB && p.aTop == c0.tlog - 1)  // a whole contiguous merge
             e = launch_tiles<MODE, false>(c, s, data, p.ilogA, c0.tlog, c0.tlog, seed, pbase,
                                           last ? sink : SelSink{}, 0u, io);

@@ -20,4 +20,4 @@ for name, steps in (("c3", 200), ("c4", 10), ("c5", 10)):
         r = bench.bench_workload(torch, D, name, steps=steps, warmup=3, device=torch.device("cuda", 0))
         print(json.dumps(dict(workload=name, pad_skip=on, kernel_ms=r["kernel_s"] * 1e3,
                               passes=r["net"]["passes"], net_bytes=r["net"]["bytes"])), flush=True)
-L.lib().fltee_debug_set_pad_skip(1)
+L.lib().fltee_debug_set_pad_skip(2)

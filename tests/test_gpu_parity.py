@@ -508,9 +508,10 @@ def test_nips19_c4_full_size_bit_exact(dev, oracle):
                                        (2, 12, 3000, 300), (2, 10, 16000, 1000), (4, 40, 1 << 22, 3000),
                                        (1, 1000, 10_000_000, 100_000)])
 def test_pad_skip_bit_identical(dev, oracle, alg, n, d, k):
-    """The networks skip the stage blocks made of pads alone (k_bitonic.hip stage_steps):
-    the same bits as running them, at pad fractions from ~0 to ~50 % (advanced C3/C5
-    shapes, nips19, non_oblivious's composite sort)."""
+    """The networks skip the stage blocks made of pads alone (level 1, k_bitonic.hip
+    stage_steps) and, sorting by key, the pad-only units inside a stage's mixed block
+    (level 2, pad_map): the same bits as running them all (level 0), at pad fractions from
+    ~0 to ~50 % (advanced C3/C5 shapes, nips19, non_oblivious's composite sort)."""
     from fltee import _lib as L
     rng = np.random.default_rng(n * 7 + d)
     if n * k > 10_000_000:
@@ -520,14 +521,14 @@ def test_pad_skip_bit_identical(dev, oracle, alg, n, d, k):
         idx, val = rand_sparse(rng, n, d, k)
     rec = cuda_records(dev, idx, val)
     outs = []
-    for on in (1, 0):
+    for on in (2, 1, 0):
         L.lib().fltee_debug_set_pad_skip(on)
         try:
             outs.append(dev.aggregate(alg, rec, n, k, d, seed=77).cpu().numpy())
         finally:
-            L.lib().fltee_debug_set_pad_skip(1)
+            L.lib().fltee_debug_set_pad_skip(2)
         assert dev.status() == 0
-    assert bits_equal(outs[0], outs[1])
+    assert bits_equal(outs[0], outs[1]) and bits_equal(outs[0], outs[2])
     if n * k <= 2_000_000 and alg != 2:
         ref, st = (oracle.advanced(k, oracle.as_weights(idx, val), d, n) if alg == 1
                    else oracle.non_oblivious(oracle.as_weights(idx, val), d, n))
