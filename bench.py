@@ -976,7 +976,7 @@ def main():
                 roofline=dict(bound="hbm", achieved=lit["bytes"] / lit["kernel_s"] / 1e9,
                               peak=HBM_PEAK_GBS, unit="GB/s",
                               frac=lit["bytes"] / lit["kernel_s"] / 1e9 / HBM_PEAK_GBS,
-                              algorithmic_bytes=lit["bytes"], kernel="dense_accumulate_lds",
+                              algorithmic_bytes=lit["bytes"], kernel="dense_accumulate_w",
                               note="cold: inputs rotated over > 1.5 x 256 MiB; 40.7 MB per launch "
                                    "is short enough that launch latency is a visible share"))
             if not args.no_cpu_baseline and not args.no_cpu_configs:

@@ -53,6 +53,67 @@ static __device__ __forceinline__ uint4 ld4(const uint4 *p, bool nt) {
     return nt ? ld_nt(p) : *p;
 }
 
+// Small d (MLP-MNIST: d/2 = 25,445 output pairs = 398 waves, under one wave per SIMD):
+// one lane per output pair with a whole batch of U clients' 16-B loads in flight at once —
+// the wave may take the whole register file (one wave per SIMD: up to 512 VGPRs + AGPRs),
+// so one HBM latency covers the batch instead of one per 16 clients.  Full batches, then
+// one clamped batch for the rest (clients past n re-read the last row; their adds are
+// selected away, branch-free: a branch per client kept 100 conditions live in spilled
+// SGPRs; REM = false when U divides n).  The same adds in the same order as
+// dense_accumulate_v: bit-identical.  A/B (MI355X, 50,890 params, cold inputs,
+// `profiles/r03/ab/ab17_dense_small_d.jsonl`): n = 100 9.2-9.5 us against 10.4-10.6 us for
+// the LDS-staged kernel below; n = 64 8.8 vs 9.1; n <= 32 and n > 100 no faster (those keep
+// the LDS kernel).
+template <int U, bool CLIP, bool ACC>
+__device__ __forceinline__ void dw_batch(const uint4 *__restrict__ p, size_t d2, uint32_t n, uint32_t c,
+                                         bool clamp, uint32_t jx, const float *__restrict__ ccoef,
+                                         float &a0, float &a1, uint32_t &bad) {
+    uint4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t cc = (clamp && c + (uint32_t)u >= n) ? n - 1 : c + (uint32_t)u;
+        x[u] = ld_nt(p + (size_t)cc * d2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool take = !clamp || c + (uint32_t)u < n;
+        float a = __uint_as_float(x[u].y), b = __uint_as_float(x[u].w);
+        if (CLIP) {
+            const float cf = ccoef[take ? c + u : n - 1];
+            a = __fmul_rn(a, cf);
+            b = __fmul_rn(b, cf);
+        }
+        const float s0 = __fadd_rn(a0, a), s1 = __fadd_rn(a1, b);
+        a0 = take ? s0 : a0;
+        a1 = take ? s1 : a1;
+        bad |= take ? (x[u].x ^ jx) | (x[u].z ^ (jx + 1)) : 0u;
+    }
+}
+
+template <int U, bool REM, bool CLIP, bool ACC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void dense_accumulate_w(
+    const uint4 *__restrict__ rec, size_t d2, uint32_t n, float coef, float *__restrict__ out,
+    const float *__restrict__ ccoef, uint32_t *status) {
+    const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (j >= d2) return;
+    const uint4 *p = rec + j;
+    const uint32_t jx = (uint32_t)(2 * j);
+    float a0 = 0.0f, a1 = 0.0f;
+    uint32_t bad = 0, c = 0;
+    for (; c + U <= n; c += U) dw_batch<U, CLIP, ACC>(p, d2, n, c, false, jx, ccoef, a0, a1, bad);
+    if (REM && c < n) dw_batch<U, CLIP, ACC>(p, d2, n, c, true, jx, ccoef, a0, a1, bad);
+    float2 *o = reinterpret_cast<float2 *>(out) + j;
+    float2 r;
+    if (ACC) {
+        const float2 prev = *o;
+        r = make_float2(__fadd_rn(prev.x, a0), __fadd_rn(prev.y, a1));
+    } else {
+        r = make_float2(__fmul_rn(a0, coef), __fmul_rn(a1, coef));
+    }
+    *o = r;
+    if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
 template <int V, int U, bool CLIP, bool ACC, bool NT, int NTH = 256>
 __global__ __launch_bounds__(NTH) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
                                                           uint32_t n, float coef,
@@ -391,6 +452,13 @@ static void launch_lds(bool vec, const void *rec, size_t n, size_t d, float coef
                            s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
 }
 
+template <int U, bool REM, bool ACC>
+static void dw_launch(unsigned blocks, const void *rec, size_t n, size_t d, float coef, float *out,
+                      uint32_t *status, hipStream_t s) {
+    hipLaunchKernelGGL((dense_accumulate_w<U, REM, false, ACC>), dim3(blocks), dim3(64), 0, s,
+                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status);
+}
+
 template <bool CLIP, bool ACC>
 static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef, float *out,
                                  const float *ccoef, uint32_t *status, hipStream_t s) {
@@ -403,6 +471,21 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         case 21: launch_lds<CLIP, ACC, 128, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
         case 22: launch_lds<CLIP, ACC, 256, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
         case 23: launch_lds<CLIP, ACC, 64, 16>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        // 40-43: dense_accumulate_w, batches of 100 / 32 / 64 / 50 clients
+        case 40: case 41: case 42: case 43:
+            if (vec) {
+                const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
+#define DW_GO(U_) hipLaunchKernelGGL((dense_accumulate_w<U_, true, CLIP, ACC>), dim3(blocks), dim3(64), 0, s, \
+                                     (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, ccoef, status)
+                if (g_dense_variant == 40) DW_GO(100);
+                else if (g_dense_variant == 41) DW_GO(32);
+                else if (g_dense_variant == 42) DW_GO(64);
+                else DW_GO(50);
+#undef DW_GO
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
         case 24:
             if (vec && d >= 2) {
                 hipLaunchKernelGGL((dense_accumulate_glds<CLIP, ACC>), dim3((unsigned)((d + 63) / 64)),
@@ -412,7 +495,17 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
             }
             launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
             break;
-        default: launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s); break;
+        default:
+            if (vec && !CLIP && n > 32 && n <= 100) {  // dense_accumulate_w, one batch in flight
+                const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
+                if (n == 100) dw_launch<100, false, ACC>(blocks, rec, n, d, coef, out, status, s);
+                else if (n > 64) dw_launch<100, true, ACC>(blocks, rec, n, d, coef, out, status, s);
+                else if (n == 64) dw_launch<64, false, ACC>(blocks, rec, n, d, coef, out, status, s);
+                else dw_launch<64, true, ACC>(blocks, rec, n, d, coef, out, status, s);
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
         }
         return hipGetLastError();
     }

@@ -18,7 +18,10 @@ VARIANTS = {0: "V1 U16 nt 512 lanes (shipped)", 1: "V1 U8 nt", 2: "V1 U32 nt", 3
             13: "V1 U16 nt 256 lanes (round-1 default)",
             20: "small d: LDS 64 outputs x 32 clients", 21: "small d: LDS 128 x 16",
             22: "small d: LDS 256 x 16", 23: "small d: LDS 64 x 16",
-            24: "small d: LDS-DMA ring, 64 outputs x 4 chunks of 16 clients"}
+            24: "small d: LDS-DMA ring, 64 outputs x 4 chunks of 16 clients",
+            40: "small d: lane per output pair, 100 clients in flight, whole register file",
+            41: "small d: the same, 32 in flight", 42: "small d: the same, 64 in flight",
+            43: "small d: the same, 50 in flight"}
 
 
 def main():

@@ -46,7 +46,8 @@ def bits_equal(a, b):
 
 # ------------------------------------------------------- flat algorithms ----
 @pytest.mark.parametrize("n,d", [(1, 2), (3, 7), (5, 1000), (30, 50890), (2, 65537), (17, 4099),
-                                 (100, 50890), (70, 50891), (33, 300000)])
+                                 (100, 50890), (70, 50891), (33, 300000), (64, 50890), (99, 1000),
+                                 (40, 2002)])
 @pytest.mark.parametrize("alg", [3, 4, 5])
 def test_dense_bit_exact(dev, oracle, n, d, alg):
     rng = np.random.default_rng(n * 1000 + d)
@@ -63,10 +64,11 @@ def test_dense_bit_exact(dev, oracle, n, d, alg):
                                  (1000, 256), (30, 50890)])
 @pytest.mark.parametrize("clip,acc", [(True, False), (False, True), (True, True)])
 def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
-    """The LDS-staged small-d kernels (register-staged chunks, variant 0's default; the
-    LDS-DMA ring, variant 24) == the one-lane-per-pair streaming kernel (variant 13), bit
-    for bit, with the per-client clip and accumulate fused; partial and whole chunks of
-    16 / 32 clients, a partial last block of outputs."""
+    """The small-d kernels (variant 0's default: the whole-batch kernel for 32 < n <= 100,
+    else register-staged LDS chunks; the LDS-DMA ring, variant 24; the whole-batch kernel
+    with clamped batches of 100 / 32, variants 40 / 41) == the one-lane-per-pair streaming
+    kernel (variant 13), bit for bit, with the per-client clip and accumulate fused;
+    partial and whole chunks of 16 / 32 clients, a partial last block of outputs."""
     import torch
 
     from fltee import _lib as L
@@ -77,7 +79,7 @@ def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
     prev = torch.from_numpy(rng.normal(0, 1, d).astype(np.float32)).cuda()
     outs = []
     try:
-        for variant in (0, 13, 24):
+        for variant in (0, 13, 24, 40, 41):
             L.lib().fltee_debug_set_dense_variant(variant)
             out = prev.clone()
             dev.aggregate(3, rec, n, d, d, out=out, dense=True, clip=clip, clipping=0.5,
@@ -86,13 +88,13 @@ def test_dense_small_d_kernel_equals_streaming_kernel(dev, n, d, clip, acc):
             outs.append(out.cpu().numpy())
     finally:
         L.lib().fltee_debug_set_dense_variant(0)
-    assert bits_equal(outs[0], outs[1]) and bits_equal(outs[0], outs[2])
+    assert all(bits_equal(outs[0], o) for o in outs[1:])
 
 
-def test_dense_order_violation_is_reported(dev):
-    n, d = 2, 64
+@pytest.mark.parametrize("n,d", [(2, 64), (50, 2000), (100, 50890)])
+def test_dense_order_violation_is_reported(dev, n, d):
     idx = np.tile(np.arange(d, dtype=np.uint32), n)
-    idx[70] = 3
+    idx[d + 6] = 3
     rec = cuda_records(dev, idx, np.ones(n * d, np.float32))
     dev.aggregate(3, rec, n, d, d, dense=True)
     assert dev.status() & 0x1
