@@ -290,8 +290,20 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 // kernel, and the caller reruns with a wider halo.  The folded array (1 GB at C5) is
 // never written and read back.  Dummies and non-representatives are never selected by
 // the compaction, so their contents do not matter.
+// Resident blocks per CU of the fused first pass, and whether a block prefetches its next
+// window during the fold.  Round 3 (A/B in one process, `profiles/r03/ab/ab18_fold_blocks_*`):
+// three blocks (6 waves per SIMD, <= 85 VGPRs) without the prefetch — the other resident
+// blocks hide the window load, and the prefetch registers no longer spill — run C5's pass
+// in 1,065-1,077 us against 1,198-1,206 us for two prefetching blocks (three prefetching:
+// 1,153-1,157, spilling; four without: 1,149-1,150); C3 unchanged.
+#ifndef FLTEE_FC_BLOCKS
+#define FLTEE_FC_BLOCKS 3
+#endif
+#ifndef FLTEE_FC_PF
+#define FLTEE_FC_PF 0
+#endif
 template <int NT, int PER, int FINAL, int XMAX>
-__global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__restrict__ A,
+__global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
                                                             uint32_t M, uint32_t d, uint32_t G,
                                                             uint32_t S, uint32_t Hr,
@@ -330,8 +342,9 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
     };
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
-    prefetch(tile);
+    if (FLTEE_FC_PF) prefetch(tile);
     for (;;) {
+        if (!FLTEE_FC_PF) prefetch(tile);
         const long long a = (long long)tile * S, wlo = a - (long long)Hr;
 #pragma unroll
         for (uint32_t i = 0; i < PER + XMAX; ++i)
@@ -340,7 +353,7 @@ __global__ __launch_bounds__(NT, 1) void fold_compact_first(const uint64_t *__re
             atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
         // Each lane owns window slots [x0, x1) and folds the runs whose heads lie there,
         // left to right: one loop that goes past x1 only to finish its last run, so a
         // wave's trip count is about chunk + the longest run (a loop per head nested in
@@ -518,7 +531,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const uint32_t CAP = NT * per, S = CAP - H;
     const uint64_t ntiles = (L + S - 1) / S;
     const bool last = G == nlev;
-    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);
+    const unsigned grid = (unsigned)(ntiles < 256u * FLTEE_FC_BLOCKS ? ntiles : 256u * FLTEE_FC_BLOCKS);
     const size_t lds = (Hr + CAP + 1) * 8;
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
     const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr <= 512)
