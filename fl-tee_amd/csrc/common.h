@@ -195,6 +195,12 @@ hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_
                                      size_t tf, size_t pbase, size_t m, uint64_t *dst,
                                      hipStream_t s);
 
+// k_radix.hip: the stable sort by idx of an ordered fold's n entries (8-B records) ->
+// keys[0, n) = (idx << 32 | position), the stable composite order
+size_t radix_scratch_bytes(size_t n, size_t d);
+hipError_t launch_radix_by_idx(const void *rec, size_t n, size_t d, void *scratch, size_t bytes,
+                               uint64_t *keys, uint32_t *status, hipStream_t s);
+
 // k_dp.hip
 hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,
                            uint64_t seed, hipStream_t s);

@@ -27,6 +27,7 @@ struct DeviceCtx {
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel, ws_keys, ws_start;            // ordered folds (nips19, non_oblivious)
+    Buffer ws_radix;                                     // their stable radix sort by idx
     uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)

@@ -186,17 +186,37 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
            c->ws_start.reserve(p.start_bytes);
 }
 
+// The stable order by (idx, position) of an ordered fold's entries: a stable radix sort by
+// idx (k_radix.hip: the sequence of indices in list order is what the enclave's own
+// g[idx] += val loop touches) — or, fltee_debug_set_radix_order(0), the composite-key
+// bitonic sort (the same order, bit for bit: test_gpu_parity.py).
+static bool g_radix_order = true;
+void set_radix_order(int on) { g_radix_order = on != 0; }
+
+static hipError_t stable_by_idx(DeviceCtx *c, const void *rec, size_t n, size_t d, uint64_t *&keys,
+                                uint32_t *status, hipStream_t s) {
+    if (g_radix_order) {
+        const size_t need = radix_scratch_bytes(n, d);
+        if (!c->ws_keys.reserve(n * 8) || !c->ws_radix.reserve(need)) return hipErrorOutOfMemory;
+        keys = (uint64_t *)c->ws_keys.ptr;
+        return launch_radix_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, keys, status, s);
+    }
+    const size_t mc = next_pow2_sz(n);
+    if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
+    keys = (uint64_t *)c->ws_keys.ptr;
+    hipError_t e = launch_composite_init(rec, n, d, mc, keys, status, s);
+    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, n);  // ~0 keys past n
+    return e;
+}
+
 // the selected list sel[0, lc) (entries with idx < d in position order) -> out: stable
-// composite sort by (idx, list position), then the ordered fold
+// order by (idx, list position), then the ordered fold
 hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d, float coef,
                              float *out, bool acc, uint32_t *status, hipStream_t s) {
     if (lc == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
     if (!c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
-    const size_t mc = next_pow2_sz(lc);
-    if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
-    uint64_t *keys = (uint64_t *)c->ws_keys.ptr;
-    hipError_t e = launch_composite_init(sel, lc, d, mc, keys, status, s);
-    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, lc);  // ~0 keys past lc
+    uint64_t *keys = nullptr;
+    hipError_t e = stable_by_idx(c, sel, lc, d, keys, status, s);
     if (e == hipSuccess)
         e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
     return e;
@@ -371,10 +391,8 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
                                    c->status + 16, coef, out, acc, status, s);
             if (e != hipSuccess) c->mat_clean = 0;  // the emptying pass may not have run
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
-            const size_t M = next_pow2_sz(n * k);
-            uint64_t *K = (uint64_t *)c->ws_a.ptr;
-            e = launch_composite_init(rec, n * k, d, M, K, status, s);
-            if (e == hipSuccess) e = bitonic_sort(K, M, 1, 0, s, n * k);
+            uint64_t *K = nullptr;
+            e = stable_by_idx(c, rec, n * k, d, K, status, s);
             if (e == hipSuccess)
                 e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
         } else {
@@ -807,6 +825,7 @@ extern "C" void fltee_debug_set_compact_variant(int v) { fltee::set_compact_vari
 extern "C" void fltee_debug_set_fold_compact(int on) { fltee::set_fold_compact(on); }
 // A/B hook: 0 runs the networks over the pad-only stage blocks too
 extern "C" void fltee_debug_set_pad_skip(int on) { fltee::set_pad_skip(on); }
+extern "C" void fltee_debug_set_radix_order(int on) { fltee::set_radix_order(on); }
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes

@@ -109,6 +109,7 @@ EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_net_log": (_S, [_S, ctypes.c_char_p, _S, _P, _P]),
     "fltee_debug_set_fold_compact": (None, [ctypes.c_int]),
     "fltee_debug_set_pad_skip": (None, [ctypes.c_int]),
+    "fltee_debug_set_radix_order": (None, [ctypes.c_int]),
     "fltee_debug_set_swizzle": (None, [ctypes.c_int]),
     "fltee_debug_sort_fused": (_U32, [_U32, _P, _S, _P, _S, _P, _S, _S,
                                        _U32, _P]),

@@ -791,3 +791,26 @@ def test_parallel_paths_single_rank(dev, oracle):
     got = dev.sum_rows(torch.stack(parts), coef).cpu().numpy()
     ref, st = oracle.client_size_optimized(4, k, oracle.as_weights(idx, val), dk, nc)
     assert st == 0 and bits_equal(got, ref)
+
+
+@pytest.mark.parametrize("alg,n,d,k", [(2, 300, 44964, 4496), (2, 12, 3000, 300), (4, 2, 2_000_000, 100),
+                                       (4, 3, 1 << 24, 50000)])
+def test_radix_order_equals_composite_sort(dev, alg, n, d, k):
+    """The ordered folds' stable order by (idx, position) from the radix sort by idx
+    (k_radix.hip, the default) == the composite-key bitonic sort, bit for bit: nips19's
+    selected list (C4 shape and a small one) and non_oblivious's sparse fallback (repeated
+    indices across clients, runs in upload order)."""
+    from fltee import _lib as L
+    rng = np.random.default_rng(n * 31 + d)
+    idx = rng.integers(0, d, n * k).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    outs = []
+    try:
+        for on in (1, 0):
+            L.lib().fltee_debug_set_radix_order(on)
+            outs.append(dev.aggregate(alg, rec, n, k, d, seed=91).cpu().numpy())
+            assert dev.status() == 0
+    finally:
+        L.lib().fltee_debug_set_radix_order(1)
+    assert bits_equal(outs[0], outs[1])
