@@ -241,11 +241,21 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         }
         const uint32_t ngroups = (uint32_t)(((uint64_t)1 << j0) >> logW);
         const uint64_t bands = (rows + S - 1) / S;
-        const uint64_t ntiles = bands * ngroups;
+        uint64_t ntiles = bands * ngroups;
         if (ntiles == 0 || ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
         const int fin = last ? (accumulate ? 2 : 1) : 0;
-        net_account((uint64_t)(last ? 8 : 16) * L, "compact_pass", s);
+        // The last pass writes out[p] for p < d only.  With one band and 2^j0 >= d, a tile's
+        // output slots lie at p = row * 2^j0 + grp * W + f: rows >= 1 are past d, so the
+        // groups with grp * W >= d write nothing — a suffix of the tiles, skipped (public
+        // sizes only).  C5's last pass: 39,063 of 65,536 tiles.
+        uint64_t live = ntiles;
+        if (last && bands == 1 && j0 > 0 && ((uint64_t)1 << j0) >= d) {
+            const uint64_t g = (d + ((uint64_t)1 << logW) - 1) >> logW;
+            if (g < live) live = g;
+        }
+        net_account((uint64_t)(last ? 8 : 16) * L * live / ntiles, "compact_pass", s);
+        ntiles = live;
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
         const int blk = j0 == 0 ? kCompactFirstBlocks : kCompactBlocks;
         const unsigned res = small ? 256u * (unsigned)blk : 256u;
