@@ -191,8 +191,16 @@ __device__ __forceinline__ uint32_t lane_tid() {
 }
 
 // One wave's LDS accesses stay in program order (the LDS executes a wave's DS
-// instructions in issue order): a compiler-only barrier suffices between wave-local rounds.
-__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_wave_barrier(); }
+// instructions in issue order), so between wave-local rounds only the compiler must be
+// kept from moving a later round's LDS reads above an earlier round's writes: the
+// __syncwarp idiom — wavefront-scope release/acquire fences around the wave barrier.  The
+// bare wave barrier touches no memory and orders nothing at the compiler level; the
+// wavefront-scope fences emit no instructions (ISA unchanged, `make asm`).
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Raw buffer access: byte offset = soffset (wave-uniform, SGPR) + voffset (per lane).
 typedef unsigned int bt_u32x2 __attribute__((ext_vector_type(2)));
@@ -431,6 +439,9 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
         }
         sort_stages_ct<MODE, E, NT, IL + 1, TL, RL>(sm, base, seed);
     } else {
+        // stage TL runs block-wide rounds: if the stage before it was wave-local and did
+        // not end in a block barrier (TL <= WB), order the waves here
+        if constexpr (WB && TL <= WB) __syncthreads();
         lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base, (uint32_t)TL, seed);
     }
 }

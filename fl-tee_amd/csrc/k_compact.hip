@@ -543,8 +543,11 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 256u * FLTEE_FC_BLOCKS ? ntiles : 256u * FLTEE_FC_BLOCKS);
     const size_t lds = (Hr + CAP + 1) * 8;
+    // FLTEE_FC_BLOCKS resident blocks per CU must fit the 160 KiB LDS at the largest window
+    static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
+    if (lds * FLTEE_FC_BLOCKS > 160 * 1024) return hipErrorNotSupported;
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
-    const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr <= 512)
+    const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr < 1024)
     const int F = !last ? 0 : (accumulate ? 2 : 1);
     hipError_t e;
     if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
