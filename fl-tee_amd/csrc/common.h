@@ -170,10 +170,6 @@ hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint
                                  uint64_t *tmp, float coef, float *out, hipStream_t s);
 hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,
                                  uint32_t *status, hipStream_t s);
-// writes every out[i], i < d (accumulate: adds where index i has records); start: d u32
-hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,
-                               float *out, size_t d, bool accumulate, uint32_t *start,
-                               hipStream_t s);
 
 // k_nips19.hip
 hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t *r,
@@ -195,11 +191,17 @@ hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_
                                      size_t tf, size_t pbase, size_t m, uint64_t *dst,
                                      hipStream_t s);
 
-// k_radix.hip: the stable sort by idx of an ordered fold's n entries (8-B records) ->
-// keys[0, n) = (idx << 32 | position), the stable composite order
+// k_radix.hip: the stable sort by idx of an ordered fold's n records (hand-written LSD
+// counting sort; scratch: radix_scratch_bytes) -> sorted[0, n), and the ordered fold over
+// sorted records: writes every out[i], i < d (accumulate: adds where index i has records)
 size_t radix_scratch_bytes(size_t n, size_t d);
-hipError_t launch_radix_by_idx(const void *rec, size_t n, size_t d, void *scratch, size_t bytes,
-                               uint64_t *keys, uint32_t *status, hipStream_t s);
+hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void *scratch,
+                                      size_t bytes, uint64_t *sorted, uint32_t *status,
+                                      hipStream_t s);
+hipError_t launch_fold_sorted(const uint64_t *sorted, size_t n, size_t d, float coef, float *out,
+                              bool accumulate, hipStream_t s);
+hipError_t launch_gather_by_keys(const uint64_t *keys, size_t n, const void *rec, uint64_t *dst,
+                                 hipStream_t s);
 
 // k_dp.hip
 hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,

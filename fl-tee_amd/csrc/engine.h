@@ -26,8 +26,8 @@ struct DeviceCtx {
     void *mat_clean_ptr = nullptr;
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
     Buffer ws_client, ws_client_coef;                   // client-side producers
-    Buffer ws_cnt, ws_sel, ws_keys, ws_start;            // ordered folds (nips19, non_oblivious)
-    Buffer ws_radix;                                     // their stable radix sort by idx
+    Buffer ws_cnt, ws_sel;                               // nips19's selected list
+    Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch
     uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)

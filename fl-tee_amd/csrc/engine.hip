@@ -136,7 +136,7 @@ static size_t f32_to_usize_sat(float x) {
 // scratch plan per algorithm
 struct Plan {
     size_t a_bytes = 0, b_bytes = 0, mat_bytes = 0, r_bytes = 0, coef_bytes = 0, rec_bytes = 0;
-    size_t start_bytes = 0;
+    size_t keys_bytes = 0, radix_bytes = 0;  // ordered fold: sorted records, sort scratch
 };
 
 static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -155,7 +155,7 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (!dense) {
             if (use_scatter_rows(n, k, d)) p.mat_bytes = n * d * 4;
-            else p.a_bytes = next_pow2_sz(n * k) * 8, p.start_bytes = d * 4;
+            else p.keys_bytes = n * k * 8, p.radix_bytes = radix_scratch_bytes(n * k, d);
         }
         break;
     case FLTEE_ALG_ADVANCED:
@@ -171,7 +171,6 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         const float T = nips19_threshold(d, kq, n);
         p.a_bytes = next_pow2_sz(n * k + d * f32_to_usize_sat(T)) * 8;
         p.r_bytes = d * 4;
-        p.start_bytes = d * 4;
         break;
     }
     default: break;
@@ -183,43 +182,45 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
     return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
            c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
            c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes) &&
-           c->ws_start.reserve(p.start_bytes);
+           c->ws_keys.reserve(p.keys_bytes) && c->ws_radix.reserve(p.radix_bytes);
 }
 
-// The stable order by (idx, position) of an ordered fold's entries: a stable radix sort by
-// idx (k_radix.hip: the sequence of indices in list order is what the enclave's own
-// g[idx] += val loop touches) — or, fltee_debug_set_radix_order(0), the composite-key
-// bitonic sort (the same order, bit for bit: test_gpu_parity.py).
+// The ordered fold of n records (common.rs:25-35, non_oblivious.rs:11-13): the records in
+// stable order by idx, then out[i] = the in-order sum of index i's.  The order comes from
+// the hand-written counting sort (k_radix.hip: the sequence of indices in list order is
+// what the enclave's own g[idx] += val loop touches) — or, fltee_debug_set_radix_order(0),
+// from the composite-key bitonic sort, the records gathered by its keys (the same order,
+// bit for bit: test_gpu_parity.py).
 static bool g_radix_order = true;
 void set_radix_order(int on) { g_radix_order = on != 0; }
 
-static hipError_t stable_by_idx(DeviceCtx *c, const void *rec, size_t n, size_t d, uint64_t *&keys,
-                                uint32_t *status, hipStream_t s) {
+static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, size_t d,
+                                       float coef, float *out, bool acc, uint32_t *status,
+                                       hipStream_t s) {
+    if (!c->ws_keys.reserve(n * 8)) return hipErrorOutOfMemory;
+    uint64_t *sorted = (uint64_t *)c->ws_keys.ptr;
+    hipError_t e;
     if (g_radix_order) {
-        const size_t need = radix_scratch_bytes(n, d);
-        if (!c->ws_keys.reserve(n * 8) || !c->ws_radix.reserve(need)) return hipErrorOutOfMemory;
-        keys = (uint64_t *)c->ws_keys.ptr;
-        return launch_radix_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, keys, status, s);
+        if (!c->ws_radix.reserve(radix_scratch_bytes(n, d))) return hipErrorOutOfMemory;
+        e = launch_sort_records_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, sorted, status, s);
+    } else {
+        const size_t mc = next_pow2_sz(n);
+        if (!c->ws_radix.reserve(mc * 8)) return hipErrorOutOfMemory;
+        uint64_t *keys = (uint64_t *)c->ws_radix.ptr;
+        e = launch_composite_init(rec, n, d, mc, keys, status, s);
+        if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, n);  // ~0 keys past n
+        if (e == hipSuccess) e = launch_gather_by_keys(keys, n, rec, sorted, s);
     }
-    const size_t mc = next_pow2_sz(n);
-    if (!c->ws_keys.reserve(mc * 8)) return hipErrorOutOfMemory;
-    keys = (uint64_t *)c->ws_keys.ptr;
-    hipError_t e = launch_composite_init(rec, n, d, mc, keys, status, s);
-    if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, n);  // ~0 keys past n
+    if (e == hipSuccess) e = launch_fold_sorted(sorted, n, d, coef, out, acc, s);
     return e;
 }
 
 // the selected list sel[0, lc) (entries with idx < d in position order) -> out: stable
-// order by (idx, list position), then the ordered fold
+// order by idx (list position within an index), then the ordered fold
 hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d, float coef,
                              float *out, bool acc, uint32_t *status, hipStream_t s) {
     if (lc == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
-    if (!c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
-    uint64_t *keys = nullptr;
-    hipError_t e = stable_by_idx(c, sel, lc, d, keys, status, s);
-    if (e == hipSuccess)
-        e = launch_ordered_fold(keys, lc, sel, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
-    return e;
+    return ordered_fold_records(c, sel, lc, d, coef, out, acc, status, s);
 }
 
 hipError_t read_device_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s) {
@@ -239,7 +240,7 @@ hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, s
     if (d == 0) return hipSuccess;
     if (m == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
     const size_t nb = select_tiles(m);
-    if (!c->ws_cnt.reserve((2 * nb + 2) * 4) || !c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
+    if (!c->ws_cnt.reserve((2 * nb + 2) * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
     hipError_t e = launch_select_count(src, m, d, cnt, base, s);
     size_t lc = 0;  // entries with idx < d (the DP-noised histogram total)
@@ -261,7 +262,7 @@ static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, 
                                            uint32_t *status, hipStream_t s) {
     const size_t ntl = bitonic_select_tiles(M);
     if (ntl == 0 || d == 0) return hipErrorNotSupported;
-    if (!c->ws_cnt.reserve((2 * ntl + 2) * 4) || !c->ws_start.reserve(d * 4)) return hipErrorOutOfMemory;
+    if (!c->ws_cnt.reserve((2 * ntl + 2) * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + ntl + 1;
     // tiles of pads alone are skipped by the last pass and keep a zero count
     hipError_t e = hipMemsetAsync(cnt, 0, ntl * 4, s);
@@ -391,10 +392,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
                                    c->status + 16, coef, out, acc, status, s);
             if (e != hipSuccess) c->mat_clean = 0;  // the emptying pass may not have run
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
-            uint64_t *K = nullptr;
-            e = stable_by_idx(c, rec, n * k, d, K, status, s);
-            if (e == hipSuccess)
-                e = launch_ordered_fold(K, n * k, rec, coef, out, d, acc, (uint32_t *)c->ws_start.ptr, s);
+            e = ordered_fold_records(c, rec, n * k, d, coef, out, acc, status, s);
         } else {
             if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
                 e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
@@ -477,7 +475,7 @@ fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t 
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
     const Plan p = plan_for(alg, n, k, d, o);
     return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes +
-           p.start_bytes;
+           p.keys_bytes + p.radix_bytes;
 }
 
 bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {

@@ -114,6 +114,65 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
 
+// The same output pairs with the clients split over W waves of one block (wave w: clients
+// [w*UC, (w+1)*UC)): every wave issues its UC rows' loads at once, so W times the waves
+// (and SIMDs) pull the batch; the in-order sum then passes from wave to wave through LDS —
+// wave w adds its clients to wave w-1's partial sums, after a block barrier — the same adds
+// in the same order as dense_accumulate_w: bit-identical.  n <= W * UC (clients past n are
+// clamped and selected away as in dw_batch).
+template <int W, int UC, bool ACC>
+__global__ __launch_bounds__(64 * W) void dense_accumulate_wk(const uint4 *__restrict__ rec,
+                                                            size_t d2, uint32_t n, float coef,
+                                                            float *__restrict__ out,
+                                                            uint32_t *status) {
+    __shared__ float2 part[W][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t j = (size_t)blockIdx.x * 64 + lane;
+    const bool live = j < d2;
+    const uint4 *p = rec + (live ? j : 0);
+    const uint32_t jx = (uint32_t)(2 * j), c0 = w * (uint32_t)UC;
+    uint4 x[UC];
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+        const uint32_t cc = c0 + (uint32_t)u < n ? c0 + (uint32_t)u : n - 1;
+        x[u] = ld_nt(p + (size_t)cc * d2);
+    }
+    float a0 = 0.0f, a1 = 0.0f;
+    uint32_t bad = 0;
+    for (uint32_t s = 0; s < (uint32_t)W; ++s) {
+        if (s) __syncthreads();
+        if (s == w) {
+            if (s) {
+                const float2 pr = part[s - 1][lane];
+                a0 = pr.x;
+                a1 = pr.y;
+            }
+#pragma unroll
+            for (int u = 0; u < UC; ++u) {
+                const bool take = c0 + (uint32_t)u < n;
+                const float s0 = __fadd_rn(a0, __uint_as_float(x[u].y));
+                const float s1 = __fadd_rn(a1, __uint_as_float(x[u].w));
+                a0 = take ? s0 : a0;
+                a1 = take ? s1 : a1;
+                bad |= take ? (x[u].x ^ jx) | (x[u].z ^ (jx + 1)) : 0u;
+            }
+            part[s][lane] = make_float2(a0, a1);
+        }
+    }
+    if (w == W - 1 && live) {
+        float2 *o = reinterpret_cast<float2 *>(out) + j;
+        float2 r;
+        if (ACC) {
+            const float2 prev = *o;
+            r = make_float2(__fadd_rn(prev.x, a0), __fadd_rn(prev.y, a1));
+        } else {
+            r = make_float2(__fmul_rn(a0, coef), __fmul_rn(a1, coef));
+        }
+        *o = r;
+    }
+    if (live && bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
 template <int V, int U, bool CLIP, bool ACC, bool NT, int NTH = 256>
 __global__ __launch_bounds__(NTH) void dense_accumulate_v(const uint4 *__restrict__ rec, size_t d2,
                                                           uint32_t n, float coef,
@@ -482,6 +541,23 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
                 else if (g_dense_variant == 42) DW_GO(64);
                 else DW_GO(50);
 #undef DW_GO
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
+        // 44-46: dense_accumulate_wk, the clients of a pair over 2 / 4 / 3 waves (n <= 100)
+        case 44: case 45: case 46:
+            if (vec && !CLIP && n <= 100) {
+                const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
+                if (g_dense_variant == 44)
+                    hipLaunchKernelGGL((dense_accumulate_wk<2, 50, ACC>), dim3(blocks), dim3(128), 0, s,
+                                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
+                else if (g_dense_variant == 45)
+                    hipLaunchKernelGGL((dense_accumulate_wk<4, 25, ACC>), dim3(blocks), dim3(256), 0, s,
+                                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
+                else
+                    hipLaunchKernelGGL((dense_accumulate_wk<3, 34, ACC>), dim3(blocks), dim3(192), 0, s,
+                                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
                 break;
             }
             launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);

@@ -53,6 +53,11 @@
 #ifndef FLTEE_KEYED_SPLIT
 #define FLTEE_KEYED_SPLIT 0
 #endif
+//   FLTEE_KEYED_DIRFOLD  the keyed comparator with the direction folded into the hashed word
+//                        (keyed_swap; off: the round-3 form, for A/B)
+#ifndef FLTEE_KEYED_DIRFOLD
+#define FLTEE_KEYED_DIRFOLD 1
+#endif
 template <int G>
 constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FLTEE_LDS_BATCH;
 //   FLTEE_LDS_READ1   LDS reads as single ds_read_b64 (no ds_read2_b64 pairing)
@@ -115,6 +120,19 @@ __device__ __forceinline__ uint32_t keyed_c(uint32_t key, uint32_t dq) {
     return (dq - 2u * (key & dq)) * 0x9E3779B1u;
 }
 
+// The keyed comparator (MODE 2) with the block's direction folded into the hashed word.
+// swap = asc ^ top bit of ((l ^ key) * K).  For S in {0, 2^31}: (y ^ S) * K = y * K + S
+// (mod 2^32; K odd), so the top bit of ((l ^ key ^ S) * K) is that of (l ^ key) * K,
+// flipped when S = 2^31.  With S = 2^31 for an ascending block (l < 2^29 never has bit 31)
+// swap = sign of ((l ^ key ^ S) * K): the same bits as cond2<2>, in a xor, a v_mul_lo and
+// one signed compare (instead of a shift and a compare with the direction), and the key,
+// the direction and the group's first position are joined once per group and step
+// (l = p0 ^ (q << dlog): p0 has zeros there).
+__device__ __forceinline__ uint32_t keyed_dir(bool asc) { return asc ? 0x80000000u : 0u; }
+__device__ __forceinline__ bool keyed_swap(uint32_t kb, uint32_t dq) {
+    return (int32_t)((kb ^ dq) * 0x9E3779B1u) < 0;
+}
+
 // Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
 // records held in v[], whose first record sits at global position p0.  The group
 // spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
@@ -124,13 +142,16 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
                                             uint32_t ilog, uint32_t seed) {
     if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
     const bool asc = (p0 & (1u << ilog)) == 0;
+    const uint32_t pdir = MODE == 2 ? p0 ^ keyed_dir(asc) : 0u;
 #pragma unroll
     for (int lv = R - 1; lv >= 0; --lv) {
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
         const uint32_t X = (MODE == 2 && FLTEE_KEYED_SPLIT) ? (p0 ^ key) * 0x9E3779B1u : 0u;
+        const uint32_t kb = pdir ^ key;
         auto decide = [&](int q, int qm) -> bool {
             if constexpr (MODE == 2 && FLTEE_KEYED_SPLIT)
                 return asc ^ ((int32_t)(X + keyed_c(key, (uint32_t)q << dlog)) < 0);
+            if constexpr (MODE == 2 && FLTEE_KEYED_DIRFOLD) return keyed_swap(kb, (uint32_t)q << dlog);
             return asc ^ cond2<MODE>(v[q], v[qm], p0 + ((uint32_t)q << dlog), key);
         };
 #if FLTEE_CE_BATCH
@@ -759,6 +780,8 @@ __device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32
             const bool asc = ((p0 + (uint32_t)(q & ~(B - 1))) & (1u << IL)) == 0;
             if constexpr (MODE == 2 && FLTEE_KEYED_SPLIT)
                 sw[k++] = asc ^ ((int32_t)(X + keyed_c(key, (uint32_t)q)) < 0);
+            else if constexpr (MODE == 2 && FLTEE_KEYED_DIRFOLD)
+                sw[k++] = keyed_swap(p0 ^ key ^ keyed_dir(asc), (uint32_t)q);
             else
                 sw[k++] = asc ^ cond2<MODE>(v[q], v[qm], p0 + (uint32_t)q, key);
         }

@@ -272,74 +272,4 @@ hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t 
     return hipGetLastError();
 }
 
-// The ordered fold over the stable-sorted composite keys: out[idx] = ((+0 + v1) + v2)
-// ... in key order (upload / shuffled order within an index), the order of
-// non_oblivious.rs:11-13 and common.rs:25-35.  One wave per output index: run_heads
-// marks where each index's run starts; the wave then reads its run 64 keys at a time
-// (coalesced), gathers the 64 values and adds them in lane order with readlane (a
-// uniform serial chain, the exact left fold).  One lane per run head walking its run
-// alone was latency-bound: 543 us for nips19's C4 list (3.4 M entries, runs up to
-// ~1500 long) against tens of us here.
-__global__ void run_heads_kernel(const uint64_t *__restrict__ keys, size_t nrec, size_t d,
-                                 uint32_t *__restrict__ start) {
-    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= nrec) return;
-    const uint32_t idx = (uint32_t)(keys[p] >> 32);
-    if (idx >= d) return;
-    if (p == 0 || (uint32_t)(keys[p - 1] >> 32) != idx) start[idx] = (uint32_t)p;
-}
-
-template <bool ACC>
-__global__ __launch_bounds__(256) void wave_fold_kernel(const uint64_t *__restrict__ keys,
-                                                        size_t nrec,
-                                                        const uint2 *__restrict__ rec,
-                                                        const uint32_t *__restrict__ start,
-                                                        float coef, float *__restrict__ out,
-                                                        size_t d) {
-    const size_t i = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63;
-    if (i >= d) return;  // uniform per wave
-    const uint32_t p0 = start[i];
-    float acc = 0.0f;
-    if (p0 != 0xFFFFFFFFu) {
-        for (size_t p = p0;; p += 64) {
-            const size_t q = p + lane;
-            bool valid = false;
-            float v = 0.0f;
-            if (q < nrec) {
-                const uint64_t kv = keys[q];
-                valid = (uint32_t)(kv >> 32) == (uint32_t)i;
-                if (valid) v = __uint_as_float(rec[(uint32_t)kv].y);
-            }
-            const int c = __popcll(__ballot(valid));  // the run is a prefix of the 64
-            const int vb = __float_as_int(v);
-            for (int j = 0; j < c; ++j)
-                acc = __fadd_rn(acc, __int_as_float(__builtin_amdgcn_readlane(vb, j)));
-            if (c < 64) break;
-        }
-    } else if (ACC) {
-        return;  // nothing to add: leave out[i] as it is (also a -0.0)
-    }
-    if (lane == 0) out[i] = ACC ? __fadd_rn(out[i], acc) : __fmul_rn(acc, coef);
-}
-
-hipError_t launch_ordered_fold(const uint64_t *keys, size_t nrec, const void *rec, float coef,
-                               float *out, size_t d, bool accumulate, uint32_t *start,
-                               hipStream_t s) {
-    if (d == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(start, 0xFF, d * 4, s);
-    if (e != hipSuccess) return e;
-    if (nrec)
-        hipLaunchKernelGGL(run_heads_kernel, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, s,
-                           keys, nrec, d, start);
-    const unsigned blocks = (unsigned)((d + 3) / 4);
-    if (accumulate)
-        hipLaunchKernelGGL(wave_fold_kernel<true>, dim3(blocks), dim3(256), 0, s, keys, nrec,
-                           (const uint2 *)rec, start, coef, out, d);
-    else
-        hipLaunchKernelGGL(wave_fold_kernel<false>, dim3(blocks), dim3(256), 0, s, keys, nrec,
-                           (const uint2 *)rec, start, coef, out, d);
-    return hipGetLastError();
-}
-
 }  // namespace fltee

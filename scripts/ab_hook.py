@@ -2,7 +2,8 @@
 workload timed by bench.bench_workload with `hook(value)` set before each trial, the
 values interleaved, plus the output's bits per value.  One JSON line per (value, repeat).
 
-    python scripts/ab_hook.py c5 fltee_debug_set_swizzle 1 0"""
+    python scripts/ab_hook.py c5 fltee_debug_set_swizzle 1 0
+(AB_COLD=1: inputs rotated over > 1.5 x the Infinity Cache, as the literal config runs)"""
 import hashlib
 import json
 import os
@@ -34,7 +35,8 @@ def main():
         for rep in range(reps):
             for v in values:
                 fn(v)
-                r = bench.bench_workload(torch, D, w, steps=steps, warmup=3, device=dev)
+                r = bench.bench_workload(torch, D, w, steps=steps, warmup=3, device=dev,
+                                         cold=os.environ.get("AB_COLD") == "1")
                 out = D.aggregate(wl["alg"], rec, wl["n"], wl["k"] or wl["d"], wl["d"], **kw).cpu().numpy()
                 h = hashlib.sha256(out.view(np.uint32).tobytes()).hexdigest()[:16]
                 print(json.dumps(dict(workload=w, hook=hook, value=v, rep=rep,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun job that regenerates the round's GPU evidence (run under gpurun from the
 # repo root):  TAG=r03 [TESTS=1] [BENCH=1] [PROFILE="ns c1 c3 c4 mnist100"] [PMC="ns"] \
-#              [SQ="c4 c5"] bash scripts/gpu_evidence.sh
+#              [SQ="c4 c5"] [AB="c4" ABV="FLTEE_LIB=..."] bash scripts/gpu_evidence.sh
 # Every GPU step has its own time limit and the steps stop at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
@@ -14,6 +14,17 @@ if [ "${TESTS:-1}" = 1 ]; then
       --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || exit 11
   tail -3 "$OUT/pytest_gpu.log"
 fi
+# A/B of library builds in one process per variant: AB="c4 c5" ABV="FLTEE_LIB=fl-tee_amd/lib/ab/x.so"
+for w in ${AB}; do
+  timeout -k 10 600 python -u scripts/ab_env.py "$w" ${ABV} > "$OUT/ab_$w.jsonl" 2> "$OUT/ab_$w.err" || exit 22
+  echo "ab $w"
+done
+# A/B of a runtime hook in one process: ABH="mnist100:fltee_debug_set_dense_variant:0 44 45"
+for spec in ${ABH:+"$ABH"}; do
+  IFS=: read -r w hook vals <<< "$spec"
+  timeout -k 10 600 python -u scripts/ab_hook.py "$w" "$hook" $vals > "$OUT/abh_${w}_${hook}.jsonl" 2> "$OUT/abh_$w.err" || exit 23
+  echo "abh $w $hook"
+done
 if [ "${BENCH:-1}" = 1 ]; then
   timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 12
   tail -c 600 "$OUT/bench.json"; echo

@@ -124,7 +124,12 @@ def test_index_sharded_matches_single_gpu_at_scale(dev):
 
 
 @pytest.mark.parametrize("m,d,hi", [(1, 10, 20), (777, 50, 80), (40000, 3000, 3100), (5000, 100, 100),
-                                    (5000, 100, 90000)])
+                                    (5000, 100, 90000),
+                                    # the counting sort's shapes (k_radix.hip): one pass of 3
+                                    # bits; one index (a run over every wave); a tile plus one;
+                                    # 17 key bits (3 passes of 6); 24 bits over mostly gaps
+                                    (100000, 5, 5), (4097, 1, 1), (2049, 3000, 3000),
+                                    (70000, 65536, 65536), (300000, 10_000_000, 10_000_000)])
 def test_select_and_ordered_list_match_numpy(dev, m, d, hi):
     """fltee_select_device (entries with idx < d, position order) and
     fltee_ordered_list_device (in-order f32 sums x coef) == numpy, bit for bit; hi = d:
