@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "fl-tee_amd"))
 
 from bench_legs import (ALG_NAMES, HBM_PEAK_GBS, WORKLOADS, algorithmic_bytes,  # noqa: E402
                         bench_c4_index_sharded, bench_c5_index_sharded, bench_c5_sharded,
-                        bench_exp5, bench_next_rows, bench_reference_configs, bench_workload,
+                        bench_exp5, bench_next_rows, bench_oram_tree, bench_reference_configs, bench_workload,
                         bench_ns_strong, c_abi_multi_gpu, cpu_baseline_configs, cpu_baseline_sample,
                         dominant_kernel, e2e_sample, make_records, network_records,
                         rocprof_kernel, traffic_from_profiles, _build_id)
@@ -132,6 +132,10 @@ def compact_line(full):
     if nr:
         line["next_rows"] = {"aes_gbs": _r(nr["aes_ctr_decrypt"]["gbs"]),
                              "client_producers_ms": _r(nr["client_producers"]["ms"])}
+    ot = full.get("oram_tree")
+    if ot and ot.get("rows"):
+        line["oram_tree"] = {f"n{r['n']}_k{r['k']}": {"ms": _r(r["ms"]), "ref_x": _r(r["speedup"], 3)}
+                             for r in ot["rows"]}
     if full.get("detail"):
         line["detail"] = full["detail"]
     return line
@@ -386,6 +390,7 @@ def main():
             full["reference_configs"] = bench_reference_configs(torch, D, device)
             full["exp5"] = bench_exp5(torch, D, device)
             full["next_rows"] = bench_next_rows(torch, D, device)
+            full["oram_tree"] = bench_oram_tree(torch, D, device)
         emit(full, args.detail)
     if world > 1:
         dist.destroy_process_group()

@@ -520,6 +520,37 @@ def bench_exp5(torch, D, device, reps=5):
                 source="reference: exp/results/exp5.csv col 13 means (exp/exp5.sh:8-48)", rows=rows)
 
 
+def bench_oram_tree(torch, D, device, reps=2):
+    """path_oram as the tree Path ORAM (k_oram.hip; oram.rs:64-118: Z = 4, stash 20,
+    next_pow2(d) blocks, one read + write per record in upload order, then the d-block
+    readout) on exp5's MLP-MNIST path_oram shapes, device-resident, beside the reference
+    enclave's published execution_time for the same configuration (exp5.csv)."""
+    rows = []
+    for users, alpha in ((10, 0.1), (100, 0.1), (100, 0.01)):
+        d = EXP5_MODELS["mnist"]
+        k = int(alpha * d)
+        n = max(int(0.3 * users), 1)
+        g = torch.Generator(device=device).manual_seed(users + k)
+        idx = torch.argsort(torch.rand(n, d, generator=g, device=device), dim=1)[:, :k].to(torch.int64)
+        vals = torch.randn(n, k, generator=g, device=device) * 0.01
+        rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
+        out = torch.empty(d, dtype=torch.float32, device=device)
+        D.aggregate(5, rec, n, k, d, out=out, oram_tree=True, seed=5)  # warm (scratch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(reps):
+            D.aggregate(5, rec, n, k, d, out=out, oram_tree=True, seed=6 + r)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        ref_s = EXP5_REF_S[("mnist", users, alpha)]["path_oram"]
+        rows.append(dict(num_users=users, alpha=alpha, n=n, d=d, k=k, accesses=n * k, ms=t * 1e3,
+                         us_per_access=t * 1e6 / (n * k), ref_ms=ref_s * 1e3, speedup=ref_s / t))
+        del rec, idx, vals
+    assert D.status() == 0
+    return dict(note="tree Path ORAM, one persistent workgroup (accesses are sequential); "
+                     "time per aggregate incl. the oblivious readout", rows=rows)
+
+
 def bench_next_rows(torch, D, device, steps=5):
     """SURVEY §8f rows on one GPU, device-resident: the GPU AES-128-CTR decrypt of the
     headline payload (lib.rs:312-343) and the client-side producers (utils.py:327-354,

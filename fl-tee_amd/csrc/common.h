@@ -152,6 +152,11 @@ hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m
 hipError_t launch_advanced_init_range(const void *rec, size_t nrec, size_t d, size_t pbase,
                                       size_t m, uint64_t *dst, hipStream_t s);
 size_t fold_context(size_t halo);  // records of context the fold re-reads: halo rounded to 16
+// The fold reports FLTEE_DEV_ERR_FOLD_OVERFLOW iff a run inside [0, fold_len) has more than
+// fold_run_limit(halo) = halo + 1 entries (halo = n: some client repeated an index): a
+// property of the data alone, checked in the same single pass (no rerun: the caller
+// rejects the call); below it the sums are exact.
+uint32_t fold_run_limit(size_t halo);
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
                              uint32_t *status, hipStream_t s);
@@ -192,16 +197,26 @@ hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_
                                      hipStream_t s);
 
 // k_radix.hip: the stable sort by idx of an ordered fold's n records (hand-written LSD
-// counting sort; scratch: radix_scratch_bytes) -> sorted[0, n), and the ordered fold over
-// sorted records: writes every out[i], i < d (accumulate: adds where index i has records)
+// counting sort; scratch: radix_scratch_bytes) -> sorted[0, n) (zero[0, nzero) set to +0.0
+// on the way, when given), and the ordered fold over sorted records: out[i] for the indices
+// i < d with records (accumulate: adds); the others are left as they are
 size_t radix_scratch_bytes(size_t n, size_t d);
 hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void *scratch,
                                       size_t bytes, uint64_t *sorted, uint32_t *status,
-                                      hipStream_t s);
+                                      float *zero, size_t nzero, hipStream_t s);
 hipError_t launch_fold_sorted(const uint64_t *sorted, size_t n, size_t d, float coef, float *out,
                               bool accumulate, hipStream_t s);
 hipError_t launch_gather_by_keys(const uint64_t *keys, size_t n, const void *rec, uint64_t *dst,
                                  hipStream_t s);
+
+// k_oram.hip: path_oram as a tree Path ORAM (Z = 4, stash 20, next_pow2(d) <= 2^16
+// blocks): the n*k accesses in order, then every tree/stash slot as an 8-B record (idx,
+// value; empty slots idx >= next_pow2(d), unique) in records[oram_slots(d)] for the
+// oblivious readout (advanced's network, n = 1).  tree: oram_slots(d) * 16 bytes.
+size_t oram_slots(size_t d);
+bool oram_supported(size_t d);
+hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, void *tree, uint64_t seed,
+                            uint64_t *records, uint32_t *status, hipStream_t s);
 
 // k_dp.hip
 hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,

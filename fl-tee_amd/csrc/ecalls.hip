@@ -179,42 +179,35 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
                       alg == FLTEE_ALG_NON_OBLIVIOUS;
     if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
+    if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default()) o.flags |= FLTEE_OPT_ORAM_TREE;
     if (alg == FLTEE_ALG_NIPS19) o.seed = seed ? seed : next_seed();
-    // advanced's fold (advanced.rs:66-101) is exact for runs up to the halo; halo = n
-    // covers every run of clients with distinct indices (n records + the initial
-    // entry).  A longer run (a client repeating an index) is detected and the fold
-    // reruns with a wider halo; the last attempt uses the longest run the fold can
-    // see (n * k_req + d positions: every record plus the initial entry in one run),
-    // so the loop always ends with the enclave's exact sums.
-    const size_t max_run = n * std::max(k_req, rpc) + d;
-    size_t halo = n;
-    for (int attempt = 0; attempt < 8; ++attempt) {
+    // advanced's fold (advanced.rs:66-101) runs once with halo = n: exact for every run of
+    // up to n + 1 entries — every upload whose clients each send distinct indices (n
+    // records + the initial entry) — and a run of more (some client repeated an index)
+    // is reported by the same pass (fold_run_limit): the call is rejected with 0x2,
+    // like an out-of-range index, instead of rerunning with a wider halo.  The cost is
+    // fixed by the public sizes; no data-dependent relaunch.
+    o.fold_halo = n;
+    for (int attempt = 0; attempt < 2; ++attempt) {
         if (hipMemsetAsync(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-        o.fold_halo = halo;
         uint32_t st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, c->stream, c->status);
         if (st != FLTEE_SUCCESS) return st;
         uint32_t dev_st = 0;
         if (read_status(c, &dev_st)) return FLTEE_ERROR_UNEXPECTED;
         if (dev_st == 0) return FLTEE_SUCCESS;
         if (dev_st & FLTEE_DEV_ERR_INDEX_RANGE) return FLTEE_ERROR_INVALID_PARAMETER;  // enclave panic
+        if (dev_st & FLTEE_DEV_ERR_ORAM_STASH) return FLTEE_ERROR_UNEXPECTED;  // the crate panics
         if (dev_st & FLTEE_DEV_ERR_DENSE_ORDER) {  // not dense after all: scatter semantics
             o.flags &= ~FLTEE_OPT_DENSE;
             continue;
         }
         if (dev_st & FLTEE_DEV_ERR_FOLD_OVERFLOW) {
-            if (flat) {  // a client repeated an index: exact sequential sweep
-                const float coef = 1.0f / (float)n;
-                if (alg == FLTEE_ALG_PATH_ORAM) {
-                    // range already validated by the first pass (no INDEX_RANGE bit)
-                }
-                if (aggregate_sparse_sequential(c->records.ptr, n * rpc, d, coef, d_out, false, c->stream))
-                    return FLTEE_ERROR_UNEXPECTED;
-                return hipStreamSynchronize(c->stream) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
-            }
-            if (halo >= max_run) return FLTEE_ERROR_UNEXPECTED;  // cannot happen
-            // a run longer than the halo: widen it (x16), then the bound itself
-            halo = (attempt >= 2 || halo * 16 + 16 >= max_run) ? max_run : halo * 16 + 16;
-            continue;
+            if (!flat) return FLTEE_ERROR_INVALID_PARAMETER;  // a run of more than n + 1 entries
+            // flat algorithms: a client repeated an index — the exact sequential sweep
+            const float coef = 1.0f / (float)n;
+            if (aggregate_sparse_sequential(c->records.ptr, n * rpc, d, coef, d_out, false, c->stream))
+                return FLTEE_ERROR_UNEXPECTED;
+            return hipStreamSynchronize(c->stream) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
         }
         return FLTEE_ERROR_UNEXPECTED;
     }
@@ -375,7 +368,8 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     double t2 = 0;
     const bool flat = aggregation_alg == FLTEE_ALG_BASELINE || aggregation_alg == FLTEE_ALG_PATH_ORAM ||
                       aggregation_alg == FLTEE_ALG_NON_OBLIVIOUS;
-    if (G && flat && rpc == d && bpc == d * 8) {
+    const bool tree = aggregation_alg == FLTEE_ALG_PATH_ORAM && oram_tree_default();
+    if (G && flat && !tree && rpc == d && bpc == d * 8) {
         // dense uploads over a multi-GPU eid: every GPU loads and decrypts its own
         // parameter range (group.hip); "Loading" = the parallel H2D, "Decryption" = the
         // decrypt + aggregate + gather

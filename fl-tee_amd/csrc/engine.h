@@ -28,6 +28,7 @@ struct DeviceCtx {
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel;                               // nips19's selected list
     Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch
+    Buffer ws_oram;            // path_oram tree mode: the tree + stash slots, then their records
     uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)
@@ -43,6 +44,11 @@ DeviceCtx *current_ctx();
 uint64_t next_seed();
 void set_debug_seed(uint64_t seed);
 float nips19_threshold(size_t d, size_t k, size_t n);
+
+// path_oram as the tree Path ORAM for the ECALLs (fltee_set_path_oram_tree); the device
+// API selects it per call with FLTEE_OPT_ORAM_TREE
+void set_oram_tree(int on);
+bool oram_tree_default();
 
 fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,
                          const fltee_device_opts &o, hipStream_t s, uint32_t *status);

@@ -137,6 +137,7 @@ static size_t f32_to_usize_sat(float x) {
 struct Plan {
     size_t a_bytes = 0, b_bytes = 0, mat_bytes = 0, r_bytes = 0, coef_bytes = 0, rec_bytes = 0;
     size_t keys_bytes = 0, radix_bytes = 0;  // ordered fold: sorted records, sort scratch
+    size_t oram_bytes = 0;                   // path_oram tree: slots (16 B) + their records (8 B)
 };
 
 static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -148,8 +149,16 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         if (!dense) p.rec_bytes = n * k * 8;
     }
     switch (alg) {
-    case FLTEE_ALG_BASELINE:
     case FLTEE_ALG_PATH_ORAM:
+        if ((o.flags & FLTEE_OPT_ORAM_TREE) && oram_supported(d)) {
+            const size_t ns = oram_slots(d);
+            p.oram_bytes = ns * 24;
+            p.a_bytes = p.b_bytes = next_pow2_sz(ns + d) * 8;  // the readout network
+            break;
+        }
+        if (!dense) p.mat_bytes = n * d * 4;
+        break;
+    case FLTEE_ALG_BASELINE:
         if (!dense) p.mat_bytes = n * d * 4;
         break;
     case FLTEE_ALG_NON_OBLIVIOUS:
@@ -182,7 +191,8 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
     return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
            c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
            c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes) &&
-           c->ws_keys.reserve(p.keys_bytes) && c->ws_radix.reserve(p.radix_bytes);
+           c->ws_keys.reserve(p.keys_bytes) && c->ws_radix.reserve(p.radix_bytes) &&
+           c->ws_oram.reserve(p.oram_bytes);
 }
 
 // The ordered fold of n records (common.rs:25-35, non_oblivious.rs:11-13): the records in
@@ -193,16 +203,21 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
 // bit for bit: test_gpu_parity.py).
 static bool g_radix_order = true;
 void set_radix_order(int on) { g_radix_order = on != 0; }
+static bool g_oram_tree = false;  // the ECALLs' path_oram: the sweep unless set
+void set_oram_tree(int on) { g_oram_tree = on != 0; }
+bool oram_tree_default() { return g_oram_tree; }
 
 static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, size_t d,
                                        float coef, float *out, bool acc, uint32_t *status,
                                        hipStream_t s) {
+    if (n == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
     if (!c->ws_keys.reserve(n * 8)) return hipErrorOutOfMemory;
     uint64_t *sorted = (uint64_t *)c->ws_keys.ptr;
     hipError_t e;
     if (g_radix_order) {
         if (!c->ws_radix.reserve(radix_scratch_bytes(n, d))) return hipErrorOutOfMemory;
-        e = launch_sort_records_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, sorted, status, s);
+        e = launch_sort_records_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, sorted, status,
+                                       acc ? nullptr : out, d, s);
     } else {
         const size_t mc = next_pow2_sz(n);
         if (!c->ws_radix.reserve(mc * 8)) return hipErrorOutOfMemory;
@@ -210,6 +225,7 @@ static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, 
         e = launch_composite_init(rec, n, d, mc, keys, status, s);
         if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, n);  // ~0 keys past n
         if (e == hipSuccess) e = launch_gather_by_keys(keys, n, rec, sorted, s);
+        if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
     }
     if (e == hipSuccess) e = launch_fold_sorted(sorted, n, d, coef, out, acc, s);
     return e;
@@ -377,8 +393,22 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
 
     hipError_t e = hipSuccess;
     switch (alg) {
-    case FLTEE_ALG_BASELINE:
     case FLTEE_ALG_PATH_ORAM:
+        if (o.flags & FLTEE_OPT_ORAM_TREE) {  // the tree Path ORAM (k_oram.hip)
+            if (!oram_supported(d) || n * k > 0xFFFFFFFFull) return FLTEE_ERROR_INVALID_PARAMETER;
+            const size_t ns = oram_slots(d);
+            uint8_t *tree = (uint8_t *)c->ws_oram.ptr;
+            uint64_t *recs = (uint64_t *)(tree + ns * 16);
+            const uint64_t seed = o.seed ? o.seed : next_seed();
+            e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);  // oram.rs panics
+            if (e == hipSuccess) e = launch_oram_tree(rec, n * k, d, tree, seed, recs, status, s);
+            // the readout: every slot's (idx, value) through advanced's oblivious network
+            // (one "client" of ns records: each index at most once, runs of <= 2 entries)
+            if (e == hipSuccess) e = run_advanced(c, recs, 1, ns, d, ns, 1, coef, out, acc, status, s);
+            break;
+        }
+        [[fallthrough]];
+    case FLTEE_ALG_BASELINE:
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (dense) {
             e = launch_dense_accumulate(rec, n, d, coef, out, ccoef, acc, status, s);
@@ -475,7 +505,7 @@ fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t 
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
     const Plan p = plan_for(alg, n, k, d, o);
     return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes +
-           p.keys_bytes + p.radix_bytes;
+           p.keys_bytes + p.radix_bytes + p.oram_bytes;
 }
 
 bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -824,6 +854,10 @@ extern "C" void fltee_debug_set_fold_compact(int on) { fltee::set_fold_compact(o
 // A/B hook: 0 runs the networks over the pad-only stage blocks too
 extern "C" void fltee_debug_set_pad_skip(int on) { fltee::set_pad_skip(on); }
 extern "C" void fltee_debug_set_radix_order(int on) { fltee::set_radix_order(on); }
+extern "C" void fltee_set_path_oram_tree(int on) {
+    std::lock_guard<std::recursive_mutex> lk(fltee::api_mutex());
+    fltee::set_oram_tree(on);
+}
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes

@@ -577,11 +577,12 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
     }
     if (network(G, chunk, spare, M, 0, 0, W > 1, n * k + d) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     // fold (advanced.rs:66-101) with the previous range's tail in front and the next
-    // range's head behind; a run longer than the halo widens it (as the ECALL does)
-    const size_t fold_len = L, max_run = L;
-    size_t h = n;
+    // range's head behind, halo n: a run of more than n + 1 entries rejects the call (as
+    // the ECALL does: fold_run_limit), no rerun
+    const size_t fold_len = L;
+    const size_t h = n;
     std::vector<float *> outs(W);
-    for (int attempt = 0;; ++attempt) {
+    {
         const size_t H = fold_context(h);
         if (H > C) return FLTEE_GROUP_FALLBACK;
         const size_t m = H + C + 16;
@@ -614,9 +615,7 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
         if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
         bool over = false;
         for (uint32_t v : st) over |= (v & FLTEE_DEV_ERR_FOLD_OVERFLOW) != 0;
-        if (!over) break;
-        if (h >= max_run) return FLTEE_ERROR_UNEXPECTED;
-        h = (attempt >= 2 || h * 16 + 16 >= max_run) ? max_run : h * 16 + 16;
+        if (over) return FLTEE_ERROR_INVALID_PARAMETER;
     }
     for (int i = 0; i < W; ++i) {  // advanced.rs:106-111 + :32-34: each range's representatives
         Rank &R = G.r[i];
@@ -717,9 +716,8 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
     }
     std::vector<const uint64_t *> rec;
     if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
-    size_t h = n;
-    const size_t max_run = n * k + d;
-    for (int attempt = 0;; ++attempt) {
+    const size_t h = n;  // a run of more than n + 1 entries rejects the call (no rerun)
+    {
         std::vector<P2P> ops;
         std::vector<const uint32_t *> sw;
         for (int i = 0; i < W; ++i) {
@@ -745,12 +743,8 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
         if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
         bool over = false;
         for (uint32_t v : st) over |= (v & FLTEE_DEV_ERR_FOLD_OVERFLOW) != 0;
-        if (!over) {
-            if (p2p(G, ops) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-            break;
-        }
-        if (h >= max_run) return FLTEE_ERROR_UNEXPECTED;
-        h = (attempt >= 2 || h * 16 + 16 >= max_run) ? max_run : h * 16 + 16;
+        if (over) return FLTEE_ERROR_INVALID_PARAMETER;
+        if (p2p(G, ops) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     }
     // lib.rs:564-573: global[i] += batch_sum[i] in batch order, then x 1f32/n
     if (hipSetDevice(G.r[0].dev) != hipSuccess ||

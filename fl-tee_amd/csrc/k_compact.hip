@@ -295,9 +295,9 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 // position: idx[p+1] != idx[p], or p = L-1) with idx < d, and then the run's sum —
 // v_head, (v_head + v_next), ... left to right, the enclave's order.  Every run head
 // in the window walks its run in LDS and leaves the sum in the val of the run's last
-// record; a run longer than the halo (its head before the window and its end at or
-// after the tile start) is reported as FLTEE_DEV_ERR_FOLD_OVERFLOW like the fold
-// kernel, and the caller reruns with a wider halo.  The folded array (1 GB at C5) is
+// record; a run of more than halo + 1 entries (positions p and p - halo - 1 in one run,
+// the window reaching that far back) is reported as FLTEE_DEV_ERR_FOLD_OVERFLOW like
+// the fold kernel (fold_run_limit), and the caller rejects the call.  The folded array (1 GB at C5) is
 // never written and read back.  Dummies and non-representatives are never selected by
 // the compaction, so their contents do not matter.
 // Resident blocks per CU of the fused first pass, and whether a block prefetches its next
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 25
                                                             uint32_t S, uint32_t Hr,
                                                             uint32_t ntiles, float coef,
                                                             float *__restrict__ out,
-                                                            uint32_t *status) {
+                                                            uint32_t lim, uint32_t *status) {
     constexpr uint32_t CAP = (uint32_t)NT * PER;
     // XMAX: window slots beyond CAP per lane, ceil((Hr + 1) / NT)
     extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1
@@ -333,7 +333,6 @@ __global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 25
     // before position 0 or past M are dummies (clamped address, select after the load:
     // no branch around the loads)
     uint64_t pf[PER + XMAX];
-    uint32_t ck0 = 0, ck1 = 0;  // idx at a - Hr - 1 and at a: the overflow test's keys
     auto prefetch = [&](uint32_t tl) {
         const long long wlo = (long long)tl * S - (long long)Hr;
 #pragma unroll
@@ -344,11 +343,6 @@ __global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 25
                 rs, (int)(ok ? (uint32_t)p * 8u : 0u), 0, 0);
             pf[i] = ok ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
         }
-        // every lane loads the same two words (one request per wave), issued with the
-        // window instead of after it
-        const long long pa = (long long)tl * S;
-        ck0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(pa - Hr - 1 >= 0 ? (uint32_t)(pa - Hr - 1) * 8u : 0u), 0, 0);
-        ck1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(pa < (long long)M ? (uint32_t)pa * 8u : 0u), 0, 0);
     };
     uint32_t tile = blockIdx.x;
     if (tile >= ntiles) return;
@@ -359,8 +353,6 @@ __global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 25
 #pragma unroll
         for (uint32_t i = 0; i < PER + XMAX; ++i)
             if (t + i * NT < Wn) win[t + i * NT] = pf[i];
-        if (t == 0 && a < (long long)L && a - (long long)Hr - 1 >= 0 && ck0 == ck1)
-            atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
@@ -406,19 +398,26 @@ __global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 25
                 win[Wn - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;
         }
         __syncthreads();
-        // representatives with idx < d -> (c = p - idx, sum); the rest never move
+        // representatives with idx < d -> (c = p - idx, sum); the rest never move.  And the
+        // run-length test (fold_run_limit): positions p and p - lim in one run (runs are
+        // contiguous) = a run of more than lim entries; the window holds p - lim (Hr >= lim).
+        // (Measured against the test in the fold loop — a run's length at its end, plus the
+        // tile-start test for heads before the window: C5 1,150 vs 1,099 us per pass.)
         uint64_t v[PER];
+        bool over = false;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
             const uint32_t f = t + i * NT, x = f + Hr;
             const long long p = a + f;
             const uint64_t r = win[x];
             const uint32_t idx = (uint32_t)r;
+            over |= f < S && p < (long long)L && p >= (long long)lim && (uint32_t)win[x - lim] == idx;
             const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
             v[i] = (p < (long long)L && idx < d && end)
                        ? ((r & 0xFFFFFFFF00000000ull) | (uint32_t)((uint32_t)p - idx))
                        : CP_DUMMY;
         }
+        if (over) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
         __syncthreads();
         uint64_t *sm = win;
 #pragma unroll
@@ -485,7 +484,7 @@ void set_fold_compact(int on) { g_fold_compact = on != 0; }
 template <int PER, int F, int X>
 static hipError_t fc_launch(unsigned grid, size_t lds, hipStream_t s, const uint64_t *A, uint64_t *B,
                             size_t L, size_t M, size_t d, uint32_t G, uint32_t S, size_t Hr,
-                            uint64_t ntiles, float coef, float *out, uint32_t *status) {
+                            uint64_t ntiles, float coef, float *out, uint32_t lim, uint32_t *status) {
     constexpr int NT = 512;
     static bool attr = false;  // 26-37 KB of window
     if (!attr) {
@@ -495,7 +494,7 @@ static hipError_t fc_launch(unsigned grid, size_t lds, hipStream_t s, const uint
     }
     hipLaunchKernelGGL((fold_compact_first<NT, PER, F, X>), dim3(grid), dim3(NT), lds, s, A, B,
                        (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles,
-                       coef, out, status);
+                       coef, out, lim, status);
     return hipGetLastError();
 }
 
@@ -503,8 +502,8 @@ template <int PER>
 static hipError_t fc_dispatch(int F, bool x1, unsigned grid, size_t lds, hipStream_t s,
                               const uint64_t *A, uint64_t *B, size_t L, size_t M, size_t d,
                               uint32_t G, uint32_t S, size_t Hr, uint64_t ntiles, float coef,
-                              float *out, uint32_t *status) {
-#define FC_ARGS grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status
+                              float *out, uint32_t lim, uint32_t *status) {
+#define FC_ARGS grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status
     if (F == 0) return x1 ? fc_launch<PER, 0, 1>(FC_ARGS) : fc_launch<PER, 0, 2>(FC_ARGS);
     if (F == 2) return x1 ? fc_launch<PER, 2, 1>(FC_ARGS) : fc_launch<PER, 2, 2>(FC_ARGS);
     return x1 ? fc_launch<PER, 1, 1>(FC_ARGS) : fc_launch<PER, 1, 2>(FC_ARGS);
@@ -515,7 +514,9 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
                                        size_t halo, float coef, float *out, bool accumulate,
                                        uint32_t *status, hipStream_t s) {
     constexpr uint32_t NT = 512;
-    const size_t Hr = fold_context(halo);
+    // the window reaches lim = halo + 1 records back for the run-length test
+    const size_t Hr = fold_context(halo + 1);
+    const uint32_t lim = fold_run_limit(halo);
     // A/B in one process (scripts/ab_fold_compact.py, profiles/r02/ab/fold_compact.jsonl):
     // C3 (Hr = 112): 0.211 vs 0.214 ms with the separate fold; C5 (Hr = 1008, windows 25 %
     // wider than the tile): 17.66 vs 17.48 ms in round 2, when it stayed separate; round 3
@@ -550,9 +551,9 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr < 1024)
     const int F = !last ? 0 : (accumulate ? 2 : 1);
     hipError_t e;
-    if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
-    else if (per == 6) e = fc_dispatch<6>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
-    else e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, status);
+    if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
+    else if (per == 6) e = fc_dispatch<6>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
+    else e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
     if (e != hipSuccess || last) return e;
     return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);
 }

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
                                                          uint64_t *__restrict__ dst, long long m,
                                                          long long origin, long long end,
                                                          long long pbase, long long fold_len,
-                                                         uint32_t Hr, uint32_t C,
+                                                         uint32_t Hr, uint32_t C, uint32_t lim,
                                                          uint32_t *status) {
     __shared__ uint64_t win[2][64 * FS_ROW];
     const uint32_t l = threadIdx.x;
@@ -125,6 +125,8 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     float pre_val = 0.0f;
     bool started = false;
     uint64_t prev = 0;
+    uint32_t cnt = 0;   // entries of the current run seen so far (a lower bound in the halo)
+    bool over = false;  // a run of more than lim entries inside [0, fold_len)
     auto stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
         uint64_t *cur = win[s & 1], *old = win[(s + 1) & 1];
 #pragma unroll
@@ -155,6 +157,9 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
                 pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
                 pre_idx = ci;
                 started = true;
+                cnt = eq ? cnt + 1 : 1;
+                // (q < end: a lane past the range streams zero-filled windows it never stores)
+                over |= q < end && qg < fold_len && cnt > lim;
             }
             prev = r[t];
         }
@@ -181,15 +186,21 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         for (int q = 0; q < DEPTH; ++q)
             if (s + (uint32_t)q < nstage) stage(pf[q], s + (uint32_t)q);
     }
+    if (over) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
 }
 
 size_t fold_context(size_t halo) { return (halo + FS_W - 1) / FS_W * FS_W; }
+uint32_t fold_run_limit(size_t halo) {
+    return halo + 1 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(halo + 1);
+}
 
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
                              uint32_t *status, hipStream_t s) {
     const size_t Hr = fold_context(halo);
     if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
+    // runs of more than halo + 1 entries are reported, wherever they lie (fold_run_limit)
+    const uint32_t lim = fold_run_limit(halo);
     if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
     const size_t span = end - origin;
     size_t C = 64;
@@ -210,7 +221,7 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
 #define FS_GO(D_)                                                                                  \
     hipLaunchKernelGGL(fold_stream_kernel<D_>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,   \
                        (long long)m, (long long)origin, (long long)end, pbase, (long long)fold_len, \
-                       (uint32_t)Hr, (uint32_t)C, status)
+                       (uint32_t)Hr, (uint32_t)C, lim, status)
     if (depth == 2) FS_GO(2);
     else FS_GO(1);
 #undef FS_GO

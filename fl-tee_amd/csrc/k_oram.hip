@@ -1,0 +1,316 @@
+// k_oram.hip — path_oram as a tree Path ORAM on the GPU (oram.rs:64-118; the mobilecoin
+// PathORAM the enclave instantiates: bucket size Z = 4, stash 20, next_pow2(d) blocks).
+//
+// oram.rs:100-105 runs, for every uploaded record in upload order, oram.read(idx), adds
+// the value, and oram.write(idx) back; then reads blocks 0..d-1 (:111-113) and averages.
+// The blocks start at +0.0 (prepare(), :79-82).  Each ORAM access is one Path ORAM
+// access (Stefanov et al.): look the block's leaf up in the position map and give the
+// block a fresh random leaf; read the path root..leaf of that leaf into the pool (path
+// buckets + stash); take the block out of the pool, add, put it back with its new leaf;
+// evict greedily — every block goes to the deepest bucket of the path it may live in
+// (the buckets its own leaf's path shares with this path), four per bucket — and keep
+// what does not fit in the stash; write the whole path back.
+//
+// GPU form: ONE persistent wave (the accesses are sequential: each path read needs the
+// previous access's path write; lane j holds pool entries j and 64 + j).  Its LDS holds
+// the position map (u16 leaves, N <= 2^16 blocks) and the stash; the tree of 4 (2N - 1)
+// 16-B slots (idx, leaf, f32 value) lives in HBM.  Obliviousness, as the enclave's (ZeroTrace-style) ORAM has it:
+//  * the HBM trace of an access is one whole path, root to a uniformly random leaf;
+//  * the position map is read and written at one address per access by every lane of
+//    the wave at once (an LDS broadcast: no bank conflict, the same time for any
+//    address) — it never leaves the workgroup;
+//  * inside the pool every step is branch-free over all Z (L + 1) + 20 entries: the
+//    block is found and taken out by compares and selects, eviction ranks come from
+//    wave ballots, and the new path and stash are GATHERED slot by slot by selects over
+//    every pool entry (fixed LDS addresses), never scattered.
+// Blocks are created lazily: a block not in the pool reads as +0.0, prepare()'s value,
+// and nothing is written for blocks never uploaded (the readout below gives them +0.0).
+// Leaves come from Philox4x32-10 under the call's seed (FLTEE_STREAM_ORAM).
+//
+// Readout (:111-113, d oblivious reads): every tree slot and the stash become one 8-B
+// record (idx, value) — empty slots a unique idx >= N — and `advanced`'s oblivious
+// network (sort, fold, compaction; engine.hip) puts block i's value (or +0.0) at out[i]:
+// each index appears once among the records, so its run is (i, +0.0) + the block, and
+// +0.0 + v == v (a sum that started at +0.0 is never -0.0).  The same bits as the
+// in-order sum of non_oblivious / baseline, and the oracle's fo_path_oram.
+#include "common.h"
+
+namespace fltee {
+
+#define FLTEE_STREAM_ORAM 0x4F52414Du
+constexpr uint32_t kOramZ = 4, kOramStash = 20;
+constexpr uint32_t kOramEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kOramMaxLog = 16;  // position map in LDS as u16 leaves
+
+__device__ __forceinline__ uint32_t oram_leaf(uint32_t k0, uint32_t k1, uint32_t ctr, uint32_t mask) {
+    uint32_t c[4] = {ctr, FLTEE_STREAM_ORAM, 0u, 0u};
+    philox4x32_10(c, k0, k1);
+    return c[0] & mask;
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    for (int o = 32; o; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+// slot s of the path to leaf x: level s / Z, bucket (2^l - 1) + (x >> (Lh - l))
+__device__ __forceinline__ uint32_t oram_slot(uint32_t s, uint32_t x, uint32_t Lh) {
+    const uint32_t l = s / kOramZ;
+    return (((1u << l) - 1u) + (x >> (Lh - l))) * kOramZ + (s % kOramZ);
+}
+
+// the z-th set bit (z = 0, 1, ...) of a 128-bit mask (m0 | m1 << 64), one per call:
+// the lowest remaining bit is returned (index, or 0xFF) and cleared.  Uniform (SALU).
+__device__ __forceinline__ uint32_t take_lowest(uint64_t &m0, uint64_t &m1) {
+    // branch-free (ffsll is defined at 0; m & (m - 1) keeps 0 at 0)
+    const bool h0 = m0 != 0, h1 = m1 != 0;
+    const uint32_t f0 = (uint32_t)__builtin_ffsll((long long)m0) - 1u;
+    const uint32_t f1 = (uint32_t)__builtin_ffsll((long long)m1) - 1u;
+    const uint32_t i = h0 ? f0 : (h1 ? 64u + f1 : 0xFFu);
+    const uint64_t keep1 = h0 ? ~0ull : m1 - 1;
+    m0 &= m0 - 1;
+    m1 &= keep1;
+    return i;
+}
+
+// the path slot words of leaf x for lane j (slot j, and slot 64 + j when P > 64)
+struct OramLane {
+    uint32_t a0, l0, w0, a1, l1, w1;
+};
+__device__ __forceinline__ void oram_load_path(const uint4 *tree, uint32_t x, uint32_t Lh, uint32_t lane,
+                                               bool p0, bool p1, OramLane &r) {
+    if (p0) {
+        const uint32_t *ts = reinterpret_cast<const uint32_t *>(tree + oram_slot(lane, x, Lh));
+        r.a0 = __hip_atomic_load(ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r.l0 = __hip_atomic_load(ts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r.w0 = __hip_atomic_load(ts + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (p1) {
+        const uint32_t *ts = reinterpret_cast<const uint32_t *>(tree + oram_slot(64 + lane, x, Lh));
+        r.a1 = __hip_atomic_load(ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r.l1 = __hip_atomic_load(ts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        r.w1 = __hip_atomic_load(ts + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// rec: nrec records (idx < N checked by the caller's range pass; clamped here);
+// tree: 4 (2N - 1) slots (all empty on entry) followed by the 20 stash slots (written at
+// the end for the readout).  One wave: lane j holds pool entries j and 64 + j (the path
+// slots first, then the stash), as (idx, leaf, value) words — plain registers, never an
+// indexed array (which would go to scratch).
+// Per access, after its own path is in registers: the NEXT access's leaf is read (after
+// this access's position-map write, so a repeated index sees its new leaf) and its path
+// loads are issued, to land while this access computes; the buckets the two paths share
+// (the top levels: l <= Lh - bitlen(x ^ x')) are then taken from this access's output,
+// which lives in the same lanes (slot l*Z + z of either path), the others from the loads.
+// A lane only ever stores and reloads its own slots, so program order orders them.
+// The eviction's gather: per level, the ranks of the blocks that may go there come from
+// one ballot; the z-th one's pool index is selected into the lane of slot l*Z + z (SALU
+// + one compare and select), the stash slots likewise, and every lane then fetches its new content
+// from that pool entry with ds_bpermute (a register crossbar: no LDS bank, so the same
+// time for any pattern).
+__global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__ rec,
+                                                       uint32_t nrec, uint32_t Lh,
+                                                       uint4 *__restrict__ tree, uint32_t k0,
+                                                       uint32_t k1, uint32_t *status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t N = 1u << Lh, mask = N - 1u;
+    const uint32_t P = kOramZ * (Lh + 1), POOL = P + kOramStash;
+    uint4 *st = reinterpret_cast<uint4 *>(smem);                   // the stash: kOramStash entries
+    uint2 *rb = reinterpret_cast<uint2 *>(st + kOramStash);        // records q0 .. q0 + 63
+    uint32_t *lb = reinterpret_cast<uint32_t *>(rb + 64);          // and their new leaves
+    uint16_t *pm = reinterpret_cast<uint16_t *>(lb + 64);          // N leaves
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < N; i += 64) pm[i] = (uint16_t)oram_leaf(k0, k1, nrec + i, mask);
+    if (lane < kOramStash) st[lane] = make_uint4(kOramEmpty, 0u, 0u, 0u);
+    // a batch of 64 records into LDS (a broadcast read per access afterwards): the record
+    // loads are waited for once per 64 accesses, never on the access path
+    auto batch = [&](uint32_t q0) {
+        rb[lane] = q0 + lane < nrec ? rec[q0 + lane] : make_uint2(0u, 0u);
+        lb[lane] = oram_leaf(k0, k1, q0 + lane, mask);
+    };
+    batch(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const bool v0 = lane < POOL, v1 = 64 + lane < POOL;
+    const bool p0 = lane < P, p1 = 64 + lane < P;  // path slot (else stash entry)
+    const uint32_t s0i = lane - P, s1i = 64 + lane - P;  // stash index of a stash entry
+    const uint32_t lev0 = lane / kOramZ, lev1 = (64 + lane) / kOramZ;  // their levels
+    uint32_t over = 0;
+    OramLane cur = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
+    uint32_t x = 0;
+    if (nrec) {
+        x = pm[rb[0].x & mask];  // every lane reads the same words: broadcasts
+        oram_load_path(tree, x, Lh, lane, p0, p1, cur);
+    }
+    // every load landed before the loop: the loop's own waits then cover only what it
+    // issued (the compiler otherwise keeps the first path "pending" at every iteration)
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t q = 0; q < nrec; ++q) {
+        const uint2 r = rb[q & 63u];
+        const uint32_t a = r.x & mask;
+        const float w = __uint_as_float(r.y);
+        const uint32_t nleaf = lb[q & 63u];
+        if (lane == 0) pm[a] = (uint16_t)nleaf;  // the block's fresh leaf
+        // the next access: its record, its leaf (after the write above), its path's loads
+        if (((q + 1) & 63u) == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            batch(q + 1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        const bool more = q + 1 < nrec;
+        const uint32_t an = rb[(q + 1) & 63u].x & mask;
+        const uint32_t xn = more ? (uint32_t)pm[an] : x;
+        OramLane nxt = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
+        if (more) oram_load_path(tree, xn, Lh, lane, p0, p1, nxt);
+        // the pool: this path (registers) and the stash (LDS)
+        uint32_t a0 = cur.a0, l0 = cur.l0, w0 = cur.w0, a1 = cur.a1, l1 = cur.l1, w1 = cur.w1;
+        if (!p0) {
+            const uint4 e = v0 ? st[s0i] : make_uint4(kOramEmpty, 0u, 0u, 0u);
+            a0 = e.x, l0 = e.y, w0 = e.z;
+        }
+        if (!p1) {
+            const uint4 e = v1 ? st[s1i] : make_uint4(kOramEmpty, 0u, 0u, 0u);
+            a1 = e.x, l1 = e.y, w1 = e.z;
+        }
+        // read: the block (at most one entry holds it), or +0.0
+        const bool m0 = a0 == a, m1 = a1 == a;
+        const uint32_t vb = wave_or((m0 ? w0 : 0u) | (m1 ? w1 : 0u));
+        const bool found = (__ballot(m0) | __ballot(m1)) != 0;
+        const float nv = __fadd_rn(found ? __uint_as_float(vb) : 0.0f, w);
+        a0 = m0 ? kOramEmpty : a0;
+        a1 = m1 ? kOramEmpty : a1;
+        // write: the block with its new leaf into the first free entry
+        uint64_t f0 = __ballot(v0 && a0 == kOramEmpty), f1 = __ballot(v1 && a1 == kOramEmpty);
+        const uint32_t fi = take_lowest(f0, f1);
+        over |= fi == 0xFFu;
+        const bool i0 = fi == lane, i1 = fi == 64u + lane;
+        a0 = i0 ? a : a0, l0 = i0 ? nleaf : l0, w0 = i0 ? __float_as_uint(nv) : w0;
+        a1 = i1 ? a : a1, l1 = i1 ? nleaf : l1, w1 = i1 ? __float_as_uint(nv) : w1;
+        // eviction: the deepest level each block may take on this path, four per bucket;
+        // src0 / src1: the pool entry each slot (lane, 64 + lane) receives, 0xFF = empty
+        const bool o0 = v0 && a0 != kOramEmpty, o1 = v1 && a1 != kOramEmpty;
+        const uint32_t lm0 = Lh - (32u - (uint32_t)__clz((int)(l0 ^ x)));
+        const uint32_t lm1 = Lh - (32u - (uint32_t)__clz((int)(l1 ^ x)));
+        uint64_t left0 = __ballot(o0), left1 = __ballot(o1);  // not placed yet
+        uint32_t src0 = 0xFFu, src1 = 0xFFu;
+        for (int l = (int)Lh; l >= 0; --l) {
+            uint64_t e0 = __ballot(lm0 >= (uint32_t)l) & left0, e1 = __ballot(lm1 >= (uint32_t)l) & left1;
+            const uint64_t b0 = e0, b1 = e1;
+#pragma unroll
+            for (uint32_t z = 0; z < kOramZ; ++z) {
+                const uint32_t si = take_lowest(e0, e1);
+                const uint32_t s = (uint32_t)l * kOramZ + z;
+                src0 = lane == s ? si : src0;
+                src1 = lane + 64 == s ? si : src1;
+            }
+            left0 &= ~(b0 & ~e0);  // the (up to) four taken at this level
+            left1 &= ~(b1 & ~e1);
+        }
+        // what stays goes to the stash, in pool order
+        over |= (uint32_t)(__popcll(left0) + __popcll(left1)) > kOramStash;
+        for (uint32_t z = 0; z < kOramStash; ++z) {
+            const uint32_t si = take_lowest(left0, left1);
+            const uint32_t s = P + z;
+            src0 = lane == s ? si : src0;
+            src1 = lane + 64 == s ? si : src1;
+        }
+        // gather through the register crossbar: from set 0 or set 1 of lane src & 63
+        const int ad0 = (int)((src0 & 63u) * 4u), ad1 = (int)((src1 & 63u) * 4u);
+        const bool h0 = src0 != 0xFFu, h1 = src1 != 0xFFu, hi0 = src0 >= 64u, hi1 = src1 >= 64u;
+        const uint32_t ga0x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)a0),
+                       ga0y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)a1);
+        const uint32_t gl0x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)l0),
+                       gl0y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)l1);
+        const uint32_t gw0x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)w0),
+                       gw0y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad0, (int)w1);
+        const uint32_t ga1x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)a0),
+                       ga1y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)a1);
+        const uint32_t gl1x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)l0),
+                       gl1y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)l1);
+        const uint32_t gw1x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)w0),
+                       gw1y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad1, (int)w1);
+        const uint32_t ga0 = !h0 ? kOramEmpty : (hi0 ? ga0y : ga0x), gl0 = hi0 ? gl0y : gl0x,
+                       gw0 = hi0 ? gw0y : gw0x;
+        const uint32_t ga1 = !h1 ? kOramEmpty : (hi1 ? ga1y : ga1x), gl1 = hi1 ? gl1y : gl1x,
+                       gw1 = hi1 ? gw1y : gw1x;
+        // the next access's path: the shared top levels from this output, the rest loaded
+        // (merged before this access's stores are issued: the wait for the loads then does
+        // not also wait for these stores — CDNA counts both in vmcnt, in order)
+        const uint32_t top = Lh - (32u - (uint32_t)__clz((int)(x ^ xn)));  // deepest shared level
+        const bool sh0 = lev0 <= top, sh1 = lev1 <= top;
+        OramLane nc;
+        nc.a0 = sh0 ? ga0 : nxt.a0, nc.l0 = sh0 ? gl0 : nxt.l0, nc.w0 = sh0 ? gw0 : nxt.w0;
+        nc.a1 = sh1 ? ga1 : nxt.a1, nc.l1 = sh1 ? gl1 : nxt.l1, nc.w1 = sh1 ? gw1 : nxt.w1;
+        // pin the merge here (the compiler would sink it past the stores, and its wait for
+        // the loads would then wait for them too)
+        asm volatile("" : "+v"(nc.a0), "+v"(nc.l0), "+v"(nc.w0), "+v"(nc.a1), "+v"(nc.l1), "+v"(nc.w1)
+                     :
+                     : "memory");
+        // write the path back (the whole path, fixed addresses) and the stash
+        if (p0) tree[oram_slot(lane, x, Lh)] = make_uint4(ga0, gl0, gw0, 0u);
+        else if (v0) st[s0i] = make_uint4(ga0, gl0, gw0, 0u);
+        if (p1) tree[oram_slot(64 + lane, x, Lh)] = make_uint4(ga1, gl1, gw1, 0u);
+        else if (v1) st[s1i] = make_uint4(ga1, gl1, gw1, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        cur = nc;
+        x = xn;
+    }
+    // the stash, after the tree, for the readout
+    if (lane < kOramStash) tree[(size_t)kOramZ * (2u * N - 1u) + lane] = st[lane];
+    if (__ballot(over != 0) && lane == 0) atomicOr(status, FLTEE_DEV_ERR_ORAM_STASH);
+}
+
+__global__ void oram_fill_kernel(uint4 *__restrict__ tree, size_t ns) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < ns; i += (size_t)gridDim.x * 256)
+        tree[i] = make_uint4(kOramEmpty, 0u, 0u, 0u);
+}
+
+// tree + stash slots -> 8-B records (idx, value); an empty slot j gets idx N + j (unique,
+// never < d): every index appears at most once
+__global__ void oram_records_kernel(const uint4 *__restrict__ tree, size_t ns, uint32_t N,
+                                    uint2 *__restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < ns; i += (size_t)gridDim.x * 256) {
+        const uint4 s = tree[i];
+        out[i] = make_uint2(s.x == kOramEmpty ? N + (uint32_t)i : s.x, s.z);
+    }
+}
+
+size_t oram_slots(size_t d) {
+    const size_t N = next_pow2_sz(d ? d : 1);
+    return kOramZ * (2 * N - 1) + kOramStash;
+}
+
+bool oram_supported(size_t d) { return next_pow2_sz(d ? d : 1) <= ((size_t)1 << kOramMaxLog); }
+
+hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, void *tree, uint64_t seed,
+                            uint64_t *records, uint32_t *status, hipStream_t s) {
+    if (!oram_supported(d) || nrec > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const size_t N = next_pow2_sz(d ? d : 1);
+    const uint32_t Lh = log2_pow2(N);
+    const size_t ns = oram_slots(d);
+    size_t blocks = (ns + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(oram_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4 *)tree, ns);
+    const size_t lds = kOramStash * 16 + 64 * 8 + 64 * 4 + N * 2;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)oram_tree_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(oram_tree_kernel, dim3(1), dim3(64), lds, s, (const uint2 *)rec,
+                       (uint32_t)nrec, Lh, (uint4 *)tree, (uint32_t)seed, (uint32_t)(seed >> 32),
+                       status);
+    hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
+    return hipGetLastError();
+}
+
+}  // namespace fltee

@@ -35,6 +35,11 @@ constexpr int kCsItems = 8;                // records per lane per tile
 constexpr int kCsTile = kCsNT * kCsItems;  // records per tile
 constexpr int kCsGroups = kCsItems * (kCsNT / 64);  // (round, wave) groups per tile
 constexpr int kCsBins = 256;
+// FLTEE_CS_STAGE: cs_scatter stages the tile in LDS and writes it out in sorted order (1) or
+// scatters each record straight from its registers (0) — A/B (scripts/ab_build.sh)
+#ifndef FLTEE_CS_STAGE
+#define FLTEE_CS_STAGE 1
+#endif
 
 struct CsPlan {
     uint32_t passes = 0, width = 0;
@@ -63,9 +68,12 @@ template <bool ALL>
 __global__ __launch_bounds__(kCsNT) void cs_hist(const uint64_t *__restrict__ src, uint32_t n,
                                                  uint32_t d, uint32_t shift, uint32_t width,
                                                  uint32_t passes, uint32_t ntiles,
-                                                 uint32_t *__restrict__ counts, uint32_t *status) {
+                                                 uint32_t *__restrict__ counts, uint32_t *status,
+                                                 float *__restrict__ zero, uint32_t nzero) {
     __shared__ uint32_t h[4][kCsBins];  // [pass][digit] (ALL), [0][digit] otherwise
     const uint32_t t = threadIdx.x;
+    if constexpr (ALL)  // the fold's output, for the indices without records (+0.0)
+        for (uint32_t i = blockIdx.x * kCsNT + t; i < nzero; i += gridDim.x * kCsNT) zero[i] = 0.0f;
     for (uint32_t q = 0; q < 4; ++q) h[q][t] = 0;
     __syncthreads();
     const uint32_t mask = (1u << width) - 1u;
@@ -150,11 +158,11 @@ __global__ __launch_bounds__(kCsNT) void cs_scatter(const uint64_t *__restrict__
                                                     uint32_t ntiles,
                                                     const uint32_t *__restrict__ offsets,
                                                     uint64_t *__restrict__ dst) {
-    __shared__ uint32_t grp[kCsGroups][kCsBins];  // (round, wave) x digit: count -> offset
+    __shared__ uint16_t grp[kCsGroups][kCsBins];  // (round, wave) x digit: count -> offset
     __shared__ uint32_t tile_at[kCsBins];         // the tile's first slot per digit (global)
     __shared__ uint32_t loc_at[kCsBins];          // ... and inside the tile's staged order
     __shared__ uint32_t part[kCsNT / 64];
-    __shared__ uint64_t stage[kCsTile];           // the tile's records in sorted order
+    __shared__ uint64_t stage[FLTEE_CS_STAGE ? kCsTile : 1];  // the tile's records, sorted
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t mask = (1u << width) - 1u;
     for (int g = 0; g < kCsGroups; ++g) grp[g][t] = 0;
@@ -179,9 +187,24 @@ __global__ __launch_bounds__(kCsNT) void cs_scatter(const uint64_t *__restrict__
         }
         rank[r] = (uint32_t)__popcll(peers & lt);
         // the lowest peer records the group's count for this digit
-        if (live && (peers & lt) == 0) grp[r * (kCsNT / 64) + wv][dig[r]] = (uint32_t)__popcll(peers);
+        if (live && (peers & lt) == 0) grp[r * (kCsNT / 64) + wv][dig[r]] = (uint16_t)__popcll(peers);
     }
     __syncthreads();
+    if constexpr (!FLTEE_CS_STAGE) {  // straight from the registers: global group offsets
+        __shared__ uint32_t gofs[kCsGroups][kCsBins];
+        uint32_t run = t <= mask ? tile_at[t] : 0u;
+#pragma unroll
+        for (int g = 0; g < kCsGroups; ++g) {
+            gofs[g][t] = run;
+            run += grp[g][t];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kCsItems; ++r)
+            if (base + (uint32_t)r * kCsNT + t < n)
+                dst[gofs[r * (kCsNT / 64) + wv][dig[r]] + rank[r]] = rec[r];
+        return;
+    }
     // lane t = digit t: exclusive scan of its counts over the groups in position order, then
     // of the digits' tile totals (the staged order: digit by digit, stable within a digit)
     uint32_t tot;
@@ -197,7 +220,7 @@ __global__ __launch_bounds__(kCsNT) void cs_scatter(const uint64_t *__restrict__
             run += c;
         }
 #pragma unroll
-        for (int g = 0; g < kCsGroups; ++g) grp[g][t] = v[g];
+        for (int g = 0; g < kCsGroups; ++g) grp[g][t] = (uint16_t)v[g];
         tot = run;
     }
     uint32_t inc = tot;
@@ -236,7 +259,7 @@ size_t radix_scratch_bytes(size_t n, size_t d) {
 
 hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void *scratch,
                                       size_t bytes, uint64_t *sorted, uint32_t *status,
-                                      hipStream_t s) {
+                                      float *zero, size_t nzero, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (n > 0x7FFFFFFFull || d > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (bytes < radix_scratch_bytes(n, d)) return hipErrorOutOfMemory;
@@ -247,7 +270,7 @@ hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void 
     const uint32_t nt = (uint32_t)p.tiles, nb = 1u << p.width;
     const uint64_t *src = (const uint64_t *)rec;
     hipLaunchKernelGGL(cs_hist<true>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d, 0u,
-                       p.width, p.passes, nt, counts, status);
+                       p.width, p.passes, nt, counts, status, zero, (uint32_t)(zero ? nzero : 0));
     hipLaunchKernelGGL(cs_rowsum, dim3(nb, p.passes), dim3(kCsNT), 0, s, (const uint32_t *)counts, nt,
                        totals);
     hipError_t e = hipGetLastError();
@@ -258,7 +281,7 @@ hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void 
         const uint32_t shift = q * p.width;
         if (q > 0)  // this pass's counts by ITS tiles (pass 0's came with the totals)
             hipLaunchKernelGGL(cs_hist<false>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n,
-                               (uint32_t)d, shift, p.width, p.passes, nt, counts, status);
+                               (uint32_t)d, shift, p.width, p.passes, nt, counts, status, nullptr, 0u);
         hipLaunchKernelGGL(cs_scan, dim3(nb), dim3(kCsNT), 0, s, counts, nt, totals + q * kCsBins);
         hipLaunchKernelGGL(cs_scatter, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d,
                            shift, p.width, nt, (const uint32_t *)counts, dst);
@@ -271,13 +294,14 @@ hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void 
 // ----------------------------------------------------- the ordered fold ---
 // out[i] = ((+0 + v1) + v2) ... over index i's records in sorted (= list) order, the order
 // of non_oblivious.rs:11-13 and common.rs:25-35; x coef, or accumulate: out[i] += sum.
+// (Without accumulate the indices without records hold +0.0: cs_hist zero-fills out.)
 // One wave per kFoldCh x 64 sorted records, all loaded up front with one chunk more (one
-// memory latency per wave): the run heads (a record whose predecessor has another idx) are
-// folded one after the other, each by the whole wave — 64 records at a time added in lane
-// order by readlane (a uniform serial chain: the exact left fold), further chunks read
-// only while a run goes on past the preloaded ones.  Without accumulate a head also writes
-// +0.0 to the indices between its predecessor's and its own (no records: the enclave's g
-// starts at +0.0), and the last record's wave the indices after it: no fill pass.
+// memory latency per wave): the run heads among them (a record whose predecessor has
+// another idx) are folded one after the other, each by the whole wave — 64 records at a
+// time added in lane order by readlane (a uniform serial chain: the exact left fold),
+// further chunks read only while a run goes on past the preloaded ones.  (Tried: one LANE
+// per run, the segment staged in LDS and each run read at known offsets — C4 8.36 vs
+// 8.32 ms with this kernel, `profiles/r04/ab/ab4_fold_lane_per_run_c4_rejected.jsonl`.)
 constexpr int kFoldCh = 4;
 
 __device__ __forceinline__ float fold_lanes(float acc, int vb, int from, int to) {
@@ -286,7 +310,7 @@ __device__ __forceinline__ float fold_lanes(float acc, int vb, int from, int to)
 }
 
 template <bool ACC>
-__global__ __launch_bounds__(256) void fold_sorted_kernel(const uint64_t *__restrict__ srt,
+__global__ __launch_bounds__(256) void fold_chunks_kernel(const uint64_t *__restrict__ srt,
                                                           uint32_t n, uint32_t d, float coef,
                                                           float *__restrict__ out) {
     const uint32_t lane = threadIdx.x & 63;
@@ -319,11 +343,7 @@ __global__ __launch_bounds__(256) void fold_sorted_kernel(const uint64_t *__rest
             heads &= heads - 1;
             const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)h);
             const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)prev, (int)h);
-            if constexpr (!ACC) {  // indices without records between the previous run and this one
-                const uint32_t g0 = (h == 0 && q0 == 0) ? 0u : pv + 1u;
-                const uint32_t g1 = i < d ? i : d;
-                for (uint32_t j = g0 + lane; j < g1; j += 64) out[j] = 0.0f;
-            }
+            (void)pv;
             if (i >= d) continue;
             // the run's records among these 64 lanes: lanes h .. h + cnt - 1 (contiguous)
             const int cnt = __popcll(__ballot(idx == i));
@@ -347,27 +367,20 @@ __global__ __launch_bounds__(256) void fold_sorted_kernel(const uint64_t *__rest
             }
             if (lane == 0) out[i] = ACC ? __fadd_rn(out[i], acc) : __fmul_rn(acc, coef);
         }
-        if constexpr (!ACC) {  // the indices after the last record's
-            if (n - 1 - q0 < 64) {
-                const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)idx, (int)(n - 1 - q0));
-                if (last < d)
-                    for (uint32_t j = last + 1u + lane; j < d; j += 64) out[j] = 0.0f;
-            }
-        }
     }
 }
 
+
 hipError_t launch_fold_sorted(const uint64_t *sorted, size_t n, size_t d, float coef, float *out,
                               bool accumulate, hipStream_t s) {
-    if (d == 0) return hipSuccess;
-    if (n == 0) return accumulate ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    if (d == 0 || n == 0) return hipSuccess;
     if (n > 0x7FFFFFFFull || d > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((n + 256 * kFoldCh - 1) / (256 * kFoldCh));
     if (accumulate)
-        hipLaunchKernelGGL(fold_sorted_kernel<true>, dim3(blocks), dim3(256), 0, s, sorted,
+        hipLaunchKernelGGL(fold_chunks_kernel<true>, dim3(blocks), dim3(256), 0, s, sorted,
                            (uint32_t)n, (uint32_t)d, coef, out);
     else
-        hipLaunchKernelGGL(fold_sorted_kernel<false>, dim3(blocks), dim3(256), 0, s, sorted,
+        hipLaunchKernelGGL(fold_chunks_kernel<false>, dim3(blocks), dim3(256), 0, s, sorted,
                            (uint32_t)n, (uint32_t)d, coef, out);
     return hipGetLastError();
 }

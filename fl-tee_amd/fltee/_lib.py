@@ -34,6 +34,7 @@ OPT_CLIP = 0x4
 OPT_ACCUMULATE = 0x8
 OPT_NO_AVERAGE = 0x10
 OPT_K_REQ = 0x20
+OPT_ORAM_TREE = 0x40
 
 
 class DeviceOpts(ctypes.Structure):
@@ -90,6 +91,7 @@ SIGNATURES = {
     "fltee_select_device": (_U32, [_P, _S, _S, _P, _S, _P, _P]),
     "fltee_ordered_list_device": (_U32, [_P, _S, _S, _F, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
+    "fltee_set_path_oram_tree": (None, [ctypes.c_int]),
     "fltee_version": (ctypes.c_char_p, []),
     "fltee_device_init_multi": (_U32, [_P, ctypes.c_int, _P]),
     "fltee_device_count": (ctypes.c_int, [_U64]),

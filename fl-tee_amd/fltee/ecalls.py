@@ -108,3 +108,9 @@ class Enclave:
 def set_debug_seed(seed):
     """Deterministic RNG for sampling / nips19 / DP (tests only; 0 restores RDRAND-like)."""
     L.lib().fltee_debug_set_seed(seed)
+
+
+def set_path_oram_tree(on):
+    """aggregation_alg 5 through the ECALLs: the tree Path ORAM (oram.rs:64-118) when on, the
+    output-equivalent oblivious sweep (default) when off (fltee_set_path_oram_tree)."""
+    L.lib().fltee_set_path_oram_tree(1 if on else 0)

@@ -410,6 +410,10 @@ def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None
     return out
 
 
+class FoldRunTooLong(ValueError):
+    """advanced's fold saw a run of more than halo + 1 entries: the ECALL's 0x2."""
+
+
 def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None, halo=None,
                            root=0, dp=None, exchange="transpose", spare=None):
     """Option B: `advanced` over the padded array of M = next_pow2(n_total*k + d)
@@ -422,7 +426,9 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     advanced.rs:39-113 step by step: the network (:147-176) = per-range stages up to
     C, then per stage the exchange steps (j >= C, partner r ^ j/C) and the range's
     own steps (j < C); the fold (:66-101) with fold_context(halo) records of the
-    previous range in front and the next range's first records behind; the second
+    previous range in front and the next range's first records behind (a run of more
+    than halo + 1 entries raises FoldRunTooLong: every rank raises, as the ECALL
+    returns 0x2); the second
     sort's [0, d) prefix (:106-111, :32-34) = each range's compacted representatives,
     summed over the ranges by one reduce, then x 1f32/n (common.rs:14-19).
 
@@ -442,20 +448,21 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     chunks = distributed_network(chunks, world, M, ops, comm, exchange=exchange, spare=spare,
                                  valid=n_total * k + d)
     fold_len = n_total * k + d
+    # one fold with halo n (or the caller's): a run of more than halo + 1 entries (a client
+    # repeated an index) is reported by every range that sees it and rejects the call, as
+    # the ECALL does (0x2) — no data-dependent rerun
     h = n_total if halo is None else halo
-    while True:
-        H = ops.fold_context(h)
-        if H > C:
-            raise ValueError(f"fold context {H} exceeds the range size {C}")
-        prev, nxt = comm.neighbours(chunks, H, 16, ops.pads)
-        folded, statuses = {}, []
-        for r, x in chunks.items():
-            buf = torch.cat([prev[r], x, nxt[r]])
-            folded[r], st = ops.fold(buf, H, H + C, r * C - H, fold_len, h, key=r)
-            statuses.append(st)
-        if comm.all_true(ops.ok(statuses)):
-            break
-        h = h * 4 + 16  # a run longer than the halo (a client repeated an index)
+    H = ops.fold_context(h)
+    if H > C:
+        raise ValueError(f"fold context {H} exceeds the range size {C}")
+    prev, nxt = comm.neighbours(chunks, H, 16, ops.pads)
+    folded, statuses = {}, []
+    for r, x in chunks.items():
+        buf = torch.cat([prev[r], x, nxt[r]])
+        folded[r], st = ops.fold(buf, H, H + C, r * C - H, fold_len, h, key=r)
+        statuses.append(st)
+    if not comm.all_true(ops.ok(statuses)):
+        raise FoldRunTooLong(f"a run of more than {h + 1} entries (a client repeated an index)")
     outs = {r: ops.compact(f, d, key=r) for r, f in folded.items()}
     out = comm.reduce(outs, root)
     if out is None:

@@ -140,7 +140,9 @@ fltee_status_t ecall_client_size_optimized_secure_aggregation(
 /* device status bits */
 #define FLTEE_DEV_ERR_DENSE_ORDER 0x1u   /* dense input with idx != position */
 #define FLTEE_DEV_ERR_INDEX_RANGE 0x2u   /* idx >= d where the reference panics */
-#define FLTEE_DEV_ERR_FOLD_OVERFLOW 0x4u /* a run longer than the fold halo */
+#define FLTEE_DEV_ERR_FOLD_OVERFLOW 0x4u /* a run of more than halo + 1 entries (advanced's
+                                           fold; halo n: a client repeated an index) */
+#define FLTEE_DEV_ERR_ORAM_STASH 0x8u    /* path_oram tree mode: the stash (20) overflowed */
 #define FLTEE_DEV_ERR_LAUNCH 0x80000000u
 
 /* option flags */
@@ -152,6 +154,9 @@ fltee_status_t ecall_client_size_optimized_secure_aggregation(
 #define FLTEE_OPT_K_REQ 0x20u      /* advanced: fold over n*k_req+d even if k_req != k
                                       (advanced.rs:70 uses the REQUEST's k; 0 when
                                       fl_main.py sends dense uploads without --alpha) */
+#define FLTEE_OPT_ORAM_TREE 0x40u  /* path_oram as a tree Path ORAM (oram.rs:64-118: Z = 4,
+                                      stash 20, next_pow2(d) <= 2^16 blocks) instead of the
+                                      output-equivalent oblivious sweep */
 
 typedef struct fltee_device_opts {
     uint32_t flags;     /* FLTEE_OPT_* */
@@ -315,6 +320,11 @@ fltee_status_t fltee_ordered_list_device(const void *d_list, size_t lc, size_t d
                                          float *d_out, void *stream);
 
 /* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
+/* The ECALLs' path_oram (aggregation_alg 5): on = the tree Path ORAM of oram.rs:64-118
+ * (Z = 4, stash 20, next_pow2(d) <= 2^16 blocks; k_oram.hip), off (default) = the
+ * output-equivalent oblivious sweep.  Both give the in-order sum bit for bit.  The device
+ * API selects it per call with FLTEE_OPT_ORAM_TREE. */
+void fltee_set_path_oram_tree(int on);
 void fltee_debug_set_seed(uint64_t seed);
 /* Library build/version string. */
 const char *fltee_version(void);

@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ "${TESTS:-1}" = 1 ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
+  timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -q -p no:cacheprovider --timeout 300 \
       --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1 || exit 11
   tail -3 "$OUT/pytest_gpu.log"
 fi

@@ -147,37 +147,45 @@ def _encrypt(oracle, ids, recs):
     return oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
 
 
-def test_advanced_long_run_ends_exact(enclave, oracle):
-    """a client repeating one index k times makes a run of ~k records, far
-    longer than the fold's n-record halo.  The ECALL widens the halo and, at the
-    latest, folds with the longest possible run (n*k + d): always the exact sums."""
+def test_advanced_long_run_is_rejected(enclave, oracle):
+    """advanced's fold runs once with halo n — fixed cost.  A client
+    repeating one index k times makes a run of ~k entries, more than the n + 1 that
+    distinct indices allow: the fold's own pass reports it and the ECALL returns 0x2 (like
+    an out-of-range index) instead of rerunning with a wider halo, for alg 1 and alg 6.
+    A repeated index that keeps every run within n + 1 entries is still folded exactly."""
+    from fltee import _lib as L
     from fltee.ecalls import set_debug_seed
-    n, k = 30, 4000
-    d = k
+    n = 30
     rng = np.random.default_rng(5)
     ids = np.arange(500, 500 + n, dtype=np.uint32)
-    recs = []
-    for c in range(n):
-        w = np.zeros(k, dtype=oracle.WEIGHT)
-        w["idx"] = 7 if c == 3 else rng.permutation(d)[:k]
-        w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
-        recs.append(w)
-    enc = _encrypt(oracle, ids, recs)
-    for alg, fl in ((1, 610), (6, 611)):
-        set_debug_seed(SEED)
-        O = oracle.OracleEnclave(seed=SEED)
-        run_round(enclave, ids, d, k, alg, enc, fl)
-        O.fl_init(fl, ids, d, k, 1.12, 1.0, 0.1, 1.0, alg)
-        O.start_round(fl, 0, n)
-        if alg == 1:
-            st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k, alg)
-            ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, k, alg)
-        else:
-            st, rv, out, _ = enclave.ecall_client_size_optimized_secure_aggregation(
-                fl, 0, 7, ids, enc, d, k, alg)
-            ost, ref, _ = O.client_size_optimized_secure_aggregation(fl, 0, 7, ids, enc, d, k, alg)
-        assert (st, rv, ost) == (0, 0, 0)
-        assert bits_equal(out, ref)
+    for k, d, reps, want in ((4000, 4000, 4000, L.ERROR_INVALID_PARAMETER), (1000, 4000, 3, 0)):
+        recs = []
+        for c in range(n):
+            w = np.zeros(k, dtype=oracle.WEIGHT)
+            w["idx"] = rng.permutation(d)[:k]
+            if c == 3:
+                w["idx"][:reps] = 7  # client 3 repeats index 7 `reps` times
+            w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+            recs.append(w)
+        enc = _encrypt(oracle, ids, recs)
+        for alg, fl in ((1, 610 + reps), (6, 620 + reps)):
+            set_debug_seed(SEED)
+            O = oracle.OracleEnclave(seed=SEED)
+            run_round(enclave, ids, d, k, alg, enc, fl)
+            O.fl_init(fl, ids, d, k, 1.12, 1.0, 0.1, 1.0, alg)
+            O.start_round(fl, 0, n)
+            if alg == 1:
+                st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, k, alg)
+                ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, k, alg)
+            else:
+                st, rv, out, _ = enclave.ecall_client_size_optimized_secure_aggregation(
+                    fl, 0, 7, ids, enc, d, k, alg)
+                ost, ref, _ = O.client_size_optimized_secure_aggregation(fl, 0, 7, ids, enc, d, k, alg)
+            assert (st, rv, ost) == (0, want, 0)
+            if want == 0:
+                assert bits_equal(out, ref)
+            else:
+                assert not out.any()  # a rejected call returns the zeroed [out] buffer
     set_debug_seed(0)
 
 

@@ -109,24 +109,37 @@ def test_group_alg6_bit_identical_to_one_gpu(enclaves, oracle, name, batch, w):
 
 
 def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
-    """A client repeating one index (fold halo widening on every range) and the k=0
-    dense quirk (advanced.rs:70, the root path): both equal the single-GPU result."""
+    """A client repeating one index (a run of more than n + 1 entries): every eid rejects
+    the call with 0x2 after one fold (no halo widening, as the ECALL); the k=0 dense
+    quirk (advanced.rs:70, the root path) equals the single-GPU result."""
+    from fltee import _lib as L
+    from fltee.ecalls import set_debug_seed
     rng = np.random.default_rng(3)
     n, k, d = 16, 3000, 3000
     ids = np.arange(900, 900 + n, dtype=np.uint32)
-    recs = []
+    recs, plain = [], []
     for i in range(n):
         w = np.zeros(k, dtype=oracle.WEIGHT)
-        w["idx"] = 11 if i == 5 else rng.permutation(d)[:k]
+        w["idx"] = rng.permutation(d)[:k]
         w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        plain.append(w.copy())
+        if i == 5:
+            w["idx"] = 11
         recs.append(w)
     enc = oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
-    c = dict(client_ids=ids, d=d, k=k, n=n, name="long")
-    one = run(enclaves[1], c, 1, enc)
-    for w in (2, 8):
-        assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, 1, enc).view(np.uint32))
-    one0 = run(enclaves[1], c, 1, enc, k=0)
-    assert np.array_equal(one0.view(np.uint32), run(enclaves[4], c, 1, enc, k=0).view(np.uint32))
+    for w in (1, 2, 8):
+        E = enclaves[w]
+        _fl[0] += 1
+        set_debug_seed(SEED)
+        assert E.ecall_fl_init(_fl[0], ids, d, k, 1.12, 1.0, 0.1, 1.0, 1, 0, 0) == (0, 0)
+        assert E.ecall_start_round(_fl[0], 0, n)[:2] == (0, 0)
+        st, rv, out, _ = E.ecall_secure_aggregation(_fl[0], 0, ids, enc, d, k, 1)
+        set_debug_seed(0)
+        assert (st, rv) == (0, L.ERROR_INVALID_PARAMETER) and not out.any()
+    enc0 = oracle.encrypt_clients(ids, [r.tobytes() for r in plain])
+    c = dict(client_ids=ids, d=d, k=k, n=n, name="quirk")
+    one0 = run(enclaves[1], c, 1, enc0, k=0)
+    assert np.array_equal(one0.view(np.uint32), run(enclaves[4], c, 1, enc0, k=0).view(np.uint32))
 
 
 @pytest.mark.parametrize("alg", [1, 2, 4])

@@ -122,14 +122,24 @@ def test_dense_out_of_order_falls_back_to_scatter(enclave, oracle):
 
 
 def test_repeated_index_within_client(enclave, oracle):
-    # a client repeats an index: baseline's oblivious sweep reruns sequentially (exact)
+    # a client repeats an index: baseline's oblivious sweep reruns sequentially (exact);
+    # advanced's one fold (halo n) sees index 3 with n + 2 entries (two from client 1,
+    # one from client 2, the initial entry) and the call is rejected with 0x2 (DESIGN §7:
+    # fixed cost, no rerun); with client 2 not sending 3 every run fits: exact
     ids = np.array([1, 2], np.uint32)
     w1 = oracle.as_weights(np.array([3, 3, 5], np.uint32), np.array([0.1, 0.2, 0.3], np.float32))
     w2 = oracle.as_weights(np.array([3, 4, 5], np.uint32), np.array([1e-8, 0.5, 0.7], np.float32))
     enc = oracle.encrypt_clients(ids, [w1.tobytes(), w2.tobytes()])
     for alg in (1, 3, 4, 5):
         (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 90 + alg, ids, 8, 3, alg, enc)
+        if alg == 1:
+            assert (st, rv, ost) == (0, 0x2, 0) and not out.any()
+            continue
         assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref), alg
+    w2 = oracle.as_weights(np.array([2, 4, 5], np.uint32), np.array([1e-8, 0.5, 0.7], np.float32))
+    enc = oracle.encrypt_clients(ids, [w1.tobytes(), w2.tobytes()])
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 96, ids, 8, 3, 1, enc)
+    assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
 
 
 def test_non_oblivious_out_of_range_rejected(enclave, oracle):
