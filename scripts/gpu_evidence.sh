@@ -26,22 +26,22 @@ for spec in ${ABH:+"$ABH"}; do
   echo "abh $w $hook"
 done
 if [ "${BENCH:-1}" = 1 ]; then
-  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 12
+  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} --detail "$OUT/bench_detail.json" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 12
   tail -c 600 "$OUT/bench.json"; echo
 fi
 for w in ${PROFILE}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 20 --warmup 3 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/prof_$w.log" 2>&1 || exit 13
+      --no-e2e --detail "$OUT/prof_$w.detail.json" > "$OUT/prof_$w.log" 2>&1 || exit 13
   echo "profiled $w"
 done
 for w in ${PMC}; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/pmc_fetch_$w.log" 2>&1 || exit 14
+      --no-e2e --detail "" > "$OUT/pmc_fetch_$w.log" 2>&1 || exit 14
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
+      --no-e2e --detail "" > "$OUT/pmc_write_$w.log" 2>&1 || exit 15
   echo "pmc $w"
 done
 # SQ counters per kernel (one pass of <= 8 SQ counters each, its own run)
@@ -52,18 +52,28 @@ SQC=${SQC:-SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ}
 for w in ${SQ}; do
   timeout -s KILL 150 rocprofv3 --pmc ${SQ1} --output-format csv -d "$OUT/sq1_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/sq1_$w.log" 2>&1 || exit 18
+      --no-e2e --detail "" > "$OUT/sq1_$w.log" 2>&1 || exit 18
   timeout -s KILL 150 rocprofv3 --pmc ${SQ2} --output-format csv -d "$OUT/sq2_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/sq2_$w.log" 2>&1 || exit 19
+      --no-e2e --detail "" > "$OUT/sq2_$w.log" 2>&1 || exit 19
   timeout -s KILL 150 rocprofv3 --pmc ${SQ3} --output-format csv -d "$OUT/sq3_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/sq3_$w.log" 2>&1 || exit 20
+      --no-e2e --detail "" > "$OUT/sq3_$w.log" 2>&1 || exit 20
   timeout -s KILL 150 rocprofv3 --pmc ${SQC} --output-format csv -d "$OUT/sqc_$w" -o run \
       -- python3 bench.py --workload "$w" --steps 6 --warmup 1 --no-extra --no-cpu-baseline \
-      --no-e2e > "$OUT/sqc_$w.log" 2>&1 || exit 21
+      --no-e2e --detail "" > "$OUT/sqc_$w.log" 2>&1 || exit 21
   echo "sq $w"
 done
+if [ "${ORAM:-0}" = 1 ]; then  # the tree Path ORAM (scripts/oram_probe.py): timing + SQ passes
+  timeout -k 10 120 python3 -u scripts/oram_probe.py 10 5089 50890 > "$OUT/oram_probe.log" 2>&1 || exit 24
+  cat "$OUT/oram_probe.log"
+  for p in 1 2 3; do
+    eval "cs=\$SQ$p"
+    timeout -s KILL 120 rocprofv3 --pmc ${cs} --output-format csv -d "$OUT/sq${p}_oram" -o run \
+        -- python3 scripts/oram_probe.py 3 5089 50890 > "$OUT/sq${p}_oram.log" 2>&1 || exit 25
+  done
+  echo "oram"
+fi
 if [ "${AESPROF:-0}" = 1 ]; then  # the constant-time AES-CTR kernel (scripts/bench_aes.py shapes)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_aes" -o run \
       -- python3 scripts/bench_aes.py > "$OUT/prof_aes.log" 2>&1 || exit 17

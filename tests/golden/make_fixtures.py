@@ -227,6 +227,63 @@ def reference_aggregate_fixtures(utils, update, models):
     np.savez_compressed(os.path.join(OUT, "ref_aggregate.npz"), **flat)
 
 
+CFG_CASES = [  # (name, dense, n): BASELINE configs[3]'s shape, Purchase100 x 300 clients
+    ("purchase100_sparse_n300", False, 300),
+    ("purchase100_dense_n300", True, 300),
+]
+
+
+def config_aggregate_fixtures(utils, update, models):
+    """The reference's own aggregate at a benchmark configuration's full size
+    (ref_aggregate_cfg.npz): MLPPurchase100 (fl_main.py:69-77, d = 44,964), 300 clients,
+    alpha = 0.1 top-k (k = 4,496) and dense — configs[3]'s shape.
+
+    The 300 payloads (10.8 MB sparse, 108 MB dense) are not stored.  They are a pure
+    function of the stored seeds and parameter shapes: each client's diff is
+    perturbed_diff (torch.randn from its seed, in state-dict order), its payload
+    zero_except_top_k_weights + serialize_sparse (utils.py:327-354,193-209: stable sort
+    by |value| descending, the first k) or serialize_dense.  tests/refcheck.py
+    regenerates the records with numpy/torch and checks them against the sha256 of the
+    reference's bytes stored here, so the expected aggregate (update_global_weights,
+    update.py:173-184) is pinned to the reference's own client and aggregator code."""
+    import hashlib
+    from collections import OrderedDict
+    model = models.MLPPurchase100(dim_in=600, dim_hidden=64, dim_out=100)
+    bn = utils.get_buffer_names(model)
+    d = utils.count_parameters(model)
+    shapes = [tuple(v.shape) for key, v in model.state_dict().items() if key not in bn]
+    flat = {}
+    for ci, (name, dense, n) in enumerate(CFG_CASES):
+        k = d if dense else int(0.1 * d)
+        ids = (np.arange(n, dtype=np.uint32) * 7 + 11).astype(np.uint32)
+        seeds = (np.arange(n, dtype=np.int64) + 900_000 + 10_000 * ci).astype(np.int64)
+        h = hashlib.sha256()
+        states = []
+        for seed in seeds:
+            diff = perturbed_diff(model, seed=int(seed))
+            if dense:
+                st = diff
+                b = utils.serialize_dense(st, bn, d)
+            else:
+                st, idxs = utils.zero_except_top_k_weights(diff, bn, k)
+                b = utils.serialize_sparse(st, bn, idxs)
+            h.update(b)
+            states.append(OrderedDict((key, v.clone()) for key, v in st.items()))
+        glob = OrderedDict((key, torch.zeros_like(v)) for key, v in model.state_dict().items())
+        update.update_global_weights(glob, states)   # the reference's aggregator
+        ref_avg = utils.flatten_params(utils.get_learnable_parameters(glob, bn)).numpy()
+        fx = dict(client_ids=ids, seeds=seeds, d=d, k=k, n=n, dense=dense,
+                  ref_avg=ref_avg.astype(np.float32), payload_sha256=h.hexdigest(),
+                  scale=0.01)
+        for key, v in fx.items():
+            flat[name + "__" + key] = np.asarray(v)
+        print("ref_aggregate_cfg", name, "d", d, "k", k, "n", n, h.hexdigest()[:16])
+    flat["cases"] = np.array([c[0] for c in CFG_CASES])
+    flat["shapes"] = np.array([list(s) + [1] * (2 - len(s)) for s in shapes], dtype=np.int64)
+    flat["shape_rank"] = np.array([len(s) for s in shapes], dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "ref_aggregate_cfg.npz"), **flat)
+
+
 def main():
     if "--wire-only" in sys.argv:
         wire_fixtures()
@@ -237,6 +294,9 @@ def main():
         return
     if "--ref-aggregate-only" in sys.argv:
         reference_aggregate_fixtures(utils, update, models)
+        return
+    if "--ref-aggregate-cfg-only" in sys.argv:
+        config_aggregate_fixtures(utils, update, models)
         return
     torch.manual_seed(1)
 
@@ -322,6 +382,7 @@ def main():
     print("ffi kat ok")
     client_fixtures(utils, update, models)
     reference_aggregate_fixtures(utils, update, models)
+    config_aggregate_fixtures(utils, update, models)
     wire_fixtures()
 
 

@@ -85,4 +85,64 @@ def assert_reassociated(out, c, rel=1e-6):
 def records(c):
     """The reference's plaintext payload as oracle.WEIGHT records (client-major)."""
     import oracle as O
+    if "recs" in c:
+        return c["recs"]
     return np.frombuffer(c["plaintext"].tobytes(), dtype=O.WEIGHT)
+
+
+# ---- configuration-size cases (ref_aggregate_cfg.npz, make_fixtures.py
+# config_aggregate_fixtures): the payloads are regenerated from the stored seeds and
+# checked against the sha256 of the bytes the reference's client code produced
+
+
+def _load_cfg():
+    if "cfg" not in _cache:
+        _cache["cfg"] = np.load(os.path.join(GOLDEN, "ref_aggregate_cfg.npz"))
+    return _cache["cfg"]
+
+
+def cfg_cases():
+    return [str(c) for c in _load_cfg()["cases"]]
+
+
+def regen_records(shapes, seeds, k, dense, scale=0.01):
+    """Each client's diff as make_fixtures.perturbed_diff draws it (torch.randn from the
+    seed, parameter by parameter), flattened; its payload as the reference's
+    zero_except_top_k_weights + serialize_sparse build it (utils.py:327-354,193-209:
+    a stable sort by |value| descending, the first k, in that order) or serialize_dense
+    (every index in order)."""
+    import torch
+
+    import oracle as O
+    out = []
+    for s in seeds:
+        g = torch.Generator().manual_seed(int(s))
+        flat = torch.cat([(torch.randn(sh, generator=g) * scale).reshape(-1) for sh in shapes]).numpy()
+        idx = (np.arange(flat.size) if dense else np.argsort(-np.abs(flat), kind="stable")[:k])
+        w = np.empty(idx.size, dtype=O.WEIGHT)
+        w["idx"] = idx
+        w["val"] = flat[idx]
+        out.append(w)
+    return np.concatenate(out)
+
+
+def cfg_case(name):
+    import hashlib
+    if ("cfgcase", name) in _cache:
+        return _cache[("cfgcase", name)]
+    fx = _load_cfg()
+    rank = fx["shape_rank"]
+    shapes = [tuple(int(x) for x in s[:r]) for s, r in zip(fx["shapes"], rank)]
+    c = {key: fx[name + "__" + key] for key in ("client_ids", "seeds", "d", "k", "n", "dense",
+                                                 "ref_avg", "payload_sha256", "scale")}
+    c["d"], c["k"], c["n"] = int(c["d"]), int(c["k"]), int(c["n"])
+    c["dense"] = bool(c["dense"])
+    c["name"] = name
+    recs = regen_records(shapes, c["seeds"], c["k"], c["dense"], float(c["scale"]))
+    assert hashlib.sha256(recs.tobytes()).hexdigest() == str(c["payload_sha256"]), \
+        f"{name}: regenerated payload differs from the reference client's bytes"
+    c["recs"] = recs
+    vals = recs["val"].astype(np.float64)
+    c["abs_sum"] = np.bincount(recs["idx"], weights=np.abs(vals), minlength=c["d"])
+    _cache[("cfgcase", name)] = c
+    return c

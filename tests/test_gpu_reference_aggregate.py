@@ -130,3 +130,62 @@ def test_device_nips19_bit_exact_vs_oracle_and_close_to_reference(oracle, name):
     assert st == 0
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
     R.assert_reassociated(out, c)
+
+
+# ---- configs[3]'s full shape: Purchase100 x 300 clients (ref_aggregate_cfg.npz; the
+# payloads are rebuilt from seeds and checked against the reference client's bytes) ----
+
+def cfg_payload(oracle, c):
+    if c["name"] not in _enc_cache:
+        w = R.records(c).reshape(c["n"], c["k"])
+        _enc_cache[c["name"]] = oracle.encrypt_clients(
+            c["client_ids"], [w[i].tobytes() for i in range(c["n"])])
+    return _enc_cache[c["name"]]
+
+
+CFG_IN_ORDER = [("purchase100_sparse_n300", 3), ("purchase100_sparse_n300", 4),
+                ("purchase100_sparse_n300", 5), ("purchase100_dense_n300", 3),
+                ("purchase100_dense_n300", 4)]
+
+
+@pytest.mark.parametrize("name,alg", CFG_IN_ORDER)
+def test_cfg_ecall_in_order_algs_match_reference(enclave, oracle, name, alg):
+    """baseline / non_oblivious / path_oram through the ECALL at configs[3]'s size vs
+    the reference's update_global_weights: within 1 ulp (n = 300)."""
+    c = R.cfg_case(name)
+    fl = round0(enclave, c, alg)
+    st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, c["client_ids"], cfg_payload(oracle, c),
+                                                      c["d"], c["k"], alg)
+    assert (st, rv) == (0, 0)
+    R.assert_in_order_exact(out, c)
+
+
+def test_cfg_ecall_advanced_matches_reference(enclave, oracle):
+    """advanced (M = 2^21) at configs[3]'s size: within the reassociation bound of the
+    reference's aggregate, and bit for bit the oracle's network."""
+    c = R.cfg_case("purchase100_sparse_n300")
+    fl = round0(enclave, c, 1)
+    st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, c["client_ids"], cfg_payload(oracle, c),
+                                                      c["d"], c["k"], 1)
+    assert (st, rv) == (0, 0)
+    R.assert_reassociated(out, c)
+    ref, ost = oracle.advanced(c["k"], R.records(c), c["d"], c["n"])
+    assert ost == 0 and np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+def test_cfg_ecall_nips19_and_alg6_match_reference(enclave, oracle):
+    """nips19 at configs[3]'s full size (request k = 4,496: the C4 shuffle, M = 2^27) and
+    alg 6 in batches of 64, vs the reference's aggregate."""
+    c = R.cfg_case("purchase100_sparse_n300")
+    fl = round0(enclave, c, 2)
+    st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, c["client_ids"], cfg_payload(oracle, c),
+                                                      c["d"], c["k"], 2)
+    assert (st, rv) == (0, 0)
+    R.assert_reassociated(out, c)
+    fl = round0(enclave, c, 6)
+    st, rv, out, _ = enclave.ecall_client_size_optimized_secure_aggregation(
+        fl, 0, 64, c["client_ids"], cfg_payload(oracle, c), c["d"], c["k"], 6)
+    assert (st, rv) == (0, 0)
+    R.assert_reassociated(out, c)
+    ref, ost = oracle.client_size_optimized(64, c["k"], R.records(c), c["d"], c["n"])
+    assert ost == 0 and np.array_equal(out.view(np.uint32), ref.view(np.uint32))

@@ -98,3 +98,41 @@ def test_oracle_ecall_matches_reference(oracle):
             R.assert_in_order_exact(out, c)
         else:
             R.assert_reassociated(out, c)
+
+
+# ---- configs[3]'s full shape (Purchase100, 300 clients): ref_aggregate_cfg.npz ------
+
+CFG = R.cfg_cases()
+
+
+@pytest.mark.parametrize("name", CFG)
+def test_cfg_payload_regenerates_the_reference_bytes(name):
+    """The records the tests rebuild from the stored seeds are byte for byte the
+    payloads the reference's client code serialised (sha256 in the fixture)."""
+    c = R.cfg_case(name)  # asserts the sha256
+    w = R.records(c)
+    assert w.size == c["n"] * c["k"] and (w["idx"] < c["d"]).all()
+    assert c["ref_avg"].shape == (c["d"],) and np.isfinite(c["ref_avg"]).all()
+
+
+@pytest.mark.parametrize("name", CFG)
+def test_cfg_oracle_in_order_matches_reference(oracle, name):
+    """non_oblivious (and, sparse, baseline's o_update sweep) at the full configuration
+    vs update_global_weights (n = 300: within 1 ulp — torch.div vs x * (1f32/n)).  The
+    dense baseline is the same in-order sum; its oracle sweep takes a minute here, so
+    the GPU test covers it (test_gpu_reference_aggregate.py)."""
+    c = R.cfg_case(name)
+    w = R.records(c)
+    g, st = oracle.non_oblivious(w, c["d"], c["n"])
+    assert st == 0
+    R.assert_in_order_exact(g, c)
+    if not c["dense"]:
+        R.assert_in_order_exact(oracle.baseline(w, c["d"], c["n"]), c)
+
+
+def test_cfg_oracle_advanced_matches_reference(oracle):
+    """advanced at configs[3]'s size (M = 2^21 network) vs the reference's aggregate."""
+    c = R.cfg_case("purchase100_sparse_n300")
+    g, st = oracle.advanced(c["k"], R.records(c), c["d"], c["n"])
+    assert st == 0
+    R.assert_reassociated(g, c)
