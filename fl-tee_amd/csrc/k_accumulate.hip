@@ -114,6 +114,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
 }
 
+// One lane per output index (8-B loads): twice the waves of dense_accumulate_w (796 at
+// MLP-MNIST), 2 VGPRs per client in flight, so two waves fit a SIMD.  Same adds, same
+// order: bit-identical.  A/B variant 47.
+template <int U, bool ACC>
+__global__ __launch_bounds__(64) void dense_accumulate_w1(const uint2 *__restrict__ rec, size_t d,
+                                                          uint32_t n, float coef,
+                                                          float *__restrict__ out, uint32_t *status) {
+    const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (j >= d) return;
+    const uint2 *p = rec + j;
+    const uint32_t jx = (uint32_t)j;
+    float a = 0.0f;
+    uint32_t bad = 0;
+    for (uint32_t c = 0; c < n; c += U) {
+        uint2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t cc = c + (uint32_t)u < n ? c + (uint32_t)u : n - 1;
+            x[u] = ld_nt(p + (size_t)cc * d);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool take = c + (uint32_t)u < n;
+            const float s = __fadd_rn(a, __uint_as_float(x[u].y));
+            a = take ? s : a;
+            bad |= take ? (x[u].x ^ jx) : 0u;
+        }
+    }
+    out[j] = ACC ? __fadd_rn(out[j], a) : __fmul_rn(a, coef);
+    if (bad) atomicOr(status, FLTEE_DEV_ERR_DENSE_ORDER);
+}
+
 // The same output pairs with the clients split over W waves of one block (wave w: clients
 // [w*UC, (w+1)*UC)): every wave issues its UC rows' loads at once, so W times the waves
 // (and SIMDs) pull the batch; the in-order sum then passes from wave to wave through LDS —
@@ -558,6 +590,20 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
                 else
                     hipLaunchKernelGGL((dense_accumulate_wk<3, 34, ACC>), dim3(blocks), dim3(192), 0, s,
                                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
+        // 47 / 48: dense_accumulate_w1, one lane per index, 100 / 50 clients in flight
+        case 47: case 48:
+            if (!CLIP && ((uintptr_t)rec % 8 == 0)) {
+                const unsigned blocks = (unsigned)((d + 63) / 64);
+                if (g_dense_variant == 47)
+                    hipLaunchKernelGGL((dense_accumulate_w1<100, ACC>), dim3(blocks), dim3(64), 0, s,
+                                       (const uint2 *)rec, d, (uint32_t)n, coef, out, status);
+                else
+                    hipLaunchKernelGGL((dense_accumulate_w1<50, ACC>), dim3(blocks), dim3(64), 0, s,
+                                       (const uint2 *)rec, d, (uint32_t)n, coef, out, status);
                 break;
             }
             launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);

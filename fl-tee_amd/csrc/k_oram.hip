@@ -15,7 +15,9 @@
 // previous access's path write; lane j holds pool entries j and 64 + j).  Its LDS holds
 // the position map (u16 leaves, N <= 2^16 blocks) and the stash; the tree of 4 (2N - 1)
 // 16-B slots (idx, leaf, f32 value) lives in HBM.  Obliviousness, as the enclave's (ZeroTrace-style) ORAM has it:
-//  * the HBM trace of an access is one whole path, root to a uniformly random leaf;
+//  * the HBM trace of an access is one whole path, root to a uniformly random leaf,
+//    written; read, the part of it below the buckets it shares with the previous
+//    access's path (a function of the two public random leaves);
 //  * the position map is read and written at one address per access by every lane of
 //    the wave at once (an LDS broadcast: no bank conflict, the same time for any
 //    address) — it never leaves the workgroup;
@@ -104,11 +106,13 @@ __device__ __forceinline__ void oram_load_path(const uint4 *tree, uint32_t x, ui
 // (the top levels: l <= Lh - bitlen(x ^ x')) are then taken from this access's output,
 // which lives in the same lanes (slot l*Z + z of either path), the others from the loads.
 // A lane only ever stores and reloads its own slots, so program order orders them.
-// The eviction's gather: per level, the ranks of the blocks that may go there come from
-// one ballot; the z-th one's pool index is selected into the lane of slot l*Z + z (SALU
-// + one compare and select), the stash slots likewise, and every lane then fetches its new content
-// from that pool entry with ds_bpermute (a register crossbar: no LDS bank, so the same
-// time for any pattern).
+// The eviction: every block's rank by (deepest legal level, pool index) from one ballot
+// pair per level (mbcnt), the rank each slot receives from the per-level counts (uniform),
+// the pool entry holding that rank by matching its 7 bits against one ballot per bit;
+// every lane then fetches its new content from that pool entry with ds_bpermute (a
+// register crossbar: no LDS bank, so the same time for any pattern).  All lane-parallel
+// selects over fixed ballots: no per-slot scalar search (round 4: 1,810 SALU per access
+// before, `profiles/r04/oram_sq.txt`).
 __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__ rec,
                                                        uint32_t nrec, uint32_t Lh,
                                                        uint4 *__restrict__ tree, uint32_t k0,
@@ -166,7 +170,13 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         const uint32_t an = rb[(q + 1) & 63u].x & mask;
         const uint32_t xn = more ? (uint32_t)pm[an] : x;
         OramLane nxt = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
-        if (more) oram_load_path(tree, xn, Lh, lane, p0, p1, nxt);
+        // the buckets the two paths share (levels <= top) come from this access's output:
+        // only the rest is loaded (which levels is a function of the two public leaves).
+        // Those shared ones are also the slots the previous access's stores may still be
+        // writing, which a load would wait behind.
+        const uint32_t top = Lh - (32u - (uint32_t)__clz((int)(x ^ xn)));  // deepest shared level
+        const bool sh0 = lev0 <= top, sh1 = lev1 <= top;
+        if (more) oram_load_path(tree, xn, Lh, lane, p0 && !sh0, p1 && !sh1, nxt);
         // the pool: this path (registers) and the stash (LDS)
         uint32_t a0 = cur.a0, l0 = cur.l0, w0 = cur.w0, a1 = cur.a1, l1 = cur.l1, w1 = cur.w1;
         if (!p0) {
@@ -191,34 +201,74 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         const bool i0 = fi == lane, i1 = fi == 64u + lane;
         a0 = i0 ? a : a0, l0 = i0 ? nleaf : l0, w0 = i0 ? __float_as_uint(nv) : w0;
         a1 = i1 ? a : a1, l1 = i1 ? nleaf : l1, w1 = i1 ? __float_as_uint(nv) : w1;
-        // eviction: the deepest level each block may take on this path, four per bucket;
-        // src0 / src1: the pool entry each slot (lane, 64 + lane) receives, 0xFF = empty
+        // eviction: the deepest level each block may take on this path (lm), four per
+        // bucket, deepest first.  The blocks ranked by (lm descending, pool index): level
+        // l then takes the next min(4, #(lm >= l) - placed) ranks, the stash the rest —
+        // the greedy's count at every level, whichever blocks it picks, so the same
+        // stash size as any deepest-first eviction.
         const bool o0 = v0 && a0 != kOramEmpty, o1 = v1 && a1 != kOramEmpty;
         const uint32_t lm0 = Lh - (32u - (uint32_t)__clz((int)(l0 ^ x)));
         const uint32_t lm1 = Lh - (32u - (uint32_t)__clz((int)(l1 ^ x)));
-        uint64_t left0 = __ballot(o0), left1 = __ballot(o1);  // not placed yet
-        uint32_t src0 = 0xFFu, src1 = 0xFFu;
+        uint32_t rank0 = 0, rank1 = 0;  // this lane's blocks' ranks
+        uint32_t rw0, rw1;              // the rank this lane's slots receive
+        bool fill0, fill1;
+        uint32_t tfirst = 0, tcount = 0;  // lane l: level l's first rank and count
+        uint32_t before = 0, placed = 0;  // blocks with lm > l; ranks handed out so far
         for (int l = (int)Lh; l >= 0; --l) {
-            uint64_t e0 = __ballot(lm0 >= (uint32_t)l) & left0, e1 = __ballot(lm1 >= (uint32_t)l) & left1;
-            const uint64_t b0 = e0, b1 = e1;
+            const bool e0 = o0 && lm0 == (uint32_t)l, e1 = o1 && lm1 == (uint32_t)l;
+            const uint64_t mv0 = __ballot(e0), mv1 = __ballot(e1);
+            const uint32_t c0 = (uint32_t)__popcll(mv0);
+            const uint32_t below0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(mv0 >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mv0, 0u));
+            const uint32_t below1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(mv1 >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mv1, 0u));
+            rank0 = e0 ? before + below0 : rank0;
+            rank1 = e1 ? before + c0 + below1 : rank1;
+            before += c0 + (uint32_t)__popcll(mv1);
+            const uint32_t pl = min(kOramZ, before - placed);
+            // level l's first rank and count, kept in lane l
+            tfirst = lane == (uint32_t)l ? placed : tfirst;
+            tcount = lane == (uint32_t)l ? pl : tcount;
+            placed += pl;
+        }
+        // slot l*Z + z (lane-static l, z) takes rank first(l) + z when z < count(l): the
+        // level's pair fetched from lane l (a lane-static crossbar read)
+        {
+            const uint32_t f0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lev0 & 63u) * 4u), (int)tfirst);
+            const uint32_t n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lev0 & 63u) * 4u), (int)tcount);
+            const uint32_t f1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lev1 & 63u) * 4u), (int)tfirst);
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lev1 & 63u) * 4u), (int)tcount);
+            rw0 = f0 + (lane & 3u);
+            rw1 = f1 + (lane & 3u);
+            fill0 = p0 && (lane & 3u) < n0;
+            fill1 = p1 && (lane & 3u) < n1;
+        }
+        // the rest to the stash, by rank
+        const uint32_t nst = before - placed;
+        over |= nst > kOramStash;
+        rw0 = (!p0 && v0) ? placed + s0i : rw0;
+        rw1 = (!p1 && v1) ? placed + s1i : rw1;
+        fill0 = (!p0 && v0) ? s0i < nst : fill0;
+        fill1 = (!p1 && v1) ? s1i < nst : fill1;
+        // src0 / src1: the pool entry holding the wanted rank (0xFF = empty slot), by
+        // matching the rank's bits against one ballot per bit (uniform masks, selects)
+        uint64_t m00 = __ballot(o0), m01 = __ballot(o1);
+        uint64_t m10 = m00, m11 = m01;
 #pragma unroll
-            for (uint32_t z = 0; z < kOramZ; ++z) {
-                const uint32_t si = take_lowest(e0, e1);
-                const uint32_t s = (uint32_t)l * kOramZ + z;
-                src0 = lane == s ? si : src0;
-                src1 = lane + 64 == s ? si : src1;
-            }
-            left0 &= ~(b0 & ~e0);  // the (up to) four taken at this level
-            left1 &= ~(b1 & ~e1);
+        for (uint32_t b = 0; b < 7; ++b) {
+            const uint64_t B0 = __ballot(o0 && ((rank0 >> b) & 1u)), B1 = __ballot(o1 && ((rank1 >> b) & 1u));
+            const bool q0 = (rw0 >> b) & 1u, q1 = (rw1 >> b) & 1u;
+            m00 &= q0 ? B0 : ~B0;
+            m01 &= q0 ? B1 : ~B1;
+            m10 &= q1 ? B0 : ~B0;
+            m11 &= q1 ? B1 : ~B1;
         }
-        // what stays goes to the stash, in pool order
-        over |= (uint32_t)(__popcll(left0) + __popcll(left1)) > kOramStash;
-        for (uint32_t z = 0; z < kOramStash; ++z) {
-            const uint32_t si = take_lowest(left0, left1);
-            const uint32_t s = P + z;
-            src0 = lane == s ? si : src0;
-            src1 = lane + 64 == s ? si : src1;
-        }
+        const uint32_t src0 = !fill0 ? 0xFFu
+                                     : (m00 ? (uint32_t)__builtin_ffsll((long long)m00) - 1u
+                                            : 63u + (uint32_t)__builtin_ffsll((long long)m01));
+        const uint32_t src1 = !fill1 ? 0xFFu
+                                     : (m10 ? (uint32_t)__builtin_ffsll((long long)m10) - 1u
+                                            : 63u + (uint32_t)__builtin_ffsll((long long)m11));
         // gather through the register crossbar: from set 0 or set 1 of lane src & 63
         const int ad0 = (int)((src0 & 63u) * 4u), ad1 = (int)((src1 & 63u) * 4u);
         const bool h0 = src0 != 0xFFu, h1 = src1 != 0xFFu, hi0 = src0 >= 64u, hi1 = src1 >= 64u;
@@ -241,8 +291,6 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         // the next access's path: the shared top levels from this output, the rest loaded
         // (merged before this access's stores are issued: the wait for the loads then does
         // not also wait for these stores — CDNA counts both in vmcnt, in order)
-        const uint32_t top = Lh - (32u - (uint32_t)__clz((int)(x ^ xn)));  // deepest shared level
-        const bool sh0 = lev0 <= top, sh1 = lev1 <= top;
         OramLane nc;
         nc.a0 = sh0 ? ga0 : nxt.a0, nc.l0 = sh0 ? gl0 : nxt.l0, nc.w0 = sh0 ? gw0 : nxt.w0;
         nc.a1 = sh1 ? ga1 : nxt.a1, nc.l1 = sh1 ? gl1 : nxt.l1, nc.w1 = sh1 ? gw1 : nxt.w1;
