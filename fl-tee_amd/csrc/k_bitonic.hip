@@ -84,6 +84,14 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_WAVE_LOCAL
 #define FLTEE_WAVE_LOCAL 1
 #endif
+//   FLTEE_WAVE_SPLIT  the first pass's stages above log2(64 E): the steps that cross waves
+//   block-wide, then the stage's steps inside a wave's records wave-local (1: always;
+//   2: only where the split adds no LDS round; 0: the whole stage block-wide).  A/B
+//   (`profiles/r04/ab/ab6_wave_split.jsonl`): 2 takes C4's first pass 1,085 -> 1,065 us and
+//   C5's 1,234 -> 1,227 us; 1 is slower than 0 (the extra rounds cost more than the barriers)
+#ifndef FLTEE_WAVE_SPLIT
+#define FLTEE_WAVE_SPLIT 2
+#endif
 
 namespace fltee {
 
@@ -448,6 +456,28 @@ __device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32
 // of the first round (a block barrier, or the wave's own order when WAVE_FIRST).
 template <int E>
 constexpr int kWaveLog = E >= 32 ? 11 : (E >= 16 ? 10 : (E >= 8 ? 9 : (E >= 4 ? 8 : 7)));
+// Steps IL-1 .. JBOT of stage IL (> log2(64 E) with FLTEE_WAVE_SPLIT): the steps of
+// distance >= 64 E cross waves and run block-wide; the rest stay inside each wave's 64 E
+// consecutive records and run as wave-local rounds (no block barrier: the waves drift and
+// overlap one another's LDS traffic with their compare-exchanges), then one block barrier.
+// The same steps in the same order: the network is unchanged.  Ends in a block barrier.
+template <int MODE, int E, int NT, int IL, int JBOT>
+__device__ __forceinline__ void stage_steps_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
+    constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
+    constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
+    constexpr int r_all = (IL - JBOT + rmax - 1) / rmax;
+    constexpr int r_split = WB ? (IL - WB + rmax - 1) / rmax + (WB - JBOT + rmax - 1) / rmax : 0;
+    constexpr bool split = WB != 0 && FLTEE_WAVE_SPLIT != 0 && IL > WB && JBOT < WB &&
+                           (FLTEE_WAVE_SPLIT == 1 || r_split <= r_all);
+    if constexpr (split) {
+        lds_steps_ct<MODE, E, NT, IL - 1, WB>(sm, base, (uint32_t)IL, seed);
+        lds_steps_ct<MODE, E, NT, WB - 1, JBOT, 0, WB>(sm, base, (uint32_t)IL, seed);
+        __syncthreads();
+    } else {
+        lds_steps_ct<MODE, E, NT, IL - 1, JBOT>(sm, base, (uint32_t)IL, seed);
+    }
+}
+
 template <int MODE, int E, int NT, int IL, int TL, int RL>
 __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
     constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
@@ -456,14 +486,14 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
             lds_steps_ct<MODE, E, NT, IL - 1, 0, 0, WB>(sm, base, (uint32_t)IL, seed);
             if constexpr (IL == WB) __syncthreads();  // the next stage crosses waves
         } else {
-            lds_steps_ct<MODE, E, NT, IL - 1, 0>(sm, base, (uint32_t)IL, seed);
+            stage_steps_ct<MODE, E, NT, IL, 0>(sm, base, seed);
         }
         sort_stages_ct<MODE, E, NT, IL + 1, TL, RL>(sm, base, seed);
     } else {
         // stage TL runs block-wide rounds: if the stage before it was wave-local and did
         // not end in a block barrier (TL <= WB), order the waves here
         if constexpr (WB && TL <= WB) __syncthreads();
-        lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base, (uint32_t)TL, seed);
+        stage_steps_ct<MODE, E, NT, TL, RL>(sm, base, seed);
     }
 }
 
