@@ -46,13 +46,17 @@ __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint3
 }
 
 typedef unsigned int cp_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int cp_u32x4 __attribute__((ext_vector_type(4)));
 
 // FIRST: src holds folded records (idx, val); else (c, val).
 // FINAL: 0 = write (c, val) records, 1 = out[i] = val*coef, 2 = out[i] += val.
 // Persistent: block b walks tiles b, b + grid, ...; the next tile's records are
 // prefetched into registers (raw buffer loads, out-of-range lanes selected to the
 // dummy afterwards: no per-load branch) while the current tile runs its levels.
-template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1>
+// V2 (rows of W >= 2 residues, L even): a lane loads and stores two adjacent slots of a
+// row (16 B; 8-B accesses run at about half the 16-B rate, MI355X_MICROARCH.md); the
+// levels keep the one-slot-per-lane assignment.
+template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1, bool V2 = false>
 __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restrict__ src,
                                                    uint64_t *__restrict__ dst, uint32_t L,
                                                    uint32_t d, uint32_t j0, uint32_t G,
@@ -79,28 +83,44 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         const uint32_t band = tl / ngroups, grp = tl - band * ngroups;
         return ((uint64_t)(band * S + (f >> logW)) << j0) + (grp << logW) + (f & (W - 1));
     };
+    static_assert(!V2 || (!FIRST && PER % 2 == 0), "V2: strided passes, slot pairs");
+    // the tile slot of prefetch register i: tid + i NT, or with V2 slot pair tid + (i/2) NT
+    auto slot = [&](uint32_t i) -> uint32_t {
+        return V2 ? 2u * (tid() + (i >> 1) * NT) + (i & 1u) : tid() + i * NT;
+    };
     uint64_t pf[PER];
     // the loads only: the dummy for slots past L is selected when the tile lands (a use of
     // the loaded value here would make the compiler wait for the prefetch right away)
     auto prefetch = [&](uint32_t tl) {
+        if constexpr (V2) {
 #pragma unroll
-        for (uint32_t i = 0; i < PER; ++i) {
-            const uint64_t p = pos_of(tl, tid() + i * NT);
-            const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
-                rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
-            pf[i] = ((uint64_t)x.y << 32) | x.x;
+            for (uint32_t i = 0; i < PER; i += 2) {
+                const uint64_t p = pos_of(tl, slot(i));  // even (W even), and p + 1 < L with p
+                const cp_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
+                    rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
+                pf[i] = ((uint64_t)x.y << 32) | x.x;
+                pf[i + 1] = ((uint64_t)x.w << 32) | x.z;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < PER; ++i) {
+                const uint64_t p = pos_of(tl, tid() + i * NT);
+                const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
+                    rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
+                pf[i] = ((uint64_t)x.y << 32) | x.x;
+            }
         }
     };
     prefetch(tile);
     for (;;) {
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
-            uint64_t v = pos_of(tile, tid() + i * NT) < L ? pf[i] : CP_DUMMY;
+            uint64_t v = pos_of(tile, slot(i)) < L ? pf[i] : CP_DUMMY;
             if (FIRST) {  // key -> shift c = p - idx (u32::MAX when not selected)
                 const uint32_t p = (uint32_t)pos_of(tile, tid() + i * NT), idx = (uint32_t)v;
                 v = (v & 0xFFFFFFFF00000000ull) | (idx < d ? (uint64_t)(p - idx) : CP_DUMMY);
             }
-            sm[tid() + i * NT] = v;
+            sm[slot(i)] = v;
         }
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
@@ -143,6 +163,26 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             g += two ? 2 : 1;
         }
         const uint32_t nout = S << logW;
+        if constexpr (V2 && FINAL == 0) {
+            // slot pairs as 16-B stores (p even; nout and L even)
+            const __amdgpu_buffer_rsrc_t ds =
+                __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)(L * 8u), 0x00020000);
+#pragma unroll
+            for (uint32_t i = 0; i < PER; i += 2) {
+                const uint32_t f = slot(i);
+                if (f < nout) {
+                    const uint64_t p = pos_of(tile, f);
+                    const uint64_t a = sm[f], b = sm[f + 1];
+                    const cp_u32x4 x = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+                    // p >= L: past the buffer's range, the store is dropped (no branch)
+                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_raw_buffer_store_b128(x, ds, (int)(p < L ? (uint32_t)p * 8u : L * 8u), 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_nop 1" ::: "memory");  // dwordx4 store data hazard (k_bitonic.hip)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else {
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
             const uint32_t f = tid() + i * NT;
@@ -155,6 +195,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
                     out[p] = FINAL == 2 ? __fadd_rn(out[p], v) : __fmul_rn(v, coef);
                 }
             }
+        }
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
@@ -183,18 +224,26 @@ constexpr int kCompactFirstBlocks = FLTEE_COMPACT_FIRST_BLOCKS;
 static int g_compact_variant = 1;
 void set_compact_variant(int v) { g_compact_variant = v; }
 
+#ifndef FLTEE_COMPACT_V2
+#define FLTEE_COMPACT_V2 1
+#endif
 template <int NT, int PER, int MINB = 1>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
                               uint64_t *dst, uint32_t L, uint32_t d, uint32_t j0, uint32_t G,
                               uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
                               float coef, float *out, uint32_t ntiles) {
-#define CP_GO(F, X)                                                                              \
-    hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB>), dim3(grid), dim3(NT), 0, s, src, dst, L, d, \
-                       j0, G, logW, S, rows, ngroups, coef, out, ntiles)
+#define CP_GO(F, X, V)                                                                           \
+    hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
+                       d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
+    // 16-B slot pairs: rows of >= 2 residues, L even, both buffers 16-B aligned
+    const bool v2 = FLTEE_COMPACT_V2 && !first && logW >= 1 && L % 2 == 0 &&
+                    (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
     if (first) {
-        if (fin == 0) CP_GO(true, 0); else if (fin == 1) CP_GO(true, 1); else CP_GO(true, 2);
+        if (fin == 0) CP_GO(true, 0, false); else if (fin == 1) CP_GO(true, 1, false); else CP_GO(true, 2, false);
+    } else if (v2) {
+        if (fin == 0) CP_GO(false, 0, true); else if (fin == 1) CP_GO(false, 1, true); else CP_GO(false, 2, true);
     } else {
-        if (fin == 0) CP_GO(false, 0); else if (fin == 1) CP_GO(false, 1); else CP_GO(false, 2);
+        if (fin == 0) CP_GO(false, 0, false); else if (fin == 1) CP_GO(false, 1, false); else CP_GO(false, 2, false);
     }
 #undef CP_GO
     return hipGetLastError();
