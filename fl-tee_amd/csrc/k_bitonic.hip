@@ -92,6 +92,11 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_WAVE_SPLIT
 #define FLTEE_WAVE_SPLIT 2
 #endif
+//   FLTEE_TILE_PAIRS  the compile-time-shaped tile passes load and store slot pairs (16 B
+//   per lane: lane t holds tile elements 2t, 2t + 1 (+ 2 NT r)) instead of single records
+#ifndef FLTEE_TILE_PAIRS
+#define FLTEE_TILE_PAIRS 1
+#endif
 
 namespace fltee {
 
@@ -288,6 +293,28 @@ template <bool SW>
 __device__ __forceinline__ void tl_store(__amdgpu_buffer_rsrc_t rs, uint32_t vl, uint32_t u, uint64_t v) {
     if constexpr (SW) bt_store<kTileCP>(rs, vl ^ (phys(u) * 8u), 0u, v);
     else bt_store<kTileCP>(rs, vl, u * 8u, v);
+}
+
+// Two adjacent records (16 B, the lane part even): the tile passes' slot pairs.  Stores
+// fenced with s_nop 1 (the dwordx4 store data hazard, see bitonic_merge_direct).
+template <bool SW>
+__device__ __forceinline__ void tl_load2(__amdgpu_buffer_rsrc_t rs, uint32_t vl, uint32_t u, uint64_t &a,
+                                         uint64_t &b) {
+    const uint32_t off = SW ? (vl ^ (phys(u) * 8u)) : vl;
+    const bt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, SW ? 0 : (int)(u * 8u), kTileCP);
+    a = ((uint64_t)x.y << 32) | x.x;
+    b = ((uint64_t)x.w << 32) | x.z;
+}
+template <bool SW>
+__device__ __forceinline__ void tl_store2(__amdgpu_buffer_rsrc_t rs, uint32_t vl, uint32_t u, uint64_t a,
+                                          uint64_t b) {
+    const uint32_t off = SW ? (vl ^ (phys(u) * 8u)) : vl;
+    const bt_u32x4 x = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)off, SW ? 0 : (int)(u * 8u), kTileCP);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // ------------------------------------------------------------- LDS tile ----
@@ -522,40 +549,64 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     // SW (static_assert: middle passes only, read and written in the swizzled layout):
     // the lane part swizzled once, each record's uniform part (tile base + row) per access
     static_assert(!SW || !SORT, "the first pass is bitonic_sort_direct");
-    const uint32_t lpos = tile_pos(0u, threadIdx.x, wlog, dtile);
+    // P2: lane t holds the slot pairs 2t, 2t + 1 (+ 2 NT r) — adjacent positions (the
+    // compile-time shapes have W >= 2; SW keeps bits 0..3), one 16-B load and store each
+    constexpr bool P2 = FLTEE_TILE_PAIRS && !SORT && TL != 0;
+    constexpr uint32_t LS = P2 ? 2u : 1u;  // records per load
+    auto elem = [](int r) -> uint32_t {     // the tile element held in pf[r]
+        return P2 ? 2u * threadIdx.x + (uint32_t)(r & 1) + (uint32_t)(r >> 1) * (2u * NT)
+                  : threadIdx.x + (uint32_t)r * NT;
+    };
+    const uint32_t lpos = tile_pos(0u, LS * threadIdx.x, wlog, dtile);
     const uint32_t voff = (SW ? phys(lpos) : lpos) * 8u;          // per-lane bytes
-    const uint32_t rrow = (uint32_t)NT << (dtile - wlog);         // records, uniform
+    const uint32_t rrow = (LS * (uint32_t)NT) << (dtile - wlog);  // records per load row, uniform
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t pf[E];
-    {
-        const uint32_t sb = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
+    auto load_tile = [&](uint32_t sb) {
+        if constexpr (P2) {
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
-    }
+            for (int r = 0; r < E; r += 2) tl_load2<SW>(rs, voff, sb + (uint32_t)(r >> 1) * rrow, pf[r], pf[r + 1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
+        }
+    };
+    load_tile(tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile));
     constexpr int R1 = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     // a strided tile with no fused tail (seg0 == 0) starts with the stage's top row steps:
-    // element t + r * NT of lane t differs from its other records in the top log2(E) row
-    // bits only, so that first round runs on the prefetch registers before they go to LDS
-    // (one LDS write + read of the tile less, as in bitonic_merge_direct)
-    constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && (TL - R1) >= WL;
+    // the records of lane t (one parity class with P2) differ in the top log2(E) (P2:
+    // log2(E) - 1) row bits only, so that first round runs on the prefetch registers
+    // before they go to LDS (one LDS write + read of the tile less, as in
+    // bitonic_merge_direct)
+    constexpr int RH = P2 ? R1 - 1 : R1;  // the head round's steps
+    constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && RH >= 1 && (TL - RH) >= WL;
     for (;;) {
         const uint32_t base = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
         const bool head_reg = kHeadReg && seg0 == 0;
         if constexpr (kHeadReg) {
-            if (head_reg)
-                group_steps<MODE, R1>(pf, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
-                                      (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
+            if (head_reg) {
+                if constexpr (P2) {
+                    uint64_t g0[E / 2], g1[E / 2];
+#pragma unroll
+                    for (int k = 0; k < E / 2; ++k) g0[k] = pf[2 * k], g1[k] = pf[2 * k + 1];
+                    const uint32_t p0 = tile_pos(base, 2u * threadIdx.x, (uint32_t)WL, dtile) + pbase;
+                    group_steps<MODE, RH>(g0, p0, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
+                    group_steps<MODE, RH>(g1, p0 + 1u, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
+#pragma unroll
+                    for (int k = 0; k < E / 2; ++k) pf[2 * k] = g0[k], pf[2 * k + 1] = g1[k];
+                } else {
+                    group_steps<MODE, R1>(pf, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
+                                          (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
+                }
+            }
         }
 #pragma unroll
-        for (int r = 0; r < E; ++r) sm[lpad(threadIdx.x + r * NT)] = pf[r];
+        for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
         auto prefetch = [&]() {
-            const uint32_t sb = tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog,
-                                          wlog, dtile);
-#pragma unroll
-            for (int r = 0; r < E; ++r) pf[r] = tl_load<SW>(rs, voff, sb + (uint32_t)r * rrow);
+            load_tile(tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog, wlog, dtile));
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
         // registers are then not live through the tail)
@@ -591,7 +642,7 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
             } else if constexpr (TL != 0) {  // strided, tlog == TL and wlog == WL (launcher)
                 if constexpr (kHeadReg) {
                     if (head_reg)
-                        lds_steps_ct<MODE, E, NT, TL - R1 - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
+                        lds_steps_ct<MODE, E, NT, TL - RH - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
                     else
                         lds_steps_ct<MODE, E, NT, TL - 1, WL, WL>(sm, base + pbase, ilog, seed, dtile);
                 } else {
@@ -602,9 +653,16 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                                        wlog < tlog ? (int)wlog : 0, seed);
             }
         }
+        if constexpr (P2) {
 #pragma unroll
-        for (int r = 0; r < E; ++r)
-            tl_store<SW>(rs, voff, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
+            for (int r = 0; r < E; r += 2)
+                tl_store2<SW>(rs, voff, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[lpad(elem(r))]),
+                              lds_ld(&sm[lpad(elem(r + 1))]));
+        } else {
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                tl_store<SW>(rs, voff, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
+        }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
         tile = next;
