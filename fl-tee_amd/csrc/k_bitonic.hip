@@ -97,6 +97,20 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_TILE_PAIRS
 #define FLTEE_TILE_PAIRS 1
 #endif
+//   FLTEE_MERGE_PAIRS  the same for the contiguous direct merges (bitonic_merge_direct):
+//   1 all, 2 the selecting last pass of nips19's shuffle only, 0 none.  A/B
+//   (`profiles/r04/ab/ab9_merge_pairs_*.jsonl`): the selecting pass 552 -> 517 us, the
+//   plain merges 251 -> 279 us (C4) / 335 -> 364 us (C5) — their last round then stores
+//   groups of 8 instead of 4
+#ifndef FLTEE_MERGE_PAIRS
+#define FLTEE_MERGE_PAIRS 2
+#endif
+//   FLTEE_SEL_STORE_OOB  the selecting pass stores every record, the unselected ones out of
+//   the tile's buffer range (dropped), instead of a branch per record (A/B: 530 vs 520 us,
+//   not kept; `profiles/r04/ab/ab10_sel_store_oob_c4.jsonl`)
+#ifndef FLTEE_SEL_STORE_OOB
+#define FLTEE_SEL_STORE_OOB 0
+#endif
 
 namespace fltee {
 
@@ -708,38 +722,57 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
     // rows at stride 2^dtile (W <= NT), as in bitonic_tiles
     static_assert(!(STRIDED && (SWI || SWO)), "swizzled layout: contiguous merges only");
     static_assert(!(SEL && SWO), "the selection is written in position order");
-    const uint32_t lpos = tile_pos(0u, t, wlog, dtile);
+    // P2 (contiguous, compile-time shape): lane t loads the slot pairs 2t, 2t + 1 (+ 2 NT r),
+    // 16 B each; the head round in registers then covers the top R1 - 1 steps per parity
+    // class and the last round takes one step more (RL + 1): the same LDS rounds
+    constexpr bool P2 = (FLTEE_MERGE_PAIRS == 1 || (FLTEE_MERGE_PAIRS == 2 && SEL)) && TL != 0 && !STRIDED && RL < R1;
+    constexpr int RH = P2 ? R1 - 1 : R1;  // head round (registers)
+    constexpr int RT = P2 ? RL + 1 : RL;  // last round (registers)
+    auto elem = [&](int r) -> uint32_t {  // the tile element held in pf[r]
+        return P2 ? 2u * t + (uint32_t)(r & 1) + (uint32_t)(r >> 1) * (2u * NT) : t + (uint32_t)r * NT;
+    };
+    const uint32_t lpos = tile_pos(0u, (P2 ? 2u : 1u) * t, wlog, dtile);
     const uint32_t voff = (SWI ? phys(lpos) : lpos) * 8u;
-    const uint32_t rrow = (uint32_t)NT << (dtile - wlog);  // records
+    const uint32_t rrow = ((P2 ? 2u : 1u) * (uint32_t)NT) << (dtile - wlog);  // records per load row
     const uint32_t dlog1 = tlog - (uint32_t)R1;  // == log2 NT: the first round's tile-local distance
     const uint32_t dlog1_g = STRIDED ? dlog1 - wlog + dtile : dlog1;
     const uint32_t jbot = STRIDED ? wlog : 0u;  // the tile's lowest step
     uint64_t pf[E];
-    {
-        const uint32_t sb = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
+    auto load_tile = [&](uint32_t sb) {
+        if constexpr (P2) {
 #pragma unroll
-        for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
-    }
-    for (;;) {
-        const uint32_t ptile = past_hole(tile, hole_at, hole_len);
-        const uint32_t base = tile_base(ptile, tlog, wlog, dtile);
-        group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
-#pragma unroll
-        for (int r = 0; r < E; ++r) sm[lpad(t + r * NT)] = pf[r];
-        __syncthreads();
-        const uint32_t next = tile + gridDim.x;
-        {
-            const uint32_t sb = tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog,
-                                          wlog, dtile);
+            for (int r = 0; r < E; r += 2) tl_load2<SWI>(rs, voff, sb + (uint32_t)(r >> 1) * rrow, pf[r], pf[r + 1]);
+        } else {
 #pragma unroll
             for (int r = 0; r < E; ++r) pf[r] = tl_load<SWI>(rs, voff, sb + (uint32_t)r * rrow);
         }
+    };
+    load_tile(tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile));
+    for (;;) {
+        const uint32_t ptile = past_hole(tile, hole_at, hole_len);
+        const uint32_t base = tile_base(ptile, tlog, wlog, dtile);
+        if constexpr (P2) {
+            uint64_t g0[E / 2], g1[E / 2];
+#pragma unroll
+            for (int k = 0; k < E / 2; ++k) g0[k] = pf[2 * k], g1[k] = pf[2 * k + 1];
+            group_steps<MODE, RH>(g0, base + 2u * t + pbase, dlog1_g + 1u, ilog, seed);
+            group_steps<MODE, RH>(g1, base + 2u * t + 1u + pbase, dlog1_g + 1u, ilog, seed);
+#pragma unroll
+            for (int k = 0; k < E / 2; ++k) pf[2 * k] = g0[k], pf[2 * k + 1] = g1[k];
+        } else {
+            group_steps<MODE, R1>(pf, tile_pos(base, t, wlog, dtile) + pbase, dlog1_g, ilog, seed);
+        }
+#pragma unroll
+        for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
+        __syncthreads();
+        const uint32_t next = tile + gridDim.x;
+        load_tile(tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog, wlog, dtile));
         if constexpr (TL != 0 && !STRIDED)  // tlog == TL (checked by the launcher)
-            lds_steps_ct<MODE, E, NT, TL - R1 - 1, RL>(sm, base + pbase, ilog, seed);
+            lds_steps_ct<MODE, E, NT, TL - 1 - RH, RT>(sm, base + pbase, ilog, seed);
         else
             lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, ilog, (int)dlog1 - 1,
                                    (int)(jbot + RL), seed);
-        constexpr int G = E >> RL;
+        constexpr int G = E >> RT;
         if constexpr (SEL && !STRIDED) {
             uint64_t v[E];
             const uint64_t *own = sm + lpad(t * (uint32_t)E);  // E >= 16: lpad splits
@@ -748,8 +781,8 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
             uint32_t c = 0;
 #pragma unroll
             for (int h = 0; h < G; ++h) {
-                uint64_t (&g)[1 << RL] = *reinterpret_cast<uint64_t (*)[1 << RL]>(&v[h << RL]);
-                group_steps<MODE, RL>(g, base + pbase + t * (uint32_t)E + ((uint32_t)h << RL), 0u,
+                uint64_t (&g)[1 << RT] = *reinterpret_cast<uint64_t (*)[1 << RT]>(&v[h << RT]);
+                group_steps<MODE, RT>(g, base + pbase + t * (uint32_t)E + ((uint32_t)h << RT), 0u,
                                       ilog, seed);
             }
 #pragma unroll
@@ -771,6 +804,21 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                 pre += w < wv ? x : 0u;
                 tot += x;
             }
+#if FLTEE_SEL_STORE_OOB
+            // branch-free: every record is stored, the unselected ones at the first byte
+            // past the tile's own slot of a tile-sized buffer resource, where the store is
+            // dropped (no data-dependent branch, no per-record exec mask kept live)
+            const uint32_t tbytes = (1u << tlog) * 8u;
+            const __amdgpu_buffer_rsrc_t ts =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(data + base), (short)0, (int)tbytes, 0x00020000);
+            uint32_t o = pre + inc - c;  // tile-relative
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const bool sq = (uint32_t)v[q] < sel_d;
+                bt_store<kTileCP>(ts, sq ? o * 8u : tbytes, 0u, v[q]);
+                o += sq ? 1u : 0u;
+            }
+#else
             uint32_t o = base + pre + inc - c;
 #pragma unroll
             for (int q = 0; q < E; ++q) {
@@ -779,6 +827,7 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                     ++o;
                 }
             }
+#endif
             if (t == NT - 1) sel_cnt[ptile] = tot;
             if (next >= ntiles) break;
             __syncthreads();  // wtot and the last round's LDS reads retire
@@ -793,32 +842,32 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
         const uint32_t sxb = SWO ? swz_x(base) : 0u;
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += BW) {
-        uint64_t vv[BW][1 << RL];
+        uint64_t vv[BW][1 << RT];
         uint32_t bb[BW];
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            const uint32_t b = bb[h] = spread(lane_tid<NT>() + (uint32_t)(h0 + h) * NT, jbot, RL);
-            if (!STRIDED) {  // b = g << RL: lpad(b + q) = lpad(b) + q + (q >> 4)
+            const uint32_t b = bb[h] = spread(lane_tid<NT>() + (uint32_t)(h0 + h) * NT, jbot, RT);
+            if (!STRIDED) {  // b = g << RT: lpad(b + q) = lpad(b) + q + (q >> 4)
                 const uint64_t *row = sm + lpad(b);
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = lds_ld(&row[q + (q >> 4)]);
+                for (int q = 0; q < (1 << RT); ++q) vv[h][q] = lds_ld(&row[q + (q >> 4)]);
             } else {
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) vv[h][q] = lds_ld(&sm[lpad(b + ((uint32_t)q << jbot))]);
+                for (int q = 0; q < (1 << RT); ++q) vv[h][q] = lds_ld(&sm[lpad(b + ((uint32_t)q << jbot))]);
             }
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
             const uint32_t pb = tile_pos(0u, bb[h], wlog, dtile);  // tile-relative position of v[0]
-            group_steps<MODE, RL>(vv[h], base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
+            group_steps<MODE, RT>(vv[h], base + pbase + pb, STRIDED ? dtile : 0u, ilog, seed);
         }
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
-            uint64_t (&v)[1 << RL] = vv[h];
+            uint64_t (&v)[1 << RT] = vv[h];
             const uint32_t pb = tile_pos(0u, bb[h], wlog, dtile);
             if (STRIDED) {  // v[q] sits 2^dtile positions after v[q-1]: 8-B stores
 #pragma unroll
-                for (int q = 0; q < (1 << RL); ++q)
+                for (int q = 0; q < (1 << RT); ++q)
                     bt_store<kTileCP>(rs, (pb + ((uint32_t)q << dtile)) * 8u, base * 8u, v[q]);
             } else {
                 // 16-B stores.  hipcc (ROCm 7.2) may let the next group's VALU overwrite a
@@ -826,11 +875,11 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
                 // store has read them (measured: nondeterministic output); the explicit
                 // "s_nop 1" fenced by sched_barriers gives the two wait states the hazard needs
                 // (cdna_hip_programming.md §5.7: dwordx3/x4 stores end with s_nop 1).
-                // (pb is a multiple of 2^RL and sxb of 16: (pb ^ sxb) + q is the physical
+                // (pb is a multiple of 2^RT and sxb of 16: (pb ^ sxb) + q is the physical
                 // offset of record pb + q)
                 const uint32_t pbs = SWO ? (pb ^ sxb) : pb;
 #pragma unroll
-                for (int q = 0; q < (1 << RL); q += 2) {
+                for (int q = 0; q < (1 << RT); q += 2) {
                     const bt_u32x4 x = {(uint32_t)v[q], (uint32_t)(v[q] >> 32), (uint32_t)v[q + 1],
                                         (uint32_t)(v[q + 1] >> 32)};
                     __builtin_amdgcn_sched_barrier(0);
