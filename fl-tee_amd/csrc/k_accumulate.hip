@@ -64,7 +64,7 @@ static __device__ __forceinline__ uint4 ld4(const uint4 *p, bool nt) {
 // `profiles/r03/ab/ab17_dense_small_d.jsonl`): n = 100 9.2-9.5 us against 10.4-10.6 us for
 // the LDS-staged kernel below; n = 64 8.8 vs 9.1; n <= 32 and n > 100 no faster (those keep
 // the LDS kernel).
-template <int U, bool CLIP, bool ACC>
+template <int U, bool CLIP, bool ACC, bool NTL = true>
 __device__ __forceinline__ void dw_batch(const uint4 *__restrict__ p, size_t d2, uint32_t n, uint32_t c,
                                          bool clamp, uint32_t jx, const float *__restrict__ ccoef,
                                          float &a0, float &a1, uint32_t &bad) {
@@ -72,7 +72,7 @@ __device__ __forceinline__ void dw_batch(const uint4 *__restrict__ p, size_t d2,
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t cc = (clamp && c + (uint32_t)u >= n) ? n - 1 : c + (uint32_t)u;
-        x[u] = ld_nt(p + (size_t)cc * d2);
+        x[u] = NTL ? ld_nt(p + (size_t)cc * d2) : p[(size_t)cc * d2];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -90,7 +90,7 @@ __device__ __forceinline__ void dw_batch(const uint4 *__restrict__ p, size_t d2,
     }
 }
 
-template <int U, bool REM, bool CLIP, bool ACC>
+template <int U, bool REM, bool CLIP, bool ACC, bool NTL = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void dense_accumulate_w(
     const uint4 *__restrict__ rec, size_t d2, uint32_t n, float coef, float *__restrict__ out,
     const float *__restrict__ ccoef, uint32_t *status) {
@@ -100,8 +100,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const uint32_t jx = (uint32_t)(2 * j);
     float a0 = 0.0f, a1 = 0.0f;
     uint32_t bad = 0, c = 0;
-    for (; c + U <= n; c += U) dw_batch<U, CLIP, ACC>(p, d2, n, c, false, jx, ccoef, a0, a1, bad);
-    if (REM && c < n) dw_batch<U, CLIP, ACC>(p, d2, n, c, true, jx, ccoef, a0, a1, bad);
+    for (; c + U <= n; c += U) dw_batch<U, CLIP, ACC, NTL>(p, d2, n, c, false, jx, ccoef, a0, a1, bad);
+    if (REM && c < n) dw_batch<U, CLIP, ACC, NTL>(p, d2, n, c, true, jx, ccoef, a0, a1, bad);
     float2 *o = reinterpret_cast<float2 *>(out) + j;
     float2 r;
     if (ACC) {
@@ -590,6 +590,16 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
                 else
                     hipLaunchKernelGGL((dense_accumulate_wk<3, 34, ACC>), dim3(blocks), dim3(192), 0, s,
                                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
+                break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
+        // 49: dense_accumulate_w with plain (not nontemporal) loads
+        case 49:
+            if (vec && !CLIP && n <= 100) {
+                const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
+                hipLaunchKernelGGL((dense_accumulate_w<100, true, false, ACC, false>), dim3(blocks), dim3(64), 0, s,
+                                   (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status);
                 break;
             }
             launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
