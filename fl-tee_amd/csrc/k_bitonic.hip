@@ -105,6 +105,10 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_MERGE_PAIRS
 #define FLTEE_MERGE_PAIRS 2
 #endif
+// (Measured and removed, round 4: the first pass over 2^14 tiles as 512 lanes x 32 records —
+// 5 steps per LDS round, stages 1..5 in registers — 1,640 vs 1,068 us at C4, 1,821 vs 1,220
+// at C5: the compile-time rounds spill at 32 records per lane and the runtime ones run
+// slower; `profiles/r04/ab/ab12_first_pass_e32_rejected_*.jsonl`.)
 //   FLTEE_SEL_STORE_OOB  the selecting pass stores every record, the unselected ones out of
 //   the tile's buffer range (dropped), instead of a branch per record (A/B: 530 vs 520 us,
 //   not kept; `profiles/r04/ab/ab10_sel_store_oob_c4.jsonl`)
