@@ -50,10 +50,6 @@ __device__ __forceinline__ uint32_t oram_leaf(uint32_t k0, uint32_t k1, uint32_t
     return c[0] & mask;
 }
 
-__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
-    for (int o = 32; o; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
-    return v;
-}
 
 // slot s of the path to leaf x: level s / Z, bucket (2^l - 1) + (x >> (Lh - l))
 __device__ __forceinline__ uint32_t oram_slot(uint32_t s, uint32_t x, uint32_t Lh) {
@@ -79,20 +75,29 @@ __device__ __forceinline__ uint32_t take_lowest(uint64_t &m0, uint64_t &m1) {
 struct OramLane {
     uint32_t a0, l0, w0, a1, l1, w1;
 };
-__device__ __forceinline__ void oram_load_path(const uint4 *tree, uint32_t x, uint32_t Lh, uint32_t lane,
-                                               bool p0, bool p1, OramLane &r) {
-    if (p0) {
-        const uint32_t *ts = reinterpret_cast<const uint32_t *>(tree + oram_slot(lane, x, Lh));
-        r.a0 = __hip_atomic_load(ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        r.l0 = __hip_atomic_load(ts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        r.w0 = __hip_atomic_load(ts + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (p1) {
-        const uint32_t *ts = reinterpret_cast<const uint32_t *>(tree + oram_slot(64 + lane, x, Lh));
-        r.a1 = __hip_atomic_load(ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        r.l1 = __hip_atomic_load(ts + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        r.w1 = __hip_atomic_load(ts + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+typedef unsigned int oram_u32x4 __attribute__((ext_vector_type(4)));
+// The tree as a buffer resource of its slots: a slot offset at or past the end reads zeros
+// and stores nothing, so every lane issues the same loads and stores each access (a
+// skipped slot at the out-of-range offset: no memory access) — the compiler's vmcnt waits
+// then count them exactly instead of waiting for everything.
+constexpr uint32_t kOramOob = 0x7FFFFFF0u;
+__device__ __forceinline__ void oram_load_path(__amdgpu_buffer_rsrc_t rs, uint32_t x, uint32_t Lh,
+                                               uint32_t lane, bool p0, bool p1, OramLane &r) {
+    const oram_u32x4 b0 = __builtin_amdgcn_raw_buffer_load_b128(
+        rs, (int)(p0 ? oram_slot(lane, x, Lh) * 16u : kOramOob), 0, 1);
+    const oram_u32x4 b1 = __builtin_amdgcn_raw_buffer_load_b128(
+        rs, (int)(p1 ? oram_slot(64 + lane, x, Lh) * 16u : kOramOob), 0, 1);
+    r.a0 = b0.x, r.l0 = b0.y, r.w0 = b0.z;
+    r.a1 = b1.x, r.l1 = b1.y, r.w1 = b1.z;
+}
+__device__ __forceinline__ void oram_store_slot(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t a,
+                                                uint32_t l, uint32_t w) {
+    const oram_u32x4 v = {a, l, w, 0u};
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1" ::: "memory");  // dwordx4 store data hazard (k_bitonic.hip)
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // rec: nrec records (idx < N checked by the caller's range pass; clamped here);
@@ -100,11 +105,13 @@ __device__ __forceinline__ void oram_load_path(const uint4 *tree, uint32_t x, ui
 // the end for the readout).  One wave: lane j holds pool entries j and 64 + j (the path
 // slots first, then the stash), as (idx, leaf, value) words — plain registers, never an
 // indexed array (which would go to scratch).
-// Per access, after its own path is in registers: the NEXT access's leaf is read (after
-// this access's position-map write, so a repeated index sees its new leaf) and its path
-// loads are issued, to land while this access computes; the buckets the two paths share
-// (the top levels: l <= Lh - bitlen(x ^ x')) are then taken from this access's output,
-// which lives in the same lanes (slot l*Z + z of either path), the others from the loads.
+// Per access, after its own path is in registers: the leaf of the access TWO ahead is read
+// (after this access's position-map write, so a repeated index sees its new leaf; the
+// next access's fresh leaf when both are the same block) and its path loads are issued,
+// to land during this access and the next; the buckets a path shares with the previous
+// one (the top levels: l <= Lh - bitlen(x ^ x')) are taken from that access's output, those
+// it shares with the one before only from that one's output (kept in registers), and only
+// the rest are loaded.  Each output lives in the same lanes (slot l*Z + z of any path).
 // A lane only ever stores and reloads its own slots, so program order orders them.
 // The eviction: every block's rank by (deepest legal level, pool index) from one ballot
 // pair per level (mbcnt), the rank each slot receives from the per-level counts (uniform),
@@ -121,19 +128,22 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
     const uint32_t N = 1u << Lh, mask = N - 1u;
     const uint32_t P = kOramZ * (Lh + 1), POOL = P + kOramStash;
     uint4 *st = reinterpret_cast<uint4 *>(smem);                   // the stash: kOramStash entries
-    uint2 *rb = reinterpret_cast<uint2 *>(st + kOramStash);        // records q0 .. q0 + 63
-    uint32_t *lb = reinterpret_cast<uint32_t *>(rb + 64);          // and their new leaves
-    uint16_t *pm = reinterpret_cast<uint16_t *>(lb + 64);          // N leaves
+    uint2 *rb = reinterpret_cast<uint2 *>(st + kOramStash);        // records: a ring of 128
+    uint32_t *lb = reinterpret_cast<uint32_t *>(rb + 128);         // and their new leaves
+    uint16_t *pm = reinterpret_cast<uint16_t *>(lb + 128);         // N leaves
     const uint32_t lane = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)tree, (short)0, (int)(kOramZ * (2u * N - 1u) * 16u), 0x00020000);
     for (uint32_t i = lane; i < N; i += 64) pm[i] = (uint16_t)oram_leaf(k0, k1, nrec + i, mask);
     if (lane < kOramStash) st[lane] = make_uint4(kOramEmpty, 0u, 0u, 0u);
-    // a batch of 64 records into LDS (a broadcast read per access afterwards): the record
-    // loads are waited for once per 64 accesses, never on the access path
+    // records q0 .. q0 + 63 into their half of the ring (a broadcast read per access
+    // afterwards): the record loads are waited for once per 64 accesses, off the access path
     auto batch = [&](uint32_t q0) {
-        rb[lane] = q0 + lane < nrec ? rec[q0 + lane] : make_uint2(0u, 0u);
-        lb[lane] = oram_leaf(k0, k1, q0 + lane, mask);
+        rb[(q0 + lane) & 127u] = q0 + lane < nrec ? rec[q0 + lane] : make_uint2(0u, 0u);
+        lb[(q0 + lane) & 127u] = oram_leaf(k0, k1, q0 + lane, mask);
     };
     batch(0);
+    batch(64);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -141,42 +151,59 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
     const bool p0 = lane < P, p1 = 64 + lane < P;  // path slot (else stash entry)
     const uint32_t s0i = lane - P, s1i = 64 + lane - P;  // stash index of a stash entry
     const uint32_t lev0 = lane / kOramZ, lev1 = (64 + lane) / kOramZ;  // their levels
+    // the deepest level the paths to leaves u and v share
+    auto top = [&](uint32_t u, uint32_t v) { return Lh - (32u - (uint32_t)__clz((int)(u ^ v))); };
     uint32_t over = 0;
-    OramLane cur = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
-    uint32_t x = 0;
+    const OramLane none = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
+    // cur: access q's path; nxt1: the loads of access q+1's path (its buckets not shared
+    // with the paths of q or q-1); keep: access q-1's output
+    OramLane cur = none, nxt1 = none, keep = none;
+    uint32_t x = 0, x1 = 0, xp = 0;  // the leaves of accesses q, q+1, q-1
     if (nrec) {
         x = pm[rb[0].x & mask];  // every lane reads the same words: broadcasts
-        oram_load_path(tree, x, Lh, lane, p0, p1, cur);
+        oram_load_path(trs, x, Lh, lane, p0, p1, cur);
+        xp = x;  // no access -1: its buckets are never taken (top(xp, x1) = top(x, x1))
+        x1 = x;
+    }
+    if (nrec > 1) {
+        // access 1's leaf, as the position map will hold it after access 0's update
+        const uint32_t ra = rb[0].x & mask, rb1 = rb[1].x & mask;
+        x1 = rb1 == ra ? lb[0] : (uint32_t)pm[rb1];
+        const uint32_t t01 = top(x, x1);
+        oram_load_path(trs, x1, Lh, lane, p0 && lev0 > t01, p1 && lev1 > t01, nxt1);
     }
     // every load landed before the loop: the loop's own waits then cover only what it
-    // issued (the compiler otherwise keeps the first path "pending" at every iteration)
+    // issued (the compiler otherwise keeps the first paths "pending" at every iteration)
     __builtin_amdgcn_s_waitcnt(0);
-    for (uint32_t q = 0; q < nrec; ++q) {
-        const uint2 r = rb[q & 63u];
+    // one access; nin: the loads of access q+1's path (issued one access earlier), nout:
+    // where this access issues access q+2's.  The loop runs two accesses per trip with the
+    // two load sets in swapped roles, so no register copy of a load in flight (which would
+    // wait for it) is ever made.
+    auto access = [&](uint32_t q, OramLane &nin, OramLane &nout) {
+        const uint2 r = rb[q & 127u];
         const uint32_t a = r.x & mask;
         const float w = __uint_as_float(r.y);
-        const uint32_t nleaf = lb[q & 63u];
+        const uint32_t nleaf = lb[q & 127u];
         if (lane == 0) pm[a] = (uint16_t)nleaf;  // the block's fresh leaf
-        // the next access: its record, its leaf (after the write above), its path's loads
-        if (((q + 1) & 63u) == 0) {
+        if ((q & 63u) == 0 && q) {  // records q + 64 .. q + 127 into the half q - 64 .. q - 1 left
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
-            batch(q + 1);
+            batch(q + 64);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        const bool more = q + 1 < nrec;
-        const uint32_t an = rb[(q + 1) & 63u].x & mask;
-        const uint32_t xn = more ? (uint32_t)pm[an] : x;
-        OramLane nxt = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
-        // the buckets the two paths share (levels <= top) come from this access's output:
-        // only the rest is loaded (which levels is a function of the two public leaves).
-        // Those shared ones are also the slots the previous access's stores may still be
-        // writing, which a load would wait behind.
-        const uint32_t top = Lh - (32u - (uint32_t)__clz((int)(x ^ xn)));  // deepest shared level
-        const bool sh0 = lev0 <= top, sh1 = lev1 <= top;
-        if (more) oram_load_path(tree, xn, Lh, lane, p0 && !sh0, p1 && !sh1, nxt);
+        // two accesses ahead: access q+2's leaf (after this access's position-map write;
+        // access q+1's own fresh leaf when it is the same block) and its path's loads — only
+        // the buckets it shares with neither path q nor path q+1 (which come from those
+        // accesses' outputs; which levels is a function of the public leaves).  A load then
+        // has a whole access more to land, and never waits behind the stores of the
+        // buckets just written.
+        const bool more2 = q + 2 < nrec;
+        const uint32_t an1 = rb[(q + 1) & 127u].x & mask, an2 = rb[(q + 2) & 127u].x & mask;
+        const uint32_t x2 = more2 ? (an2 == an1 ? lb[(q + 1) & 127u] : (uint32_t)pm[an2]) : x1;
+        const uint32_t sk2 = max(top(x1, x2), top(x, x2));
+        oram_load_path(trs, x2, Lh, lane, more2 && p0 && lev0 > sk2, more2 && p1 && lev1 > sk2, nout);
         // the pool: this path (registers) and the stash (LDS)
         uint32_t a0 = cur.a0, l0 = cur.l0, w0 = cur.w0, a1 = cur.a1, l1 = cur.l1, w1 = cur.w1;
         if (!p0) {
@@ -189,8 +216,15 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         }
         // read: the block (at most one entry holds it), or +0.0
         const bool m0 = a0 == a, m1 = a1 == a;
-        const uint32_t vb = wave_or((m0 ? w0 : 0u) | (m1 ? w1 : 0u));
-        const bool found = (__ballot(m0) | __ballot(m1)) != 0;
+        // the holder's value by one readlane at the ballot's lowest set bit (uniform), not a
+        // 6-step shuffle reduction (each step a crossbar round trip)
+        const uint64_t bm0 = __ballot(m0), bm1 = __ballot(m1);
+        const bool found = (bm0 | bm1) != 0;
+        const uint32_t hl0 = (uint32_t)__builtin_ffsll((long long)bm0) - 1u;
+        const uint32_t hl1 = (uint32_t)__builtin_ffsll((long long)bm1) - 1u;
+        const uint32_t vb0 = (uint32_t)__builtin_amdgcn_readlane((int)w0, (int)(hl0 & 63u));
+        const uint32_t vb1 = (uint32_t)__builtin_amdgcn_readlane((int)w1, (int)(hl1 & 63u));
+        const uint32_t vb = bm0 ? vb0 : vb1;
         const float nv = __fadd_rn(found ? __uint_as_float(vb) : 0.0f, w);
         a0 = m0 ? kOramEmpty : a0;
         a1 = m1 ? kOramEmpty : a1;
@@ -288,27 +322,42 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
                        gw0 = hi0 ? gw0y : gw0x;
         const uint32_t ga1 = !h1 ? kOramEmpty : (hi1 ? ga1y : ga1x), gl1 = hi1 ? gl1y : gl1x,
                        gw1 = hi1 ? gw1y : gw1x;
-        // the next access's path: the shared top levels from this output, the rest loaded
+        // access q+1's path: the buckets it shares with path q from this output, those it
+        // shares with path q-1 only from that access's output, the rest from the loads
         // (merged before this access's stores are issued: the wait for the loads then does
         // not also wait for these stores — CDNA counts both in vmcnt, in order)
+        const uint32_t t01 = top(x, x1), tp1 = top(xp, x1);
+        const bool sh0 = lev0 <= t01, sh1 = lev1 <= t01, kp0 = lev0 <= tp1, kp1 = lev1 <= tp1;
         OramLane nc;
-        nc.a0 = sh0 ? ga0 : nxt.a0, nc.l0 = sh0 ? gl0 : nxt.l0, nc.w0 = sh0 ? gw0 : nxt.w0;
-        nc.a1 = sh1 ? ga1 : nxt.a1, nc.l1 = sh1 ? gl1 : nxt.l1, nc.w1 = sh1 ? gw1 : nxt.w1;
+        nc.a0 = sh0 ? ga0 : (kp0 ? keep.a0 : nin.a0);
+        nc.l0 = sh0 ? gl0 : (kp0 ? keep.l0 : nin.l0);
+        nc.w0 = sh0 ? gw0 : (kp0 ? keep.w0 : nin.w0);
+        nc.a1 = sh1 ? ga1 : (kp1 ? keep.a1 : nin.a1);
+        nc.l1 = sh1 ? gl1 : (kp1 ? keep.l1 : nin.l1);
+        nc.w1 = sh1 ? gw1 : (kp1 ? keep.w1 : nin.w1);
         // pin the merge here (the compiler would sink it past the stores, and its wait for
         // the loads would then wait for them too)
         asm volatile("" : "+v"(nc.a0), "+v"(nc.l0), "+v"(nc.w0), "+v"(nc.a1), "+v"(nc.l1), "+v"(nc.w1)
                      :
                      : "memory");
         // write the path back (the whole path, fixed addresses) and the stash
-        if (p0) tree[oram_slot(lane, x, Lh)] = make_uint4(ga0, gl0, gw0, 0u);
-        else if (v0) st[s0i] = make_uint4(ga0, gl0, gw0, 0u);
-        if (p1) tree[oram_slot(64 + lane, x, Lh)] = make_uint4(ga1, gl1, gw1, 0u);
-        else if (v1) st[s1i] = make_uint4(ga1, gl1, gw1, 0u);
+        oram_store_slot(trs, p0 ? oram_slot(lane, x, Lh) * 16u : kOramOob, ga0, gl0, gw0);
+        oram_store_slot(trs, p1 ? oram_slot(64 + lane, x, Lh) * 16u : kOramOob, ga1, gl1, gw1);
+        if (!p0 && v0) st[s0i] = make_uint4(ga0, gl0, gw0, 0u);
+        if (!p1 && v1) st[s1i] = make_uint4(ga1, gl1, gw1, 0u);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        keep = {ga0, gl0, gw0, ga1, gl1, gw1};
         cur = nc;
-        x = xn;
+        xp = x;
+        x = x1;
+        x1 = x2;
+    };
+    OramLane nxt2 = none;
+    for (uint32_t q = 0; q < nrec; q += 2) {
+        access(q, nxt1, nxt2);
+        if (q + 1 < nrec) access(q + 1, nxt2, nxt1);
     }
     // the stash, after the tree, for the readout
     if (lane < kOramStash) tree[(size_t)kOramZ * (2u * N - 1u) + lane] = st[lane];
@@ -346,7 +395,7 @@ hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, void *tree, 
     size_t blocks = (ns + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(oram_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4 *)tree, ns);
-    const size_t lds = kOramStash * 16 + 64 * 8 + 64 * 4 + N * 2;
+    const size_t lds = kOramStash * 16 + 128 * 8 + 128 * 4 + N * 2;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)oram_tree_kernel,
