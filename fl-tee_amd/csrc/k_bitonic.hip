@@ -553,7 +553,8 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 // around each prefetch load makes hipcc branch and wait vmcnt(0) per load
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
-template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true, bool SW = false>
+template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true, bool SW = false,
+          bool PR = false>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase,
@@ -569,7 +570,8 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     static_assert(!SW || !SORT, "the first pass is bitonic_sort_direct");
     // P2: lane t holds the slot pairs 2t, 2t + 1 (+ 2 NT r) — adjacent positions (the
     // compile-time shapes have W >= 2; SW keeps bits 0..3), one 16-B load and store each
-    constexpr bool P2 = FLTEE_TILE_PAIRS && !SORT && TL != 0;
+    // (PR: a run-time shape whose launcher checked wlog >= 1)
+    constexpr bool P2 = FLTEE_TILE_PAIRS && !SORT && (TL != 0 || PR);
     constexpr uint32_t LS = P2 ? 2u : 1u;  // records per load
     auto elem = [](int r) -> uint32_t {     // the tile element held in pf[r]
         return P2 ? 2u * threadIdx.x + (uint32_t)(r & 1) + (uint32_t)(r >> 1) * (2u * NT)
@@ -1268,21 +1270,39 @@ constexpr int kMinWLog = 4;
 template <int MODE>
 constexpr int kSortLatePf = MODE == 2 ? FLTEE_SORT_LATEPF_SHUFFLE : FLTEE_SORT_LATEPF_KEY;
 
-template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF, bool SW>
-static hipError_t launch_tiles_sw(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF, bool SW, bool PR = false>
+static hipError_t launch_tiles_pr(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
                                   uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                   uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0,
                                   uint32_t hole_at, uint32_t hole_len) {
     static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (160 KB on gfx950)
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>,
+        (void)hipFuncSetAttribute((const void *)bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW, PR>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog, "bitonic_tiles", s);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW>), dim3(grid), dim3(NT), lds, s,
+    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW, PR>), dim3(grid), dim3(NT), lds, s,
                        data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0, hole_at, hole_len);
     return hipGetLastError();
+}
+// the run-time-shaped 2^14 tiles take the slot pairs too when their rows have >= 2 records
+#ifndef FLTEE_TILE_PAIRS_RT
+#define FLTEE_TILE_PAIRS_RT 1
+#endif
+template <int MODE, bool SORT, int E, int NT, int TL, int WL, bool LPF, bool SW>
+static hipError_t launch_tiles_sw(unsigned grid, size_t lds, hipStream_t s, uint64_t *data,
+                                  uint32_t tlog, uint32_t ilog, uint32_t wlog, uint32_t dtile,
+                                  uint32_t seed, uint32_t tiles, uint32_t pbase, uint32_t seg0,
+                                  uint32_t hole_at, uint32_t hole_len) {
+    if constexpr (FLTEE_TILE_PAIRS_RT && TL == 0 && !SORT && NT == 1024 && E == 16) {
+        if (wlog >= 1)
+            return launch_tiles_pr<MODE, SORT, E, NT, TL, WL, LPF, SW, true>(grid, lds, s, data, tlog, ilog, wlog,
+                                                                            dtile, seed, tiles, pbase, seg0,
+                                                                            hole_at, hole_len);
+    }
+    return launch_tiles_pr<MODE, SORT, E, NT, TL, WL, LPF, SW>(grid, lds, s, data, tlog, ilog, wlog, dtile,
+                                                               seed, tiles, pbase, seg0, hole_at, hole_len);
 }
 
 // sw: the pass reads and writes the block-swizzled layout (2^14 tiles of 1024 lanes only)
