@@ -108,7 +108,8 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 // (Measured and removed, round 4: the first pass over 2^14 tiles as 512 lanes x 32 records —
 // 5 steps per LDS round, stages 1..5 in registers — 1,640 vs 1,068 us at C4, 1,821 vs 1,220
 // at C5: the compile-time rounds spill at 32 records per lane and the runtime ones run
-// slower; `profiles/r04/ab/ab12_first_pass_e32_rejected_*.jsonl`.)
+// slower; `profiles/r04/ab/ab12_first_pass_e32_rejected_*.jsonl`.  Likewise C3's 2^12 tiles as
+// 256 lanes x 16: 24.0 vs 21.0 us, `ab14_first_pass_256x16_c3_rejected.jsonl`.)
 //   FLTEE_SEL_STORE_OOB  the selecting pass stores every record, the unselected ones out of
 //   the tile's buffer range (dropped), instead of a branch per record (A/B: 530 vs 520 us,
 //   not kept; `profiles/r04/ab/ab10_sel_store_oob_c4.jsonl`)
