@@ -572,8 +572,10 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     // (spill-free compaction): C5 13.22 vs 13.32 ms fused (`profiles/r03/ab/ab10_*`), so the
     // fold is fused whenever the halo fits two window slots per lane (Hr < 1024).
     // (Tried in round 3 and not kept: batched branch-free level rounds, 505.6 -> 517 us per
-    // pass; the block-swizzled layout between the passes, 508 -> 503 us, `ab12_*`, `ab13_*`;
-    // 64 KiB tiles, 3 passes of 6 levels, as slow as 4 of 5, `ab11_*`.)
+    // pass; the block-swizzled layout between the passes, 508 -> 503 us, `ab12_*`, `ab13_*`,
+    // and again in round 4 with the 16-B slot pairs: 414-418 us either way,
+    // `profiles/r04/ab/ab15_compact_swizzle_v2_rejected.jsonl`; 64 KiB tiles, 3 passes of 6
+    // levels, as slow as 4 of 5, `ab11_*`.)
     if (!g_fold_compact || d == 0 || L <= d || Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
         return hipErrorNotSupported;
     const uint32_t nlev = bitlen(L - d);
