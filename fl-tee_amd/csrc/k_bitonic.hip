@@ -113,6 +113,9 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 //   FLTEE_SEL_STORE_OOB  the selecting pass stores every record, the unselected ones out of
 //   the tile's buffer range (dropped), instead of a branch per record (A/B: 530 vs 520 us,
 //   not kept; `profiles/r04/ab/ab10_sel_store_oob_c4.jsonl`)
+#ifndef FLTEE_DIRECT_MERGE
+#define FLTEE_DIRECT_MERGE 0
+#endif
 #ifndef FLTEE_SEL_STORE_OOB
 #define FLTEE_SEL_STORE_OOB 0
 #endif
@@ -1503,7 +1506,13 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     }
     // contiguous merges of 2^13 / 2^14 tiles: first and last round in registers
     // (A/B at 2^27: 13.89 vs 14.63 ms mode 0, 14.55 vs 15.65 ms mode 2; 2^24: -6 %)
-    if (!SORT && plain && wlog == c.tlog && c.tlog > 6) {
+    // FLTEE_DIRECT_MERGE 0 (round 4): a merge that neither selects nor changes layout runs as
+    // a plain contiguous tile pass with 16-B slot pairs instead of the direct merge (8-B
+    // loads for its register head round): C4 8.02 -> 8.00 ms, C5 12.28 -> 12.26 ms
+    // (`profiles/r04/ab/ab16_tile_merges_*.jsonl`); the selecting last pass and the last
+    // merge of a swizzled sort (reads swizzled, writes in order) stay direct
+    const bool direct = FLTEE_DIRECT_MERGE || sink.cnt || sw.in != sw.out;
+    if (!SORT && plain && wlog == c.tlog && c.tlog > 6 && direct) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink, sw);
         if (c.NT == 512 && c.E == 16 && !sw.in && !sw.out)
             return launch_direct<MODE, 16, 512, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink);
@@ -1543,6 +1552,9 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     }
 #define BT_GO(E_, NT_) \
     return launch_tiles_e<MODE, SORT, E_, NT_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in, c.hole_at, c.hole_len)
+    if (!FLTEE_DIRECT_MERGE && !SORT && plain && wlog == c.tlog && c.NT == 1024 && c.E == 16 && c.tlog == 14)
+        return launch_tiles_e<MODE, SORT, 16, 1024, 14>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed,
+                                                        c.tiles, pbase, 0u, sw.in, c.hole_at, c.hole_len);
     if (c.NT == 1024) BT_GO(16, 1024);
     if (c.NT == 256) BT_GO(2, 256);
     if (c.NT == 128) BT_GO(2, 128);
