@@ -116,6 +116,9 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_DIRECT_MERGE
 #define FLTEE_DIRECT_MERGE 0
 #endif
+#ifndef FLTEE_UNSW_TILES
+#define FLTEE_UNSW_TILES 1
+#endif
 #ifndef FLTEE_SEL_STORE_OOB
 #define FLTEE_SEL_STORE_OOB 0
 #endif
@@ -558,7 +561,7 @@ __device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint
 // (cdna_hip_programming.md §5 trap 4c), and a blockDim read inside the rounds is a
 // vector load + vmcnt(0) that drains the prefetch.
 template <int MODE, bool SORT, int E, int NT, int TL = 0, int WL = 0, bool LPF = true, bool SW = false,
-          bool PR = false>
+          bool PR = false, bool UNSW = false>
 __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data, uint32_t tlog,
                                                     uint32_t ilog, uint32_t wlog, uint32_t dtile,
                                                     uint32_t seed, uint32_t ntiles, uint32_t pbase,
@@ -583,6 +586,11 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     };
     const uint32_t lpos = tile_pos(0u, LS * threadIdx.x, wlog, dtile);
     const uint32_t voff = (SW ? phys(lpos) : lpos) * 8u;          // per-lane bytes
+    // UNSW (a contiguous sort's last merge): read the swizzled layout, write positions in
+    // order — a contiguous 2^14 tile keeps its own block in both layouts, so in place
+    static_assert(!UNSW || (SW && TL != 0 && WL == 0), "UNSW: contiguous swizzled tiles");
+    constexpr bool SWO_ = SW && !UNSW;
+    const uint32_t voffo = (SWO_ ? phys(lpos) : lpos) * 8u;
     const uint32_t rrow = (LS * (uint32_t)NT) << (dtile - wlog);  // records per load row, uniform
     const __amdgpu_buffer_rsrc_t rs = bt_rsrc(data);
     uint64_t pf[E];
@@ -680,12 +688,12 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         if constexpr (P2) {
 #pragma unroll
             for (int r = 0; r < E; r += 2)
-                tl_store2<SW>(rs, voff, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[lpad(elem(r))]),
+                tl_store2<SWO_>(rs, voffo, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[lpad(elem(r))]),
                               lds_ld(&sm[lpad(elem(r + 1))]));
         } else {
 #pragma unroll
             for (int r = 0; r < E; ++r)
-                tl_store<SW>(rs, voff, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
+                tl_store<SWO_>(rs, voffo, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
@@ -1511,7 +1519,26 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     // loads for its register head round): C4 8.02 -> 8.00 ms, C5 12.28 -> 12.26 ms
     // (`profiles/r04/ab/ab16_tile_merges_*.jsonl`); the selecting last pass and the last
     // merge of a swizzled sort (reads swizzled, writes in order) stay direct
-    const bool direct = FLTEE_DIRECT_MERGE || sink.cnt || sw.in != sw.out;
+    const bool direct = FLTEE_DIRECT_MERGE || sink.cnt || (sw.in != sw.out && !FLTEE_UNSW_TILES);
+    if constexpr (!SORT) {
+        // the last merge of a swizzled sort as a slot-pair tile pass that reads swizzled and
+        // writes in order (FLTEE_UNSW_TILES)
+        if (!direct && sw.in && !sw.out && plain && wlog == c.tlog && c.NT == 1024 && c.E == 16 &&
+            c.tlog == 14) {
+            static bool attr = false;
+            if (!attr) {
+                (void)hipFuncSetAttribute(
+                    (const void *)bitonic_tiles<MODE, false, 16, 1024, 14, 0, true, true, false, true>,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr = true;
+            }
+            net_account((uint64_t)16 * c.tiles << c.tlog, "bitonic_tiles", s);
+            hipLaunchKernelGGL((bitonic_tiles<MODE, false, 16, 1024, 14, 0, true, true, false, true>), dim3(c.grid),
+                               dim3(1024), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, 0u,
+                               c.hole_at, c.hole_len);
+            return hipGetLastError();
+        }
+    }
     if (!SORT && plain && wlog == c.tlog && c.tlog > 6 && direct) {
         if (c.NT == 1024) return launch_direct<MODE, 16, 1024, false>(c, s, data, ilog, wlog, dtile, seed, pbase, sink, sw);
         if (c.NT == 512 && c.E == 16 && !sw.in && !sw.out)
