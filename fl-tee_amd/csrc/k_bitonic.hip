@@ -113,6 +113,18 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 //   FLTEE_SEL_STORE_OOB  the selecting pass stores every record, the unselected ones out of
 //   the tile's buffer range (dropped), instead of a branch per record (A/B: 530 vs 520 us,
 //   not kept; `profiles/r04/ab/ab10_sel_store_oob_c4.jsonl`)
+//   FLTEE_TAIL_CT_KEYED  compile-time tail rounds for the keyed shuffle (mode 2) too (round 4:
+//   no spills since the 1024-lane tiles lost theirs; C4 8.00 -> 7.89 ms, bit-identical,
+//   `profiles/r04/ab/ab18_keyed_tail_ct_c4.jsonl`)
+#ifndef FLTEE_TAIL_CT_KEYED
+#define FLTEE_TAIL_CT_KEYED 1
+#endif
+//   FLTEE_TILE_W10  compile-time rounds for the 1024-lane strided tiles with rows of 2^10 too
+//   (the planned passes with a 10-step tail; round 4: C4 7.90 -> 7.84 ms, C5 unchanged,
+//   `profiles/r04/ab/ab19_tile_w10_*.jsonl`)
+#ifndef FLTEE_TILE_W10
+#define FLTEE_TILE_W10 1
+#endif
 #ifndef FLTEE_DIRECT_MERGE
 #define FLTEE_DIRECT_MERGE 0
 #endif
@@ -659,7 +671,8 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                 // (2^12 tiles of 512 lanes; the 1024-lane 2^14 tiles are held to 128 VGPRs
                 // and spill with the tail unrolled: C5 14.82 -> 15.44 ms, so they keep
                 // runtime tail rounds, `profiles/r02/ab/tail_ct.jsonl`)
-                if constexpr (TL != 0 && WL != 0 && MODE != 2 && (NT <= 512 || FLTEE_TAIL_CT_1024)) {
+                if constexpr (TL != 0 && WL != 0 && (MODE != 2 || FLTEE_TAIL_CT_KEYED) &&
+                              (NT <= 512 || FLTEE_TAIL_CT_1024)) {
                     if ((seg0 & 0xFFu) == (uint32_t)WL - 1u) {
                         lds_steps_ct<MODE, E, NT, WL - 1, 0, WL>(sm, base + pbase, st, seed, dtile);
                         done = true;
@@ -1553,13 +1566,16 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     // planned tiles' 2^8 .. 2^9, whose tails fill the consecutive bits): compile-time rounds
     if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && (1u << wlog) <= c.NT &&
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
-        (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512))) {
+        (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512) || (FLTEE_TILE_W10 && c.NT == 1024 && wlog == 10))) {
 #define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
     case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in, c.hole_at, c.hole_len);
         if (c.NT == 1024) {
             switch (wlog) {
                 BT_ST_CASE(16, 1024, 14, 4) BT_ST_CASE(16, 1024, 14, 5) BT_ST_CASE(16, 1024, 14, 6)
                 BT_ST_CASE(16, 1024, 14, 7)
+#if FLTEE_TILE_W10
+                BT_ST_CASE(16, 1024, 14, 10)  // rows of 2^10 (the planned tails on 10 low bits)
+#endif
             default: break;
             }
         } else {
