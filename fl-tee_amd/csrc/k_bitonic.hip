@@ -28,6 +28,7 @@
 // LDS layout pads one slot per 16 records so that the 64 lanes of a wave hit
 // distinct banks when each walks a 16-record group.
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -138,6 +139,15 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 //   tile slots plus one LDS gather of the records (bitonic_sort_direct, PERM)
 #ifndef FLTEE_KEYED_PERM
 #define FLTEE_KEYED_PERM 1
+#endif
+//   (A/B, `profiles/r04/ab/ab21_keyed_perm_c4.jsonl`: C4's first pass 1,060 -> 857 us, C4 7.86
+//   -> 7.64 ms, the same output.)
+//   FLTEE_KEYED_PERM_TILES  the same for the keyed shuffle's compile-time tile passes.  Not
+//   kept: with the records held in registers the 1024-lane tiles fit no prefetch through
+//   their rounds, and these passes are HBM-bound (C4 7.76 vs 7.65 ms, tiles 293 vs 288 us
+//   per launch, `profiles/r04/ab/ab22_keyed_perm_tiles_c4_rejected.jsonl`)
+#ifndef FLTEE_KEYED_PERM_TILES
+#define FLTEE_KEYED_PERM_TILES 0
 #endif
 
 namespace fltee {
@@ -389,8 +399,8 @@ __device__ __forceinline__ uint32_t past_hole(uint32_t t, uint32_t hole_at, uint
 // tile of T = E * NT records.  Lane t handles the G = E >> R groups t + h*NT (R <=
 // log2 E, so every lane is busy).  A round never straddles bit wlog, so the group's
 // global distance is 2^dlog_g and its first record sits at tile_pos(b).
-template <int MODE, int R, int E, int NT>
-__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t wlog,
+template <int MODE, int R, int E, int NT, typename V = uint64_t>
+__device__ __forceinline__ void lds_round(V *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, uint32_t jtop,
                                           uint32_t seed) {
     constexpr int G = E >> R;
@@ -402,7 +412,7 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t 
     constexpr int BW = kLdsBatch<G>;
 #pragma unroll
     for (int h0 = 0; h0 < G; h0 += BW) {
-        uint64_t v[BW][1 << R];
+        V v[BW][1 << R];
         uint32_t b[BW];
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
@@ -424,19 +434,19 @@ __device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t 
 // tile-local steps jtop..jbot of stage ilog, up to log2(E) per barrier.  (Tried:
 // wave-local rounds without block barriers for steps inside 64*E-record chunks —
 // slower on MI355X: +40 us per merge pass from the extra register pressure.)
-template <int MODE, int E, int NT>
-__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t wlog,
+template <int MODE, int E, int NT, typename V = uint64_t>
+__device__ __forceinline__ void lds_steps(V *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, int jtop, int jbot,
                                           uint32_t seed) {
     constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     while (jtop >= jbot) {
         const int left = jtop - jbot + 1;
         const int r = left < rmax ? left : rmax;
-        if (rmax >= 5 && r == 5) lds_round<MODE, (rmax >= 5 ? 5 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else lds_round<MODE, 1, E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        if (rmax >= 5 && r == 5) lds_round<MODE, (rmax >= 5 ? 5 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else lds_round<MODE, 1, E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         __syncthreads();
         jtop -= r;
     }
@@ -632,28 +642,48 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     // bitonic_merge_direct)
     constexpr int RH = P2 ? R1 - 1 : R1;  // the head round's steps
     constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && RH >= 1 && (TL - RH) >= WL;
+    // PERM: the keyed shuffle on tile elements, the records gathered at the end (see
+    // bitonic_sort_direct); dv holds them while the prefetch refills pf
+    constexpr bool PERM = MODE == 2 && FLTEE_KEYED_PERM_TILES && TL != 0 && !SORT;
+    uint32_t *const si = reinterpret_cast<uint32_t *>(sm);
+    uint64_t dv[PERM ? E : 1];
+    auto head_round = [&](const uint32_t base, auto (&v)[E]) {
+        if constexpr (P2) {
+            std::remove_reference_t<decltype(v[0])> g0[E / 2], g1[E / 2];
+#pragma unroll
+            for (int k = 0; k < E / 2; ++k) g0[k] = v[2 * k], g1[k] = v[2 * k + 1];
+            const uint32_t p0 = tile_pos(base, 2u * threadIdx.x, (uint32_t)WL, dtile) + pbase;
+            group_steps<MODE, RH>(g0, p0, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
+            group_steps<MODE, RH>(g1, p0 + 1u, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
+#pragma unroll
+            for (int k = 0; k < E / 2; ++k) v[2 * k] = g0[k], v[2 * k + 1] = g1[k];
+        } else {
+            group_steps<MODE, R1>(v, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
+                                  (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
+        }
+    };
     for (;;) {
         const uint32_t base = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
         const bool head_reg = kHeadReg && seg0 == 0;
-        if constexpr (kHeadReg) {
-            if (head_reg) {
-                if constexpr (P2) {
-                    uint64_t g0[E / 2], g1[E / 2];
+        if constexpr (PERM) {
+            uint32_t iv[E];
 #pragma unroll
-                    for (int k = 0; k < E / 2; ++k) g0[k] = pf[2 * k], g1[k] = pf[2 * k + 1];
-                    const uint32_t p0 = tile_pos(base, 2u * threadIdx.x, (uint32_t)WL, dtile) + pbase;
-                    group_steps<MODE, RH>(g0, p0, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
-                    group_steps<MODE, RH>(g1, p0 + 1u, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
-#pragma unroll
-                    for (int k = 0; k < E / 2; ++k) pf[2 * k] = g0[k], pf[2 * k + 1] = g1[k];
-                } else {
-                    group_steps<MODE, R1>(pf, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
-                                          (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
-                }
+            for (int r = 0; r < E; ++r) {
+                dv[r] = pf[r];
+                iv[r] = elem(r);
             }
-        }
+            if constexpr (kHeadReg) {
+                if (head_reg) head_round(base, iv);
+            }
 #pragma unroll
-        for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
+            for (int r = 0; r < E; ++r) si[lpad(elem(r))] = iv[r];
+        } else {
+            if constexpr (kHeadReg) {
+                if (head_reg) head_round(base, pf);
+            }
+#pragma unroll
+            for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
+        }
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
@@ -662,8 +692,10 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
         // registers are then not live through the tail)
-        constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT;
-        if (!kLate) prefetch();
+        // PERM: after the rounds (dv and the rounds' registers and pf do not fit together)
+        constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT && !PERM;
+        if (!kLate && !PERM) prefetch();
+        auto rounds = [&](auto *sm) {
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
@@ -706,15 +738,34 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                                        wlog < tlog ? (int)wlog : 0, seed);
             }
         }
+        };
+        // src(r): the LDS slot of the record that ends at tile element elem(r)
+        uint32_t w[PERM ? E : 1];
+        if constexpr (PERM) {
+            rounds(si);
+            prefetch();
+#pragma unroll
+            for (int r = 0; r < E; ++r) w[r] = si[lpad(elem(r))];
+            __syncthreads();  // every slot read before the records overwrite the slots
+#pragma unroll
+            for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = dv[r];
+            __syncthreads();
+        } else {
+            rounds(sm);
+        }
+        auto src = [&](int r) -> uint32_t {
+            if constexpr (PERM) return lpad(w[r]);
+            else return lpad(elem(r));
+        };
         if constexpr (P2) {
 #pragma unroll
             for (int r = 0; r < E; r += 2)
-                tl_store2<SWO_>(rs, voffo, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[lpad(elem(r))]),
-                              lds_ld(&sm[lpad(elem(r + 1))]));
+                tl_store2<SWO_>(rs, voffo, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[src(r)]),
+                              lds_ld(&sm[src(r + 1)]));
         } else {
 #pragma unroll
             for (int r = 0; r < E; ++r)
-                tl_store<SWO_>(rs, voffo, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
+                tl_store<SWO_>(rs, voffo, base + (uint32_t)r * rrow, lds_ld(&sm[src(r)]));
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
