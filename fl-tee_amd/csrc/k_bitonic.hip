@@ -28,7 +28,6 @@
 // LDS layout pads one slot per 16 records so that the 64 lanes of a wave hit
 // distinct banks when each walks a 16-record group.
 #include <map>
-#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -135,20 +134,6 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_SEL_STORE_OOB
 #define FLTEE_SEL_STORE_OOB 0
 #endif
-//   FLTEE_KEYED_PERM  the keyed shuffle's first pass (compile-time tiles) as a network on
-//   tile slots plus one LDS gather of the records (bitonic_sort_direct, PERM)
-#ifndef FLTEE_KEYED_PERM
-#define FLTEE_KEYED_PERM 1
-#endif
-//   (A/B, `profiles/r04/ab/ab21_keyed_perm_c4.jsonl`: C4's first pass 1,060 -> 857 us, C4 7.86
-//   -> 7.64 ms, the same output.)
-//   FLTEE_KEYED_PERM_TILES  the same for the keyed shuffle's compile-time tile passes.  Not
-//   kept: with the records held in registers the 1024-lane tiles fit no prefetch through
-//   their rounds, and these passes are HBM-bound (C4 7.76 vs 7.65 ms, tiles 293 vs 288 us
-//   per launch, `profiles/r04/ab/ab22_keyed_perm_tiles_c4_rejected.jsonl`)
-#ifndef FLTEE_KEYED_PERM_TILES
-#define FLTEE_KEYED_PERM_TILES 0
-#endif
 
 namespace fltee {
 
@@ -202,10 +187,8 @@ __device__ __forceinline__ bool keyed_swap(uint32_t kb, uint32_t dq) {
 // records held in v[], whose first record sits at global position p0.  The group
 // spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
 // is the same for every compare-exchange of the group: computed once.
-// V: the records (uint64_t), or for the keyed shuffle's permutation pass (FLTEE_KEYED_PERM)
-// their tile slots (uint32_t) — MODE 2's decisions read positions only.
-template <int MODE, int R, typename V = uint64_t>
-__device__ __forceinline__ void group_steps(V (&v)[1 << R], uint32_t p0, uint32_t dlog,
+template <int MODE, int R>
+__device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, uint32_t dlog,
                                             uint32_t ilog, uint32_t seed) {
     if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
     const bool asc = (p0 & (1u << ilog)) == 0;
@@ -234,7 +217,7 @@ __device__ __forceinline__ void group_steps(V (&v)[1 << R], uint32_t p0, uint32_
         for (int q = 0, k = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const V a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool s = sw[k++];
             v[q] = s ? c : a;
             v[qm] = s ? a : c;
@@ -244,7 +227,7 @@ __device__ __forceinline__ void group_steps(V (&v)[1 << R], uint32_t p0, uint32_
         for (int q = 0; q < (1 << R); ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const V a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool sw = decide(q, qm);
             v[q] = sw ? c : a;
             v[qm] = sw ? a : c;
@@ -264,7 +247,6 @@ __device__ __forceinline__ uint64_t lds_ld(const uint64_t *p) {
     return *p;
 #endif
 }
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) { return *p; }
 
 // The lane id, re-defined where it is read (FLTEE_TID_FRESH): a round's per-lane LDS
 // addresses are then computed in the round (a few VALU) instead of being hoisted out of
@@ -399,8 +381,8 @@ __device__ __forceinline__ uint32_t past_hole(uint32_t t, uint32_t hole_at, uint
 // tile of T = E * NT records.  Lane t handles the G = E >> R groups t + h*NT (R <=
 // log2 E, so every lane is busy).  A round never straddles bit wlog, so the group's
 // global distance is 2^dlog_g and its first record sits at tile_pos(b).
-template <int MODE, int R, int E, int NT, typename V = uint64_t>
-__device__ __forceinline__ void lds_round(V *sm, uint32_t base, uint32_t wlog,
+template <int MODE, int R, int E, int NT>
+__device__ __forceinline__ void lds_round(uint64_t *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, uint32_t jtop,
                                           uint32_t seed) {
     constexpr int G = E >> R;
@@ -412,7 +394,7 @@ __device__ __forceinline__ void lds_round(V *sm, uint32_t base, uint32_t wlog,
     constexpr int BW = kLdsBatch<G>;
 #pragma unroll
     for (int h0 = 0; h0 < G; h0 += BW) {
-        V v[BW][1 << R];
+        uint64_t v[BW][1 << R];
         uint32_t b[BW];
 #pragma unroll
         for (int h = 0; h < BW; ++h) {
@@ -434,19 +416,19 @@ __device__ __forceinline__ void lds_round(V *sm, uint32_t base, uint32_t wlog,
 // tile-local steps jtop..jbot of stage ilog, up to log2(E) per barrier.  (Tried:
 // wave-local rounds without block barriers for steps inside 64*E-record chunks —
 // slower on MI355X: +40 us per merge pass from the extra register pressure.)
-template <int MODE, int E, int NT, typename V = uint64_t>
-__device__ __forceinline__ void lds_steps(V *sm, uint32_t base, uint32_t wlog,
+template <int MODE, int E, int NT>
+__device__ __forceinline__ void lds_steps(uint64_t *sm, uint32_t base, uint32_t wlog,
                                           uint32_t dtile, uint32_t ilog, int jtop, int jbot,
                                           uint32_t seed) {
     constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     while (jtop >= jbot) {
         const int left = jtop - jbot + 1;
         const int r = left < rmax ? left : rmax;
-        if (rmax >= 5 && r == 5) lds_round<MODE, (rmax >= 5 ? 5 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
-        else lds_round<MODE, 1, E, NT, V>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        if (rmax >= 5 && r == 5) lds_round<MODE, (rmax >= 5 ? 5 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 4 && r == 4) lds_round<MODE, (rmax >= 4 ? 4 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 3 && r == 3) lds_round<MODE, (rmax >= 3 ? 3 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else if (rmax >= 2 && r == 2) lds_round<MODE, (rmax >= 2 ? 2 : 1), E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
+        else lds_round<MODE, 1, E, NT>(sm, base, wlog, dtile, ilog, (uint32_t)jtop, seed);
         __syncthreads();
         jtop -= r;
     }
@@ -472,8 +454,8 @@ __device__ __forceinline__ uint32_t round_group(uint32_t t, int h, int NT, int W
     return (t & 63u) | ((uint32_t)h << 6) | ((t >> 6) << (6 + gl));
 }
 
-template <int MODE, int R, int E, int NT, int DLOG, int WL = 0, int WB = 0, typename V = uint64_t>
-__device__ __forceinline__ void lds_round_ct(V *sm, uint32_t base, uint32_t ilog,
+template <int MODE, int R, int E, int NT, int DLOG, int WL = 0, int WB = 0>
+__device__ __forceinline__ void lds_round_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     static_assert(WL == 0 || DLOG >= WL || DLOG + R <= WL, "a round stays on one side of bit WL");
     static_assert(WB == 0 || (WL == 0 && DLOG + R <= WB && (64 * E) == (1 << WB)), "wave-local round");
@@ -483,13 +465,13 @@ __device__ __forceinline__ void lds_round_ct(V *sm, uint32_t base, uint32_t ilog
     constexpr int BW = kLdsBatch<G>;
 #pragma unroll
     for (int h0 = 0; h0 < G; h0 += BW) {
-    V v[BW][1 << R];
+    uint64_t v[BW][1 << R];
     uint32_t b[BW];
 #pragma unroll
     for (int h = 0; h < BW; ++h) {
         b[h] = spread(round_group<G>(lane_tid<NT>(), h0 + h, NT, WB), (uint32_t)DLOG, (uint32_t)R);
         if constexpr (DLOG + R >= 4) {
-            const V *row = sm + lpad(b[h]);
+            const uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) v[h][q] = lds_ld(&row[(q << DLOG) + ((q << DLOG) >> 4)]);
         } else {  // a group inside 16 records: the padding slot may fall between its records
@@ -505,7 +487,7 @@ __device__ __forceinline__ void lds_round_ct(V *sm, uint32_t base, uint32_t ilog
 #pragma unroll
     for (int h = 0; h < BW; ++h) {
         if constexpr (DLOG + R >= 4) {
-            V *row = sm + lpad(b[h]);
+            uint64_t *row = sm + lpad(b[h]);
 #pragma unroll
             for (int q = 0; q < (1 << R); ++q) row[(q << DLOG) + ((q << DLOG) >> 4)] = v[h][q];
         } else {
@@ -517,8 +499,8 @@ __device__ __forceinline__ void lds_round_ct(V *sm, uint32_t base, uint32_t ilog
 }
 // WB > 0: wave-local rounds (see round_group), ordered by the wave's own LDS order
 // (a compiler-only barrier between them) instead of block barriers
-template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0, int WB = 0, typename V = uint64_t>
-__device__ __forceinline__ void lds_steps_ct(V *sm, uint32_t base, uint32_t ilog,
+template <int MODE, int E, int NT, int JTOP, int JBOT, int WL = 0, int WB = 0>
+__device__ __forceinline__ void lds_steps_ct(uint64_t *sm, uint32_t base, uint32_t ilog,
                                              uint32_t seed, uint32_t dtile = 0) {
     if constexpr (JTOP >= JBOT) {
         constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
@@ -543,8 +525,8 @@ constexpr int kWaveLog = E >= 32 ? 11 : (E >= 16 ? 10 : (E >= 8 ? 9 : (E >= 4 ? 
 // consecutive records and run as wave-local rounds (no block barrier: the waves drift and
 // overlap one another's LDS traffic with their compare-exchanges), then one block barrier.
 // The same steps in the same order: the network is unchanged.  Ends in a block barrier.
-template <int MODE, int E, int NT, int IL, int JBOT, typename V = uint64_t>
-__device__ __forceinline__ void stage_steps_ct(V *sm, uint32_t base, uint32_t seed) {
+template <int MODE, int E, int NT, int IL, int JBOT>
+__device__ __forceinline__ void stage_steps_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
     constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
     constexpr int rmax = E >= 32 ? 5 : (E >= 16 ? 4 : (E >= 8 ? 3 : (E >= 4 ? 2 : 1)));
     constexpr int r_all = (IL - JBOT + rmax - 1) / rmax;
@@ -560,8 +542,8 @@ __device__ __forceinline__ void stage_steps_ct(V *sm, uint32_t base, uint32_t se
     }
 }
 
-template <int MODE, int E, int NT, int IL, int TL, int RL, typename V = uint64_t>
-__device__ __forceinline__ void sort_stages_ct(V *sm, uint32_t base, uint32_t seed) {
+template <int MODE, int E, int NT, int IL, int TL, int RL>
+__device__ __forceinline__ void sort_stages_ct(uint64_t *sm, uint32_t base, uint32_t seed) {
     constexpr int WB = FLTEE_WAVE_LOCAL ? kWaveLog<E> : 0;
     if constexpr (IL < TL) {
         if constexpr (WB && IL <= WB) {
@@ -642,48 +624,28 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
     // bitonic_merge_direct)
     constexpr int RH = P2 ? R1 - 1 : R1;  // the head round's steps
     constexpr bool kHeadReg = FLTEE_TILE_HEADREG && TL != 0 && WL != 0 && !SORT && RH >= 1 && (TL - RH) >= WL;
-    // PERM: the keyed shuffle on tile elements, the records gathered at the end (see
-    // bitonic_sort_direct); dv holds them while the prefetch refills pf
-    constexpr bool PERM = MODE == 2 && FLTEE_KEYED_PERM_TILES && TL != 0 && !SORT;
-    uint32_t *const si = reinterpret_cast<uint32_t *>(sm);
-    uint64_t dv[PERM ? E : 1];
-    auto head_round = [&](const uint32_t base, auto (&v)[E]) {
-        if constexpr (P2) {
-            std::remove_reference_t<decltype(v[0])> g0[E / 2], g1[E / 2];
-#pragma unroll
-            for (int k = 0; k < E / 2; ++k) g0[k] = v[2 * k], g1[k] = v[2 * k + 1];
-            const uint32_t p0 = tile_pos(base, 2u * threadIdx.x, (uint32_t)WL, dtile) + pbase;
-            group_steps<MODE, RH>(g0, p0, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
-            group_steps<MODE, RH>(g1, p0 + 1u, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
-#pragma unroll
-            for (int k = 0; k < E / 2; ++k) v[2 * k] = g0[k], v[2 * k + 1] = g1[k];
-        } else {
-            group_steps<MODE, R1>(v, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
-                                  (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
-        }
-    };
     for (;;) {
         const uint32_t base = tile_base(past_hole(tile, hole_at, hole_len), tlog, wlog, dtile);
         const bool head_reg = kHeadReg && seg0 == 0;
-        if constexpr (PERM) {
-            uint32_t iv[E];
+        if constexpr (kHeadReg) {
+            if (head_reg) {
+                if constexpr (P2) {
+                    uint64_t g0[E / 2], g1[E / 2];
 #pragma unroll
-            for (int r = 0; r < E; ++r) {
-                dv[r] = pf[r];
-                iv[r] = elem(r);
-            }
-            if constexpr (kHeadReg) {
-                if (head_reg) head_round(base, iv);
-            }
+                    for (int k = 0; k < E / 2; ++k) g0[k] = pf[2 * k], g1[k] = pf[2 * k + 1];
+                    const uint32_t p0 = tile_pos(base, 2u * threadIdx.x, (uint32_t)WL, dtile) + pbase;
+                    group_steps<MODE, RH>(g0, p0, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
+                    group_steps<MODE, RH>(g1, p0 + 1u, (uint32_t)(TL - RH - WL) + dtile, ilog, seed);
 #pragma unroll
-            for (int r = 0; r < E; ++r) si[lpad(elem(r))] = iv[r];
-        } else {
-            if constexpr (kHeadReg) {
-                if (head_reg) head_round(base, pf);
+                    for (int k = 0; k < E / 2; ++k) pf[2 * k] = g0[k], pf[2 * k + 1] = g1[k];
+                } else {
+                    group_steps<MODE, R1>(pf, tile_pos(base, threadIdx.x, (uint32_t)WL, dtile) + pbase,
+                                          (uint32_t)(TL - R1 - WL) + dtile, ilog, seed);
+                }
             }
-#pragma unroll
-            for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
         }
+#pragma unroll
+        for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = pf[r];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
@@ -692,10 +654,8 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
         // registers are then not live through the tail)
-        // PERM: after the rounds (dv and the rounds' registers and pf do not fit together)
-        constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT && !PERM;
-        if (!kLate && !PERM) prefetch();
-        auto rounds = [&](auto *sm) {
+        constexpr bool kLate = LPF && TL != 0 && WL != 0 && !SORT;
+        if (!kLate) prefetch();
         if (SORT) {
             for (uint32_t il = 1; il <= tlog; ++il)
                 lds_steps<MODE, E, NT>(sm, base + pbase, wlog, dtile, il, (int)il - 1, 0, seed);
@@ -738,34 +698,15 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
                                        wlog < tlog ? (int)wlog : 0, seed);
             }
         }
-        };
-        // src(r): the LDS slot of the record that ends at tile element elem(r)
-        uint32_t w[PERM ? E : 1];
-        if constexpr (PERM) {
-            rounds(si);
-            prefetch();
-#pragma unroll
-            for (int r = 0; r < E; ++r) w[r] = si[lpad(elem(r))];
-            __syncthreads();  // every slot read before the records overwrite the slots
-#pragma unroll
-            for (int r = 0; r < E; ++r) sm[lpad(elem(r))] = dv[r];
-            __syncthreads();
-        } else {
-            rounds(sm);
-        }
-        auto src = [&](int r) -> uint32_t {
-            if constexpr (PERM) return lpad(w[r]);
-            else return lpad(elem(r));
-        };
         if constexpr (P2) {
 #pragma unroll
             for (int r = 0; r < E; r += 2)
-                tl_store2<SWO_>(rs, voffo, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[src(r)]),
-                              lds_ld(&sm[src(r + 1)]));
+                tl_store2<SWO_>(rs, voffo, base + (uint32_t)(r >> 1) * rrow, lds_ld(&sm[lpad(elem(r))]),
+                              lds_ld(&sm[lpad(elem(r + 1))]));
         } else {
 #pragma unroll
             for (int r = 0; r < E; ++r)
-                tl_store<SWO_>(rs, voffo, base + (uint32_t)r * rrow, lds_ld(&sm[src(r)]));
+                tl_store<SWO_>(rs, voffo, base + (uint32_t)r * rrow, lds_ld(&sm[lpad(threadIdx.x + r * NT)]));
         }
         if (next >= ntiles) break;
         __syncthreads();  // this tile's LDS reads retire before the next tile lands
@@ -990,8 +931,8 @@ __global__ __launch_bounds__(NT) void bitonic_merge_direct(uint64_t *__restrict_
 
 // Stage IL (< log2 E) on a lane's E consecutive records at positions p0..p0+E-1: the
 // records form E / 2^IL whole stage blocks, each with its own direction.
-template <int MODE, int IL, int E, typename V = uint64_t>
-__device__ __forceinline__ void lane_stage(V (&v)[E], uint32_t p0, uint32_t seed) {
+template <int MODE, int IL, int E>
+__device__ __forceinline__ void lane_stage(uint64_t (&v)[E], uint32_t p0, uint32_t seed) {
     constexpr int B = 1 << IL;
     if constexpr (MODE == 2 && FLTEE_KEY_AFTER_DATA) seed = after_data(seed, (uint32_t)v[0]);
 #pragma unroll
@@ -1016,7 +957,7 @@ __device__ __forceinline__ void lane_stage(V (&v)[E], uint32_t p0, uint32_t seed
         for (int q = 0, k = 0; q < E; ++q) {
             if (q & (1 << lv)) continue;
             const int qm = q | (1 << lv);
-            const V a = v[q], c = v[qm];
+            const uint64_t a = v[q], c = v[qm];
             const bool s = sw[k++];
             v[q] = s ? c : a;
             v[qm] = s ? a : c;
@@ -1162,47 +1103,24 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             }
         }
     };
-    // PERM (FLTEE_KEYED_PERM): the keyed shuffle's decisions read positions only, so the
-    // network runs on the records' tile slots (4 B in LDS, one v_cndmask pair per
-    // compare-exchange instead of two) while the records wait in dv; the last round's
-    // slots then gather the records from LDS: out[f] = in[slot[f]], the same permutation.
-    constexpr bool PERM = MODE == 2 && FLTEE_KEYED_PERM && TL != 0;
-    uint32_t *const si = reinterpret_cast<uint32_t *>(sm);
-    uint64_t dv[PERM ? E : 1];
-    auto lane_stages = [&](auto (&v)[E], uint32_t p0) {
-        lane_stage<MODE, 1, E>(v, p0, seed);
-        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(v, p0, seed);
-        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(v, p0, seed);
-        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(v, p0, seed);
-        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(v, p0, seed);
-    };
     issue(tile);
     for (;;) {
         finish(tile);
         const uint32_t base = tile << tlog;
         const uint32_t p0 = base + pbase + t * (uint32_t)E;
-        if constexpr (PERM) {
-            const uint32_t s0 = lane_tid<NT>() * (uint32_t)E;
-            uint32_t iv[E];
+        lane_stage<MODE, 1, E>(pf, p0, seed);
+        if (R1 >= 2) lane_stage<MODE, (R1 >= 2 ? 2 : 1), E>(pf, p0, seed);
+        if (R1 >= 3) lane_stage<MODE, (R1 >= 3 ? 3 : 1), E>(pf, p0, seed);
+        if (R1 >= 4) lane_stage<MODE, (R1 >= 4 ? 4 : 1), E>(pf, p0, seed);
+        if (R1 >= 5) lane_stage<MODE, (R1 >= 5 ? 5 : 1), E>(pf, p0, seed);
 #pragma unroll
-            for (int r = 0; r < E; ++r) {
-                dv[r] = pf[r];
-                iv[r] = s0 + (uint32_t)r;
-            }
-            lane_stages(iv, p0);
-#pragma unroll
-            for (int r = 0; r < E; ++r) si[lpad(s0 + (uint32_t)r)] = iv[r];
-        } else {
-            lane_stages(pf, p0);
-#pragma unroll
-            for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
-        }
+        for (int r = 0; r < E; ++r) sm[lpad(t * (uint32_t)E + (uint32_t)r)] = pf[r];
         // the lane's records are positions tE .. tE + E - 1: the wave's own 64 E records,
         // which its wave-local first rounds read back (TL != 0 with FLTEE_WAVE_LOCAL)
         if constexpr (TL != 0 && FLTEE_WAVE_LOCAL && R1 + 1 <= kWaveLog<E>) wave_lds_order();
         else __syncthreads();
         const uint32_t next = tile + stride;
-        auto rounds_ct = [&](auto *net) {
+        if constexpr (TL != 0) {  // tlog == TL (launcher)
             // the next tile's loads go out before the LAST stage's rounds, not before the
             // first: the prefetch registers stay free through the rounds of stages
             // log2 E + 1 .. TL - 1 (1024 lanes are held to 128 VGPRs; with the prefetch
@@ -1215,22 +1133,18 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
             // other in the same order, so the network and its output are unchanged.
             constexpr int kLast = RL + R1 - 1;
             if constexpr (LPF == 2 && kLast < TL - 1) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(net, base + pbase, seed);
-                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(net, base + pbase, (uint32_t)TL, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, kLast + 1>(sm, base + pbase, (uint32_t)TL, seed);
                 issue(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, kLast, RL>(net, base + pbase, (uint32_t)TL, seed);
+                lds_steps_ct<MODE, E, NT, kLast, RL>(sm, base + pbase, (uint32_t)TL, seed);
             } else if constexpr (LPF != 0) {
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(net, base + pbase, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL - 1, 0>(sm, base + pbase, seed);
                 issue(next < ntiles ? next : tile);
-                lds_steps_ct<MODE, E, NT, TL - 1, RL>(net, base + pbase, (uint32_t)TL, seed);
+                lds_steps_ct<MODE, E, NT, TL - 1, RL>(sm, base + pbase, (uint32_t)TL, seed);
             } else {
                 issue(next < ntiles ? next : tile);
-                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(net, base + pbase, seed);
+                sort_stages_ct<MODE, E, NT, R1 + 1, TL, RL>(sm, base + pbase, seed);
             }
-        };
-        if constexpr (TL != 0) {  // tlog == TL (launcher)
-            if constexpr (PERM) rounds_ct(si);
-            else rounds_ct(sm);
         } else {
             issue(next < ntiles ? next : tile);
             for (uint32_t il = (uint32_t)R1 + 1; il < tlog; ++il)
@@ -1242,38 +1156,6 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
         // would otherwise hold the next group's reads behind them)
         constexpr int BW = kLdsBatch<G>;
         const uint32_t sxb = SWO ? swz_x(base) : 0u;  // the tile's block swizzle (merge_direct)
-        if constexpr (PERM) {
-            uint32_t vi[G][1 << RL];
-            const uint32_t tf = lane_tid<NT>();
-#pragma unroll
-            for (int h = 0; h < G; ++h) {
-                const uint32_t b = (tf + (uint32_t)h * NT) << RL;
-#pragma unroll
-                for (int q = 0; q < (1 << RL); ++q) vi[h][q] = si[lpad(b + (uint32_t)q)];
-            }
-#pragma unroll
-            for (int h = 0; h < G; ++h)
-                group_steps<MODE, RL>(vi[h], base + pbase + ((tf + (uint32_t)h * NT) << RL), 0u, tlog, seed);
-            __syncthreads();  // every slot read before the records overwrite the slots
-#pragma unroll
-            for (int r = 0; r < E; ++r) sm[lpad(tf * (uint32_t)E + (uint32_t)r)] = dv[r];
-            __syncthreads();
-#pragma unroll
-            for (int h = 0; h < G; ++h) {
-                const uint32_t b = ((tf + (uint32_t)h * NT) << RL) ^ sxb;  // physical offset
-#pragma unroll
-                for (int q = 0; q < (1 << RL); q += 2) {
-                    const uint64_t a = sm[lpad(vi[h][q])], c = sm[lpad(vi[h][q + 1])];
-                    const bt_u32x4 x = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32)};
-                    __builtin_amdgcn_sched_barrier(0);
-                    __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)((b + (uint32_t)q) * 8u),
-                                                           (int)(base * 8u), kTileCP);
-                    __builtin_amdgcn_sched_barrier(0);
-                    asm volatile("s_nop 1" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        } else {
 #pragma unroll
         for (int h0 = 0; h0 < G; h0 += BW) {
         uint64_t vv[BW][1 << RL];
@@ -1304,7 +1186,6 @@ __global__ __launch_bounds__(NT) void bitonic_sort_direct(uint64_t *__restrict__
                 asm volatile("s_nop 1" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
             }
-        }
         }
         }
         if (next >= ntiles) break;
