@@ -38,7 +38,7 @@ from bench_legs import (ALG_NAMES, HBM_PEAK_GBS, WORKLOADS, algorithmic_bytes,  
                         bench_exp5, bench_next_rows, bench_oram_tree, bench_reference_configs, bench_workload,
                         bench_ns_strong, c_abi_multi_gpu, cpu_baseline_configs, cpu_baseline_sample,
                         dominant_kernel, e2e_sample, make_records, network_records,
-                        rocprof_kernel, traffic_from_profiles, _build_id)
+                        read_floor, rocprof_kernel, traffic_from_profiles, _build_id)
 
 
 LINE_MAX_BYTES = 4096  # the driver reads the last line from an 8 KB stdout tail
@@ -80,6 +80,10 @@ def compact_line(full):
             "value": _r(lit["value"]), "kernel_ms": _r(lit["kernel_ms"]),
             "kernel_ms_median": _r(lit.get("kernel_ms_median")),
             "frac": _r(lit["roofline"]["frac"]), "trials": lit.get("trials")}
+        rf = lit.get("read_floor")
+        if rf:  # the same bytes read by a plain streaming kernel in the same run
+            line["metric_literal_config"]["read_floor_ms"] = _r(rf["us"] / 1e3)
+            line["metric_literal_config"]["frac_of_floor"] = _r(rf["us"] / 1e3 / lit["kernel_ms"], 3)
     ex = full.get("extra")
     if ex and full.get("n_gpus", 1) == 1:
         cpu = full.get("cpu_baseline_configs", {})
@@ -280,6 +284,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "build": _build_id(),
             "config": {"workload": (f"{args.workload}: " + w["desc"])[:90],
+                       "value_is": "the north-star shape (SURVEY 8: 100 clients x 1M dense params "
+                                   "per GPU); the metric's literal 100 x MLP-MNIST workload is "
+                                   "metric_literal_config",
                        "alg": ALG_NAMES[w["alg"]], "n_clients": n,
                        "d_per_gpu": d, "k": kk, "record_bytes": 8,
                        "parallelism": f"param-range shard x{world}" +
@@ -332,22 +339,21 @@ def main():
                     exchange="pairwise")),
                 ("c4_index_sharded", lambda: bench_c4_index_sharded(
                     torch, D, dist, world, rank, device, steps=xsteps, warmup=1))]
-        for name, fn in legs:
-            state["leg"] = name
-            sharded[name] = fn()
         if os.environ.get("FLTEE_BENCH_NO_CABI") != "1":
-            # the C-ABI multi-GPU eid, in a child of rank 0 while every rank waits on a
-            # host (gloo) barrier with its cached HBM released
+            # the C-ABI multi-GPU eid first (its own share of the budget, so the sharded legs
+            # cannot crowd it out), in a child of rank 0 while every rank waits on a host
+            # (gloo) barrier with its cached HBM released
             state["leg"] = "c_abi_multi_gpu"
             hostpg = dist.new_group(backend="gloo")
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             dist.barrier(group=hostpg)
             if rank == 0:
-                left = budget - (time.monotonic() - t_extra) - 15
-                sharded["c_abi_multi_gpu"] = (c_abi_multi_gpu(world, timeout=left) if left > 30
-                                              else {"error": "skipped: extras budget spent"})
+                sharded["c_abi_multi_gpu"] = c_abi_multi_gpu(world, timeout=max(60.0, 0.45 * budget))
             dist.barrier(group=hostpg)
+        for name, fn in legs:
+            state["leg"] = name
+            sharded[name] = fn()
         state["leg"] = None
         disarm.set()
         if rank == 0:
@@ -372,6 +378,7 @@ def main():
                                             warmup=12, device=device, cold=True)
                              for _ in range(3)), key=lambda r: r["kernel_s"])
             lit = trials[0]
+            floor = read_floor(torch, lit["bytes"], device)
             full["metric_literal_config"] = dict(
                 workload=WORKLOADS["mnist100"]["desc"], value=lit["rate"], unit="client-params/s",
                 kernel_ms=lit["kernel_s"] * 1e3, kernel_ms_median=trials[1]["kernel_s"] * 1e3,
@@ -383,7 +390,8 @@ def main():
                               frac_median=lit["bytes"] / trials[1]["kernel_s"] / 1e9 / HBM_PEAK_GBS,
                               algorithmic_bytes=lit["bytes"], kernel="dense_accumulate_w",
                               note="cold: inputs rotated over > 1.5 x 256 MiB; best of the trials "
-                                   "(kernel_ms) and their median (kernel_ms_median)"))
+                                   "(kernel_ms) and their median (kernel_ms_median)"),
+                read_floor=floor)
             if not args.no_cpu_baseline and not args.no_cpu_configs:
                 gms = {nm: e["kernel_ms"] for nm, e in full["extra"].items()}
                 full["cpu_baseline_configs"] = cpu_baseline_configs(gms)

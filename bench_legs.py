@@ -29,6 +29,10 @@ WORKLOADS = {
                      desc="100 clients x MLP-MNIST dense (metric text), baseline"),
     "c1": dict(alg=4, n=30, d=50890, k=5089,
                desc="configs[0] shape on GPU: MLP-MNIST n=30 alpha=0.1, non_oblivious"),
+    "c2s": dict(alg=3, n=30, d=50890, k=5089,
+                desc="MLP-MNIST n=30 alpha=0.1, baseline on sparse uploads (the ordered sweep)"),
+    "b3000": dict(alg=3, n=3000, d=50890, k=5089,
+                  desc="the reference's published n=3000 shape, baseline (the ordered sweep)"),
     "c3": dict(alg=1, n=100, d=50890, k=5089,
                desc="configs[2]: MLP-MNIST num_users=1000 frac=0.1 alpha=0.1 (n=100), advanced"),
     "c4": dict(alg=2, n=300, d=44964, k=4496, dp=True,
@@ -102,6 +106,35 @@ def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False):
     del recs
     return dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
                 rate=n * kk / kern, bytes=algorithmic_bytes(w), nbuf=nbuf, net=net)
+
+
+def read_floor(torch, bytes_per_step, device, reps=3, steps=40):
+    """The achievable floor beside the metric's literal config: a plain streaming read of
+    the same bytes (fltee_debug_read_floor: 16-B non-temporal loads, 8 in flight per lane,
+    the grid swept for its best), over buffers rotated past the 256 MiB Infinity Cache
+    like the cold literal config's inputs.  Best of `reps` trials per grid, in us."""
+    import ctypes as C
+    from fltee import _lib as L
+    lib = L.lib()
+    nbuf = int(1.5 * 256 * 2 ** 20 // max(bytes_per_step, 1)) + 1
+    n16 = (bytes_per_step + 15) // 16
+    bufs = [torch.empty(n16 * 2, dtype=torch.int64, device=device).random_() for _ in range(nbuf)]
+    sink = torch.zeros(8192, dtype=torch.int32, device=device)
+    stream = torch.cuda.current_stream()
+    best = None
+    for blocks in (256, 512, 1024, 2048, 4096):
+        def go(i):
+            assert lib.fltee_debug_read_floor(C.c_void_p(bufs[i % nbuf].data_ptr()), n16 * 16,
+                                              C.c_void_p(sink.data_ptr()), blocks,
+                                              C.c_void_p(stream.cuda_stream)) == 0
+        for _ in range(reps):
+            _, t = time_steps(torch, go, steps, 2 * nbuf, stream)
+            if best is None or t < best[0]:
+                best = (t, blocks)
+    del bufs
+    return dict(us=best[0] * 1e6, blocks=best[1], bytes=n16 * 16, gbs=n16 * 16 / best[0] / 1e9,
+                input_buffers=nbuf, note="fltee_debug_read_floor: streaming read only, cold "
+                                         "(rotated buffers), best grid and trial")
 
 
 def net_stats(torch, call, reps=3):
@@ -500,7 +533,7 @@ def bench_exp5(torch, D, device, reps=5):
                 fl += 1
                 a = EXP5_ALGS[alg]
                 assert E.ecall_fl_init(fl, ids, d, k, 1.12, 1.0, alpha, 1.0, a, 0, 0) == (0, 0)
-                walls = []
+                walls, phases = [], []
                 for r in range(reps + 1):
                     assert E.ecall_start_round(fl, r, n)[:2] == (0, 0)
                     t0 = time.perf_counter()
@@ -509,10 +542,15 @@ def bench_exp5(torch, D, device, reps=5):
                     assert (st, rv) == (0, 0), (alg, st, rv)
                     if r:  # the first call grows the staging buffers
                         walls.append(wall)
+                        phases.append([float(x) for x in tt])
                 t = float(np.mean(walls))
+                ph = np.mean(np.array(phases), axis=0) * 1e3
                 rows.append(dict(dataset=ds, num_users=users, alpha=alpha, n=n, d=d, k=k, alg=alg,
-                                 ms=t * 1e3, ref_ms=ref_s * 1e3, speedup=ref_s / t,
-                                 value=n * k / t, unit="client-params/s"))
+                                 ms=t * 1e3, min_ms=float(np.min(walls)) * 1e3, ref_ms=ref_s * 1e3,
+                                 speedup=ref_s / t, value=n * k / t, unit="client-params/s",
+                                 payload_bytes=n * k * 8,
+                                 phases_ms=dict(load=float(ph[0]), decrypt=float(ph[1]),
+                                                aggregate=float(ph[2]))))
     finally:
         E.destroy()
     return dict(metric="execution_time of one Aggregate ECALL (host wall, server.rs:184-186), "

@@ -94,8 +94,10 @@ void net_account(uint64_t bytes, const char *kernel, hipStream_t s);
 hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float coef, float *out,
                                    const float *client_coef, bool accumulate, uint32_t *status,
                                    hipStream_t s);
+// baseline.rs o_update on sparse records: out[j] = the in-order sum over every record with
+// idx j (+0.0 selected elsewhere), exact for any upload, fixed cost nrec * d
 hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float coef, float *out,
-                                   bool accumulate, uint32_t *status, hipStream_t s);
+                                   bool accumulate, hipStream_t s);
 hipError_t launch_scale(float *out, size_t d, float coef, hipStream_t s);
 hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint32_t *status,
                               hipStream_t s);
@@ -209,14 +211,21 @@ hipError_t launch_fold_sorted(const uint64_t *sorted, size_t n, size_t d, float 
 hipError_t launch_gather_by_keys(const uint64_t *keys, size_t n, const void *rec, uint64_t *dst,
                                  hipStream_t s);
 
-// k_oram.hip: path_oram as a tree Path ORAM (Z = 4, stash 20, next_pow2(d) <= 2^16
-// blocks): the n*k accesses in order, then every tree/stash slot as an 8-B record (idx,
-// value; empty slots idx >= next_pow2(d), unique) in records[oram_slots(d)] for the
-// oblivious readout (advanced's network, n = 1).  tree: oram_slots(d) * 16 bytes.
+// k_oram.hip: path_oram as a tree Path ORAM (Z = 4, stash 20, next_pow2(d) <= 2^22
+// blocks).  Default: oram.rs's own access sequence (d prepare writes, a read and a write per
+// record, d readout reads -> out[i] * coef, or out[i] += with accumulate); lazy: one
+// read-modify-write per record, then every tree/stash slot as an 8-B record (idx, value;
+// empty slots idx >= next_pow2(d), unique) in records[oram_slots(d)] for the oblivious
+// readout (advanced's network, n = 1).  tree: oram_slots(d) * 16 bytes; keys, keys2:
+// next_pow2(oram_accesses()) u64 each (the leaf precompute's sorts).
 size_t oram_slots(size_t d);
 bool oram_supported(size_t d);
-hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, void *tree, uint64_t seed,
-                            uint64_t *records, uint32_t *status, hipStream_t s);
+size_t oram_accesses(size_t nrec, size_t d, bool lazy);
+void set_oram_bucket(int z);
+hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, void *tree,
+                            uint64_t seed, uint64_t *keys, uint64_t *keys2, uint64_t *records,
+                            float coef, bool accumulate, float *out, uint32_t *status,
+                            hipStream_t s);
 
 // k_dp.hip
 hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, size_t n,

@@ -166,11 +166,10 @@ static uint32_t read_status(DeviceCtx *c, uint32_t *st) {
     return FLTEE_SUCCESS;
 }
 
-// Aggregate c->records (n clients x rpc records) with alg into the device out
-// buffer (c->ws_b reused is unsafe: use records tail) and run the exact
-// fallbacks the status word asks for.
-static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t rpc, size_t d,
-                                  size_t k_req, size_t batch, float *d_out, uint64_t seed = 0) {
+// The options aggregate_records gives aggregate() for an ECALL's alg (shared with the
+// staged path below).
+static fltee_device_opts ecall_opts(uint32_t alg, size_t n, size_t rpc, size_t d, size_t k_req,
+                                    size_t batch, uint64_t seed) {
     fltee_device_opts o;
     std::memset(&o, 0, sizeof o);
     o.k_req = k_req;
@@ -179,39 +178,135 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
                       alg == FLTEE_ALG_NON_OBLIVIOUS;
     if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
-    if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default()) o.flags |= FLTEE_OPT_ORAM_TREE;
+    if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_supported(d))
+        o.flags |= FLTEE_OPT_ORAM_TREE;
     if (alg == FLTEE_ALG_NIPS19) o.seed = seed ? seed : next_seed();
     // advanced's fold (advanced.rs:66-101) runs once with halo = n: exact for every run of
     // up to n + 1 entries — every upload whose clients each send distinct indices (n
     // records + the initial entry) — and a run of more (some client repeated an index)
     // is reported by the same pass (fold_run_limit): the call is rejected with 0x2,
-    // like an out-of-range index, instead of rerunning with a wider halo.  The cost is
-    // fixed by the public sizes; no data-dependent relaunch.
-    o.fold_halo = n;
+    // like an out-of-range index, instead of rerunning with a wider halo.  With the
+    // exact-runs policy the halo is the public worst case (every record one index): one
+    // sequential walk, exact for any run.  Either way the cost is fixed by the public
+    // sizes; no data-dependent relaunch.
+    o.fold_halo = exact_runs_default() ? n * rpc + d : n;
+    return o;
+}
+
+// What an ECALL returns for the device status word of one aggregate (aggregate_records'
+// rules); *retry: a dense-sized non_oblivious upload out of position, to rerun sparse.
+static uint32_t status_to_retval(uint32_t dev_st, uint32_t alg, bool *retry) {
+    *retry = false;
+    if (dev_st == 0) return FLTEE_SUCCESS;
+    if (dev_st & FLTEE_DEV_ERR_INDEX_RANGE) return FLTEE_ERROR_INVALID_PARAMETER;
+    if (dev_st & FLTEE_DEV_ERR_ORAM_STASH) return FLTEE_ERROR_UNEXPECTED;
+    if (dev_st & FLTEE_DEV_ERR_DENSE_ORDER) {
+        // a dense-sized upload with a record out of position (not serialize_dense's
+        // layout).  non_oblivious (not oblivious in the reference) reruns it with scatter
+        // semantics; baseline / path_oram, which the enclave runs at a fixed cost, reject
+        // it (0x2) after the one fixed-cost pass: no data-dependent relaunch — the retval
+        // reveals only that the upload was malformed.
+        if (alg != FLTEE_ALG_NON_OBLIVIOUS) return FLTEE_ERROR_INVALID_PARAMETER;
+        *retry = true;
+        return FLTEE_SUCCESS;
+    }
+    if (dev_st & FLTEE_DEV_ERR_FOLD_OVERFLOW) return FLTEE_ERROR_INVALID_PARAMETER;
+    return FLTEE_ERROR_UNEXPECTED;
+}
+
+// Aggregate c->records (n clients x rpc records) with alg into the device out buffer,
+// reading the status word back (one sync) and rerunning only where status_to_retval says.
+static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t rpc, size_t d,
+                                  size_t k_req, size_t batch, float *d_out, uint64_t seed = 0) {
+    fltee_device_opts o = ecall_opts(alg, n, rpc, d, k_req, batch, seed);
+    if (alg == FLTEE_ALG_OPTIMIZED) o.flags &= ~FLTEE_OPT_K_REQ;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (hipMemsetAsync(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         uint32_t st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, c->stream, c->status);
         if (st != FLTEE_SUCCESS) return st;
         uint32_t dev_st = 0;
         if (read_status(c, &dev_st)) return FLTEE_ERROR_UNEXPECTED;
-        if (dev_st == 0) return FLTEE_SUCCESS;
-        if (dev_st & FLTEE_DEV_ERR_INDEX_RANGE) return FLTEE_ERROR_INVALID_PARAMETER;  // enclave panic
-        if (dev_st & FLTEE_DEV_ERR_ORAM_STASH) return FLTEE_ERROR_UNEXPECTED;  // the crate panics
-        if (dev_st & FLTEE_DEV_ERR_DENSE_ORDER) {  // not dense after all: scatter semantics
-            o.flags &= ~FLTEE_OPT_DENSE;
-            continue;
-        }
-        if (dev_st & FLTEE_DEV_ERR_FOLD_OVERFLOW) {
-            if (!flat) return FLTEE_ERROR_INVALID_PARAMETER;  // a run of more than n + 1 entries
-            // flat algorithms: a client repeated an index — the exact sequential sweep
-            const float coef = 1.0f / (float)n;
-            if (aggregate_sparse_sequential(c->records.ptr, n * rpc, d, coef, d_out, false, c->stream))
-                return FLTEE_ERROR_UNEXPECTED;
-            return hipStreamSynchronize(c->stream) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
-        }
-        return FLTEE_ERROR_UNEXPECTED;
+        bool retry = false;
+        st = status_to_retval(dev_st, alg, &retry);
+        if (!retry) return st;
+        o.flags &= ~FLTEE_OPT_DENSE;  // non_oblivious: scatter semantics
     }
     return FLTEE_ERROR_INVALID_PARAMETER;
+}
+
+// Small calls (payload <= kStagedBytes) on one GPU with ONE host synchronisation: the
+// round keys (computed straight into pinned memory) and the ciphertext (one memcpy into
+// it) cross PCIe in one DMA, the AES-CTR kernel and the aggregation follow on the
+// stream, and the f32[d] output comes back in one DMA together with the device status
+// word (it sits right after the output in HBM) — then one stream sync.  The large-payload
+// path (pageable 64 MB chunks with the decryption pipelined under the copies) pays a
+// stream sync per phase; here the fixed cost is the API calls and one round trip.
+// Timers (execution_time_results, lib.rs:280-353): [0] = the host staging + the H2D,
+// [1] = the AES kernel (hipEvents), [2] = the rest of the call (alg 6: [1] = decrypt +
+// aggregate, [2] = 0, lib.rs:425-592).  alg: an ECALL alg, or FLTEE_ALG_OPTIMIZED with
+// batch.
+constexpr size_t kStagedBytes = (size_t)16 << 20;
+
+static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, size_t n,
+                             const uint8_t *enc, size_t bpc, size_t d, size_t k_req, size_t batch,
+                             uint64_t seed, const FLConfig &cfg, float *host_out, float *times) {
+    const double t0 = now_s();
+    const size_t rpc = bpc / 8;
+    const size_t rkb = (n * 44 * 4 + 15) / 16 * 16, cb = n * bpc;
+    const size_t d4 = (d * 4 + 15) / 16 * 16;
+    if (!c->stage.reserve(rkb + cb + 16) || !c->records.reserve(n * rpc * 8 + 16) ||
+        !c->outbuf.reserve(d4 + 16) || !c->pin_in.reserve(rkb + cb + 16) || !c->pin_out.reserve(d4 + 16))
+        return FLTEE_ERROR_OUT_OF_MEMORY;
+    for (auto &ev : c->call_ev)
+        if (!ev && hipEventCreate(&ev) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    uint8_t *pin = (uint8_t *)c->pin_in.ptr;
+    aes128_session_round_keys(ids, n, (uint32_t *)pin);  // session_key_store.rs:21-22
+    if (cb) std::memcpy(pin + rkb, enc, cb);
+    const double t1 = now_s();
+    hipStream_t s = c->stream;
+    uint8_t *stage = (uint8_t *)c->stage.ptr;
+    float *d_out = (float *)c->outbuf.ptr;
+    uint32_t *d_st = (uint32_t *)((uint8_t *)c->outbuf.ptr + d4);
+    if (hipEventRecord(c->call_ev[0], s) != hipSuccess ||
+        hipMemcpyAsync(stage, pin, rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(c->call_ev[1], s) != hipSuccess ||
+        (cb && launch_aes_ctr(stage + rkb, n, bpc, rpc, (const uint32_t *)stage, (uint8_t *)c->records.ptr,
+                              s) != hipSuccess) ||
+        hipEventRecord(c->call_ev[2], s) != hipSuccess)
+        return FLTEE_ERROR_UNEXPECTED;
+    fltee_device_opts o = ecall_opts(alg == FLTEE_ALG_OPTIMIZED ? FLTEE_ALG_ADVANCED : alg, n, rpc, d,
+                                     k_req, batch, seed);
+    if (alg == FLTEE_ALG_OPTIMIZED) o.flags &= ~FLTEE_OPT_K_REQ;
+    uint32_t st = FLTEE_SUCCESS;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, s, d_st);
+        if (st != FLTEE_SUCCESS) return st;
+        if (cfg.dp && launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), s) != hipSuccess)
+            return FLTEE_ERROR_UNEXPECTED;
+        if (hipEventRecord(c->call_ev[3], s) != hipSuccess ||
+            hipMemcpyAsync(c->pin_out.ptr, d_out, d4 + 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return FLTEE_ERROR_UNEXPECTED;
+        bool retry = false;
+        st = status_to_retval(*(const uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg, &retry);
+        if (!retry) break;
+        o.flags &= ~FLTEE_OPT_DENSE;  // non_oblivious: scatter semantics
+    }
+    if (st) return st;
+    std::memcpy(host_out, c->pin_out.ptr, d * 4);
+    float h2d = 0, aes = 0;
+    (void)hipEventElapsedTime(&h2d, c->call_ev[0], c->call_ev[1]);
+    (void)hipEventElapsedTime(&aes, c->call_ev[1], c->call_ev[2]);
+    const float wall = (float)(now_s() - t0);
+    times[0] = (float)(t1 - t0) + h2d * 1e-3f;
+    times[1] = aes * 1e-3f;
+    times[2] = wall - times[0] - times[1];
+    if (alg == FLTEE_ALG_OPTIMIZED) {
+        times[1] += times[2];
+        times[2] = 0;
+    }
+    return FLTEE_SUCCESS;
 }
 
 }  // namespace fltee
@@ -368,7 +463,7 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     double t2 = 0;
     const bool flat = aggregation_alg == FLTEE_ALG_BASELINE || aggregation_alg == FLTEE_ALG_PATH_ORAM ||
                       aggregation_alg == FLTEE_ALG_NON_OBLIVIOUS;
-    const bool tree = aggregation_alg == FLTEE_ALG_PATH_ORAM && oram_tree_default();
+    const bool tree = aggregation_alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_supported(d);
     if (G && flat && !tree && rpc == d && bpc == d * 8) {
         // dense uploads over a multi-GPU eid: every GPU loads and decrypts its own
         // parameter range (group.hip); "Loading" = the parallel H2D, "Decryption" = the
@@ -376,11 +471,14 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         std::vector<uint32_t> rk;
         client_round_keys(client_ids, n, rk);
         st = group_dense_ecall(G, rk.data(), n, encrypted_parameters_data, d, coef, d_out,
-                               &execution_time_results[0], &execution_time_results[1]);
+                               &execution_time_results[0], &execution_time_results[1],
+                               aggregation_alg != FLTEE_ALG_NON_OBLIVIOUS);
         t2 = now_s();
         if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
     }
-    const bool sharded = G && ((aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc) ||
+    // (the exact-runs policy folds on one GPU: one sequential walk of the sorted array)
+    const bool sharded = G && ((aggregation_alg == FLTEE_ALG_ADVANCED && k_req == rpc &&
+                                !exact_runs_default()) ||
                                aggregation_alg == FLTEE_ALG_NIPS19);
     // nips19 draws its seed (Laplace counts, shuffle key) once per call, whichever path
     // runs it, so a multi-GPU eid consumes the seed sequence exactly as one GPU does
@@ -405,6 +503,22 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
         // "Aggregation" = the call minus its load and decrypt phases
         t2 = ta + execution_time_results[0] + execution_time_results[1];
+    }
+    if (st == FLTEE_GROUP_FALLBACK && !G && n * bpc <= kStagedBytes) {
+        // one GPU, a small payload: one DMA each way, one host synchronisation
+        st = staged_ecall(c, aggregation_alg, client_ids, n, encrypted_parameters_data, bpc, d, k_req,
+                          0, seed, cfg, updated_parameters_data, execution_time_results);
+        if (st) {
+            std::memset(updated_parameters_data, 0, d * sizeof(float));
+            std::memset(execution_time_results, 0, 3 * sizeof(float));
+            return fail(st);
+        }
+        if (cfg.verbose)
+            std::printf("[FLTEE CLOCK] Loading %.6f Decryption %.6f Aggregation %.6f seconds\n",
+                        execution_time_results[0], execution_time_results[1], execution_time_results[2]);
+        cfg.round += 1;  // lib.rs:421
+        *retval = FLTEE_SUCCESS;
+        return FLTEE_SUCCESS;
     }
     if (st == FLTEE_GROUP_FALLBACK) {  // (a shape the per-GPU path declines comes here too)
         st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data, bpc,
@@ -469,6 +583,7 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
 
     float t_load = 0, t_dec = 0;
     const double t1 = now_s();
+    const size_t halo6 = exact_runs_default() ? n * k + d : n;  // as aggregate_records
     float *d_out = nullptr;
     if (!c->outbuf.reserve(d * 4 + 16)) return fail(FLTEE_ERROR_OUT_OF_MEMORY);
     d_out = (float *)c->outbuf.ptr;
@@ -484,8 +599,20 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
         in.bpc = k * 8;
         in.t_load = &t_load;
         in.t_dec = &t_dec;
-        st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
+        st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out, halo6);
         execution_time_results[0] = t_load;
+    } else if (!G && n * k * 8 <= kStagedBytes) {
+        // one GPU, a small payload: one DMA each way, one host synchronisation
+        st = staged_ecall(c, FLTEE_ALG_OPTIMIZED, client_ids, n, encrypted_parameters_data_ptr, k * 8, d,
+                          k, optimal_num_of_clients, 0, cfg, updated_parameters_data, execution_time_results);
+        if (st) {
+            std::memset(updated_parameters_data, 0, d * sizeof(float));
+            std::memset(execution_time_results, 0, 3 * sizeof(float));
+            return fail(st);
+        }
+        cfg.round += 1;
+        *retval = FLTEE_SUCCESS;
+        return FLTEE_SUCCESS;
     } else {
         st = load_and_decrypt(c, client_ids, n, encrypted_parameters_data_ptr, k * 8, &t_load, &t_dec);
         if (st) return fail(st);
@@ -493,7 +620,7 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
         if (G) {
             GroupInput in;
             in.root_rec = (const uint64_t *)c->records.ptr;
-            st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out);
+            st = group_optimized(G, in, n, k, d, optimal_num_of_clients, 1.0f / (float)n, d_out, halo6);
         } else {
             st = aggregate_records(c, FLTEE_ALG_OPTIMIZED, n, k, d, k, optimal_num_of_clients, d_out);
         }

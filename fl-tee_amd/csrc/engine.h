@@ -15,6 +15,13 @@ struct Buffer {
     void release();              // hipFree (the owning device must be current)
 };
 
+// grow-only pinned host memory (the ECALL's staging: one DMA each way per call)
+struct HostBuffer {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t bytes);
+};
+
 struct DeviceCtx {
     bool ready = false;
     int device = -1;
@@ -25,6 +32,9 @@ struct DeviceCtx {
     size_t mat_clean = 0, mat_clean_cap = 0;
     void *mat_clean_ptr = nullptr;
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
+    Buffer stage;                                        // small ECALLs: round keys + ciphertext
+    HostBuffer pin_in, pin_out;                          // small ECALLs: pinned staging both ways
+    hipEvent_t call_ev[4] = {};                          // small ECALLs: the phase timers
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel;                               // nips19's selected list
     Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch
@@ -49,6 +59,10 @@ float nips19_threshold(size_t d, size_t k, size_t n);
 // API selects it per call with FLTEE_OPT_ORAM_TREE
 void set_oram_tree(int on);
 bool oram_tree_default();
+// advanced / alg 6 in the ECALLs: the exact fold for any run length at the public
+// worst-case cost (fltee_set_advanced_exact_runs), else runs > n + 1 are rejected
+void set_exact_runs(int on);
+bool exact_runs_default();
 
 fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size_t d, float *out,
                          const fltee_device_opts &o, hipStream_t s, uint32_t *status);
@@ -65,8 +79,6 @@ hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_
 hipError_t advanced_batch(const void *rec, size_t n, size_t k, size_t d, size_t halo, float *out,
                           uint32_t *status, hipStream_t s);
 hipError_t read_device_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out, hipStream_t s);
-fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
-                                           float *out, bool acc, hipStream_t s);
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);
 bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o);
 

@@ -21,8 +21,6 @@
 
 namespace fltee {
 
-hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t d, float *mat,
-                                    uint32_t *status, hipStream_t s);
 hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
                                   bool accumulate, hipStream_t s);
 hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uint32_t *mat,
@@ -115,6 +113,17 @@ bool Buffer::reserve(size_t bytes) {
     return true;
 }
 
+bool HostBuffer::reserve(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    const size_t want = bytes + bytes / 8 + 4096;
+    if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) { ptr = nullptr; return false; }
+    cap = want;
+    return true;
+}
+
 void Buffer::release() {
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
@@ -144,22 +153,24 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
     Plan p;
     const bool dense = (o.flags & FLTEE_OPT_DENSE) != 0;
     const bool clip = (o.flags & FLTEE_OPT_CLIP) != 0;
+    const bool tree = alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE) && oram_supported(d);
     if (clip) {
         p.coef_bytes = n * 4;
-        if (!dense) p.rec_bytes = n * k * 8;
+        if (!dense || tree) p.rec_bytes = n * k * 8;  // the tree reads records: clipped copies
     }
     switch (alg) {
     case FLTEE_ALG_PATH_ORAM:
-        if ((o.flags & FLTEE_OPT_ORAM_TREE) && oram_supported(d)) {
+        if (tree) {
+            const bool lazy = (o.flags & FLTEE_OPT_ORAM_LAZY) != 0;
             const size_t ns = oram_slots(d);
-            p.oram_bytes = ns * 24;
-            p.a_bytes = p.b_bytes = next_pow2_sz(ns + d) * 8;  // the readout network
-            break;
+            p.oram_bytes = ns * (lazy ? 24 : 16);
+            // the leaf precompute's two key arrays; lazy: the readout network too
+            size_t m = next_pow2_sz(oram_accesses(n * k, d, lazy));
+            if (lazy && next_pow2_sz(ns + d) > m) m = next_pow2_sz(ns + d);
+            p.a_bytes = p.b_bytes = m * 8;
         }
-        if (!dense) p.mat_bytes = n * d * 4;
         break;
     case FLTEE_ALG_BASELINE:
-        if (!dense) p.mat_bytes = n * d * 4;
         break;
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (!dense) {
@@ -203,6 +214,9 @@ static bool reserve_plan(DeviceCtx *c, const Plan &p) {
 // bit for bit: test_gpu_parity.py).
 static bool g_radix_order = true;
 void set_radix_order(int on) { g_radix_order = on != 0; }
+static bool g_exact_runs = false;  // the ECALLs' advanced / alg 6: reject runs > n + 1 unless set
+void set_exact_runs(int on) { g_exact_runs = on != 0; }
+bool exact_runs_default() { return g_exact_runs; }
 static bool g_oram_tree = false;  // the ECALLs' path_oram: the sweep unless set
 void set_oram_tree(int on) { g_oram_tree = on != 0; }
 bool oram_tree_default() { return g_oram_tree; }
@@ -383,7 +397,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         if (launch_client_clip_coef(rec, n, k, o.clipping, cf, s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
         ccoef = cf;
-        if (!dense) {
+        if (!dense || (alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE))) {
             if (hipMemcpyAsync(c->ws_rec.ptr, rec, n * k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
                 launch_apply_clip(c->ws_rec.ptr, n, k, cf, s) != hipSuccess)
                 return FLTEE_ERROR_UNEXPECTED;
@@ -395,16 +409,20 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
     switch (alg) {
     case FLTEE_ALG_PATH_ORAM:
         if (o.flags & FLTEE_OPT_ORAM_TREE) {  // the tree Path ORAM (k_oram.hip)
-            if (!oram_supported(d) || n * k > 0xFFFFFFFFull) return FLTEE_ERROR_INVALID_PARAMETER;
+            const bool lazy = (o.flags & FLTEE_OPT_ORAM_LAZY) != 0;
+            if (!oram_supported(d) || oram_accesses(n * k, d, lazy) >= 0x7F000000ull)
+                return FLTEE_ERROR_INVALID_PARAMETER;
             const size_t ns = oram_slots(d);
             uint8_t *tree = (uint8_t *)c->ws_oram.ptr;
-            uint64_t *recs = (uint64_t *)(tree + ns * 16);
+            uint64_t *recs = lazy ? (uint64_t *)(tree + ns * 16) : nullptr;
             const uint64_t seed = o.seed ? o.seed : next_seed();
             e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);  // oram.rs panics
-            if (e == hipSuccess) e = launch_oram_tree(rec, n * k, d, tree, seed, recs, status, s);
-            // the readout: every slot's (idx, value) through advanced's oblivious network
+            if (e == hipSuccess)
+                e = launch_oram_tree(rec, n * k, d, lazy, tree, seed, (uint64_t *)c->ws_a.ptr,
+                                     (uint64_t *)c->ws_b.ptr, recs, coef, acc, out, status, s);
+            // lazy readout: every slot's (idx, value) through advanced's oblivious network
             // (one "client" of ns records: each index at most once, runs of <= 2 entries)
-            if (e == hipSuccess) e = run_advanced(c, recs, 1, ns, d, ns, 1, coef, out, acc, status, s);
+            if (e == hipSuccess && lazy) e = run_advanced(c, recs, 1, ns, d, ns, 1, coef, out, acc, status, s);
             break;
         }
         [[fallthrough]];
@@ -424,13 +442,11 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         } else if (alg == FLTEE_ALG_NON_OBLIVIOUS) {
             e = ordered_fold_records(c, rec, n * k, d, coef, out, acc, status, s);
         } else {
+            // baseline / path_oram on sparse uploads: the ordered sweep (exact for any
+            // upload, a client may repeat an index; fixed cost n*k*d compare-selects)
             if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
                 e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
-            c->mat_clean = 0;  // the rows below overwrite the scatter sentinels
-            if (e == hipSuccess)
-                e = launch_sweep_materialize(rec, n, k, d, (float *)c->ws_mat.ptr, status, s);
-            if (e == hipSuccess)
-                e = launch_rows_accumulate((const float *)c->ws_mat.ptr, n, d, coef, out, acc, s);
+            if (e == hipSuccess) e = launch_sweep_accumulate(rec, n * k, d, coef, out, acc, s);
         }
         break;
     case FLTEE_ALG_ADVANCED: {
@@ -492,14 +508,6 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         std::fprintf(stderr, "[fltee] aggregate(alg %u, n %zu, k %zu, d %zu): %s\n", alg, n, k, d,
                      hipGetErrorString(e));
     return e == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
-}
-
-// Exact fallbacks, run by the ECALL layer after reading the status word.
-fltee_status_t aggregate_sparse_sequential(const void *rec, size_t nrec, size_t d, float coef,
-                                           float *out, bool acc, hipStream_t s) {
-    return launch_sweep_accumulate(rec, nrec, d, coef, out, acc, nullptr, s) == hipSuccess
-               ? FLTEE_SUCCESS
-               : FLTEE_ERROR_UNEXPECTED;
 }
 
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -843,7 +851,17 @@ extern "C" fltee_status_t fltee_dp_noise_device(float *d_out, size_t d, float si
                : FLTEE_ERROR_UNEXPECTED;
 }
 
-namespace fltee { void set_dense_variant(int v); void set_compact_variant(int v); void set_fold_compact(int on); }
+namespace fltee {
+void set_dense_variant(int v); void set_compact_variant(int v); void set_fold_compact(int on);
+hipError_t launch_read_floor(const void *src, size_t bytes, uint32_t *sink, unsigned blocks, hipStream_t s);
+}
+// measurement hook (bench.py): a plain streaming read of `bytes` (16-B multiple) of d_src;
+// d_sink: `blocks` words
+extern "C" int fltee_debug_read_floor(const void *d_src, size_t bytes, void *d_sink, unsigned blocks,
+                                      void *stream) {
+    return fltee::launch_read_floor(d_src, bytes, (uint32_t *)d_sink, blocks, (hipStream_t)stream) ==
+                   hipSuccess ? 0 : 1;
+}
 // tuning hook (not part of the public header)
 extern "C" void fltee_debug_set_dense_variant(int v) { fltee::set_dense_variant(v); }
 // A/B hook: 0 runs advanced's second bitonic sort instead of the compaction network
@@ -858,6 +876,12 @@ extern "C" void fltee_set_path_oram_tree(int on) {
     std::lock_guard<std::recursive_mutex> lk(fltee::api_mutex());
     fltee::set_oram_tree(on);
 }
+extern "C" void fltee_set_advanced_exact_runs(int on) {
+    std::lock_guard<std::recursive_mutex> lk(fltee::api_mutex());
+    fltee::set_exact_runs(on);
+}
+// test hook: blocks a bucket of the tree ORAM takes on eviction (4; 0 forces the stash)
+extern "C" void fltee_debug_set_oram_bucket(int z) { fltee::set_oram_bucket(z); }
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes

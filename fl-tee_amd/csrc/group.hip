@@ -397,7 +397,8 @@ static uint32_t group_records(Group &G, const GroupInput &in, size_t n, size_t r
 // ================================================================ dense =====
 // Parameter-range shard of dense uploads, straight from the host ciphertext.
 uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const uint8_t *enc,
-                           size_t d, float coef, float *d_out_root, float *t_load, float *t_dec) {
+                           size_t d, float coef, float *d_out_root, float *t_load, float *t_dec,
+                           bool reject_order) {
     Group &G = *Gp;
     const int W = G.W;
     std::vector<size_t> p(W + 1);
@@ -458,7 +459,8 @@ uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const u
     if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
     if (t_dec) *t_dec = std::chrono::duration<float>(std::chrono::steady_clock::now() - t1).count();
     for (uint32_t v : st)
-        if (v & FLTEE_DEV_ERR_DENSE_ORDER) return FLTEE_GROUP_FALLBACK;  // not dense: root path
+        if (v & FLTEE_DEV_ERR_DENSE_ORDER)  // not dense: rejected, or the root's scatter path
+            return reject_order ? FLTEE_ERROR_INVALID_PARAMETER : FLTEE_GROUP_FALLBACK;
     for (uint32_t v : st)
         if (v) return FLTEE_ERROR_UNEXPECTED;
     return FLTEE_SUCCESS;
@@ -701,7 +703,7 @@ uint32_t group_nips19(Group *Gp, DeviceCtx *root, const GroupInput &in, size_t n
 
 // ========================================================= optimized (alg 6) =
 uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, size_t d,
-                         size_t batch, float coef, float *d_out_root) {
+                         size_t batch, float coef, float *d_out_root, size_t halo) {
     Group &G = *Gp;
     const int W = G.W;
     if (batch == 0) return FLTEE_ERROR_INVALID_PARAMETER;
@@ -716,7 +718,7 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
     }
     std::vector<const uint64_t *> rec;
     if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
-    const size_t h = n;  // a run of more than n + 1 entries rejects the call (no rerun)
+    const size_t h = halo;  // halo n: a run of more than n + 1 entries rejects the call (no rerun)
     {
         std::vector<P2P> ops;
         std::vector<const uint32_t *> sw;

@@ -13,13 +13,13 @@
 //   access pattern does not depend on the data (every record is read once at
 //   a fixed address), so it is oblivious; idx != position is reported, not
 //   followed (FLTEE_DEV_ERR_DENSE_ORDER).
-// sweep_materialize + rows_accumulate : sparse records, oblivious.  GPU form of
-//   baseline.rs's o_update: every record of client c is compared against every
-//   output slot (LDS broadcast + branch-free select), producing the dense row
-//   mat[c][0..d) of client c; the rows are then summed in client order.  Exact
-//   while a client's indices are distinct (top-k, utils.py:327-354); a client
-//   with a repeated index sets FLTEE_DEV_ERR_FOLD_OVERFLOW and the host reruns
-//   sweep_sequential (one output per lane, all records in order).
+// sweep_ordered : sparse records, oblivious and exact for ANY upload.  GPU form of
+//   baseline.rs's o_update (and oram.rs's output): lane j owns out[j] and walks every
+//   record in upload order, adding the record's value where its idx is j and +0.0
+//   elsewhere (a select, no branch; +0.0 is the identity of a sum that started at +0.0).
+//   The same per-index order as the enclave whatever the data — a client may repeat an
+//   index — so no status word, no rerun: the cost is n*k*d compare-selects, fixed by the
+//   public sizes.
 #include <atomic>
 
 #include "common.h"
@@ -682,47 +682,119 @@ hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float co
 }
 
 // ---------------------------------------------------------------- sparse ---
-// Oblivious sweep, one client per blockIdx.y: row[c][j] = sum of client c's
-// records with idx == j (in the client's order), matches counted.
-constexpr int SW_R = 4;          // outputs per lane
-constexpr int SW_CHUNK = 2048;   // records staged per LDS pass (16 KB)
+// sweep_ordered: one lane per output, every record in upload order.  The records stream
+// through LDS in chunks of SO_CH (each lane loads 16 of them one chunk ahead, 8-B
+// non-temporal loads), and every lane reads each chunk back as 16-B broadcasts (two
+// records per ds_read, the same address for the whole wave: no bank conflict).  Per
+// record and output: one compare, one select, one add — 3 VALU.  The parallelism is the
+// d outputs: 64-lane blocks while d / 64 waves do not fill the chip (MLP-MNIST: 796 waves
+// for 1,024 SIMDs), 256-lane blocks sharing each chunk when there are waves to spare.
+// Positions past nrec read as (u32::MAX, +0.0), which no output j < d matches.
+constexpr int SO_CH = 1024;  // records per LDS chunk (8 KB)
+#ifndef FLTEE_SWEEP_CMPX
+#define FLTEE_SWEEP_CMPX 1
+#endif
 
-__global__ __launch_bounds__(256) void sweep_materialize(const uint2 *__restrict__ rec, size_t k,
-                                                         size_t d, float *__restrict__ mat,
-                                                         uint32_t *status) {
-    __shared__ uint2 tile[SW_CHUNK];
-    const uint32_t c = blockIdx.y;
-    const uint32_t base = (uint32_t)(((size_t)blockIdx.x * 256 + threadIdx.x) * SW_R);
-    const uint2 *src = rec + (size_t)c * k;
-    float acc[SW_R];
-    uint32_t cnt[SW_R];
+template <int NT, bool ACC>
+__global__ __launch_bounds__(NT) void sweep_ordered(const uint2 *__restrict__ rec, uint32_t nrec,
+                                                    uint32_t d, float coef, float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint2 tile[SO_CH];
+    constexpr int PER = SO_CH / NT;  // records each lane stages per chunk
+    const uint32_t t = threadIdx.x;
+    const uint32_t j = blockIdx.x * NT + t;
+    uint2 pf[PER];
+    auto load = [&](uint32_t c0) {
 #pragma unroll
-    for (int i = 0; i < SW_R; ++i) { acc[i] = 0.0f; cnt[i] = 0; }
-    for (size_t c0 = 0; c0 < k; c0 += SW_CHUNK) {
-        const uint32_t m = (uint32_t)((k - c0) < SW_CHUNK ? (k - c0) : SW_CHUNK);
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < m; e += 256) tile[e] = src[c0 + e];
-        __syncthreads();
-        for (uint32_t q = 0; q < m; ++q) {
-            const uint2 r = tile[q];
-            const uint32_t delta = r.x - base;
-            const float v = __uint_as_float(r.y);
+        for (int i = 0; i < PER; ++i) {
+            const uint32_t q = c0 + (uint32_t)i * NT + t;
+            pf[i] = q < nrec ? ld_nt(rec + q) : make_uint2(0xFFFFFFFFu, 0u);
+        }
+    };
+    load(0);
+    float acc = 0.0f;
+    const uint4 *t4 = reinterpret_cast<const uint4 *>(tile);
+    for (uint32_t c0 = 0; c0 < nrec; c0 += SO_CH) {
+        __syncthreads();  // every lane is done reading the previous chunk
 #pragma unroll
-            for (int i = 0; i < SW_R; ++i) {
-                const bool hit = (delta == (uint32_t)i);
-                acc[i] = __fadd_rn(acc[i], hit ? v : 0.0f);
-                cnt[i] += hit;
+        for (int i = 0; i < PER; ++i) tile[i * NT + t] = pf[i];
+        __syncthreads();
+        if (c0 + SO_CH < nrec) load(c0 + SO_CH);
+        // 16 records per step, the next step's reads issued before this step's adds; the
+        // whole 16-B reads are pinned in registers (as one 128-bit tuple each: no copies):
+        // otherwise hipcc turns the select into a load of the value under an EXEC mask of
+        // the matching lanes — a read whose lanes depend on the data, one LDS round trip
+        // per record
+        u32x4_t ra[8], rb[8];
+        auto rd = [&](u32x4_t (&r)[8], int q) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const u32x4_t *>(t4 + q + i);
+        };
+        // 16 records: the selects by hand (hipcc puts every compare in VCC, then needs two
+        // wait states before the select that reads it, and turns selects of loaded values
+        // into loads under an EXEC mask of the matching lanes): four compares into four
+        // SGPR-pair masks, then the four selects, so every mask is read four VALU after it
+        // is written; the adds stay in upload order
+        auto add = [&](const u32x4_t (&r)[8]) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const u32x4_t x = r[2 * g], y = r[2 * g + 1];
+#if FLTEE_SWEEP_CMPX
+                // EXEC-masked adds: v_cmpx sets EXEC to the lanes whose j is the record's
+                // idx, the add runs on those lanes only, EXEC is restored — two VALU per
+                // record instead of three.  The instruction stream and every VALU op's
+                // cost are the same whatever the data (a masked-off lane's slot is
+                // issued all the same); the lanes left out hold acc + 0.0 == acc.
+                uint64_t sv;
+                asm volatile(
+                    "s_mov_b64 %1, exec\n\t"
+                    "v_cmpx_eq_u32_e32 %2, %10\n\t"
+                    "v_add_f32_e32 %0, %0, %3\n\t"
+                    "s_mov_b64 exec, %1\n\t"
+                    "v_cmpx_eq_u32_e32 %4, %10\n\t"
+                    "v_add_f32_e32 %0, %0, %5\n\t"
+                    "s_mov_b64 exec, %1\n\t"
+                    "v_cmpx_eq_u32_e32 %6, %10\n\t"
+                    "v_add_f32_e32 %0, %0, %7\n\t"
+                    "s_mov_b64 exec, %1\n\t"
+                    "v_cmpx_eq_u32_e32 %8, %10\n\t"
+                    "v_add_f32_e32 %0, %0, %9\n\t"
+                    "s_mov_b64 exec, %1"
+                    : "+v"(acc), "=&s"(sv)
+                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w),
+                      "v"(j)
+                    : "vcc");
+#else
+                uint64_t m0, m1, m2, m3;
+                uint32_t t0, t1, t2, t3;
+                asm volatile(
+                    "v_cmp_eq_u32_e64 %0, %8, %16\n\t"
+                    "v_cmp_eq_u32_e64 %1, %10, %16\n\t"
+                    "v_cmp_eq_u32_e64 %2, %12, %16\n\t"
+                    "v_cmp_eq_u32_e64 %3, %14, %16\n\t"
+                    "v_cndmask_b32_e64 %4, 0, %9, %0\n\t"
+                    "v_cndmask_b32_e64 %5, 0, %11, %1\n\t"
+                    "v_cndmask_b32_e64 %6, 0, %13, %2\n\t"
+                    "v_cndmask_b32_e64 %7, 0, %15, %3"
+                    : "=&s"(m0), "=&s"(m1), "=&s"(m2), "=&s"(m3), "=&v"(t0), "=&v"(t1), "=&v"(t2),
+                      "=&v"(t3)
+                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w),
+                      "v"(j));
+                acc = __fadd_rn(acc, __uint_as_float(t0));
+                acc = __fadd_rn(acc, __uint_as_float(t1));
+                acc = __fadd_rn(acc, __uint_as_float(t2));
+                acc = __fadd_rn(acc, __uint_as_float(t3));
+#endif
             }
+        };
+        rd(ra, 0);
+        for (int q = 0; q < SO_CH / 2; q += 16) {
+            rd(rb, q + 8);
+            add(ra);
+            if (q + 16 < SO_CH / 2) rd(ra, q + 16);
+            add(rb);
         }
     }
-    uint32_t dup = 0;
-    float *row = mat + (size_t)c * d;
-#pragma unroll
-    for (int i = 0; i < SW_R; ++i) {
-        if ((size_t)base + i < d) row[base + i] = acc[i];
-        dup |= cnt[i] > 1;
-    }
-    if (dup) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+    if (j < d) out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
 }
 
 // rows [n][d] f32 summed in row order: out[j] = sum_c mat[c][j] (* coef)
@@ -770,37 +842,6 @@ __global__ __launch_bounds__(256) void rows_accumulate_s(const float *__restrict
     out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
 }
 
-// Exact fallback for clients with repeated indices: one output per lane,
-// every record in upload order (the literal o_update loop, parallel over j).
-template <bool ACC>
-__global__ __launch_bounds__(256) void sweep_sequential(const uint2 *__restrict__ rec, size_t nrec,
-                                                        size_t d, float coef,
-                                                        float *__restrict__ out) {
-    __shared__ uint2 tile[SW_CHUNK];
-    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
-    float acc = 0.0f;
-    for (size_t c0 = 0; c0 < nrec; c0 += SW_CHUNK) {
-        const uint32_t m = (uint32_t)((nrec - c0) < SW_CHUNK ? (nrec - c0) : SW_CHUNK);
-        __syncthreads();
-        for (uint32_t e = threadIdx.x; e < m; e += 256) tile[e] = rec[c0 + e];
-        __syncthreads();
-        for (uint32_t q = 0; q < m; ++q) {
-            const uint2 r = tile[q];
-            acc = __fadd_rn(acc, (r.x == (uint32_t)j) ? __uint_as_float(r.y) : 0.0f);
-        }
-    }
-    if (j < d) out[j] = ACC ? __fadd_rn(out[j], acc) : __fmul_rn(acc, coef);
-}
-
-hipError_t launch_sweep_materialize(const void *rec, size_t n, size_t k, size_t d, float *mat,
-                                    uint32_t *status, hipStream_t s) {
-    if (n == 0 || d == 0) return hipSuccess;
-    const unsigned bx = (unsigned)((d + 256 * SW_R - 1) / (256 * SW_R));
-    hipLaunchKernelGGL(sweep_materialize, dim3(bx, (unsigned)n), dim3(256), 0, s,
-                       (const uint2 *)rec, k, d, mat, status);
-    return hipGetLastError();
-}
-
 hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float coef, float *out,
                                   bool accumulate, hipStream_t s) {
     if (d == 0) return hipSuccess;
@@ -826,16 +867,25 @@ hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float co
 }
 
 hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float coef, float *out,
-                                   bool accumulate, uint32_t *status, hipStream_t s) {
-    (void)status;
+                                   bool accumulate, hipStream_t s) {
     if (d == 0) return hipSuccess;
-    const unsigned blocks = (unsigned)((d + 255) / 256);
-    if (accumulate)
-        hipLaunchKernelGGL(sweep_sequential<true>, dim3(blocks), dim3(256), 0, s,
-                           (const uint2 *)rec, nrec, d, coef, out);
-    else
-        hipLaunchKernelGGL(sweep_sequential<false>, dim3(blocks), dim3(256), 0, s,
-                           (const uint2 *)rec, nrec, d, coef, out);
+    if (nrec >= 0xFFFFFFFFull || d >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+    // 256-lane blocks: a block's four waves go to the CU's four SIMDs, one each (64-lane
+    // blocks left SIMDs holding two of them while others idled: 1.8 vs 0.8 ms at MLP-MNIST
+    // n = 30); 64-lane blocks only for a d too small to give every CU a block
+    const bool wide = d >= (size_t)256 * 64;
+    const unsigned blocks = (unsigned)((d + (wide ? 255 : 63)) / (wide ? 256 : 64));
+#define SO_GO(NT_, ACC_)                                                                         \
+    hipLaunchKernelGGL((sweep_ordered<NT_, ACC_>), dim3(blocks), dim3(NT_), 0, s,                \
+                       (const uint2 *)rec, (uint32_t)nrec, (uint32_t)d, coef, out)
+    if (wide) {
+        if (accumulate) SO_GO(256, true);
+        else SO_GO(256, false);
+    } else {
+        if (accumulate) SO_GO(64, true);
+        else SO_GO(64, false);
+    }
+#undef SO_GO
     return hipGetLastError();
 }
 
@@ -850,6 +900,7 @@ hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float
 // the sentinel, sets *dup and the row pass switches (uniformly, same launch) to
 // the in-order sequential sweep over every record.  Traffic: n*k*8 + n*d*4*2 + d*4.
 constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
+constexpr int SW_CHUNK = 2048;  // records staged per LDS pass of the repeated-index path
 
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const uint2 *__restrict__ rec, size_t n,
                                                            size_t k, size_t d,
@@ -974,6 +1025,35 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
 __global__ void scale_kernel(float *out, size_t d, float coef) {
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (j < d) out[j] = __fmul_rn(out[j], coef);
+}
+
+// Measurement only (bench.py: the achievable floor beside the metric's literal config): a
+// plain streaming read of `bytes` with 16-B non-temporal loads, 8 in flight per lane, the
+// words xor-folded so the loads stay (a store to sink only on one fold value).
+__global__ __launch_bounds__(256) void read_floor_kernel(const uint4 *__restrict__ src, size_t n16,
+                                                         uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    const size_t stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        uint4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = ld_nt(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u].x ^ x[u].y ^ x[u].z ^ x[u].w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 x = ld_nt(src + i);
+        acc ^= x.x ^ x.y ^ x.z ^ x.w;
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = threadIdx.x;  // keeps the loads; (almost) never taken
+}
+
+hipError_t launch_read_floor(const void *src, size_t bytes, uint32_t *sink, unsigned blocks,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(read_floor_kernel, dim3(blocks), dim3(256), 0, s, (const uint4 *)src, bytes / 16,
+                       sink);
+    return hipGetLastError();
 }
 
 hipError_t launch_scale(float *out, size_t d, float coef, hipStream_t s) {

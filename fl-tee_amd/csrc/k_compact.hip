@@ -361,8 +361,16 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_PF
 #define FLTEE_FC_PF 0
 #endif
-template <int NT, int PER, int FINAL, int XMAX>
-__global__ __launch_bounds__(NT, FLTEE_FC_BLOCKS > 2 ? FLTEE_FC_BLOCKS * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
+// Round 5: 8,192-record windows (1,024 lanes x 8, one block per CU: 16 waves, <= 128
+// VGPRs) for the wide-halo arrays (C5: Hr = 1,008 against 4,096 records per tile — the
+// window re-read 1.42x the records it compacts, 2.14 GB of PMC traffic against 1.76 GB
+// launch-side): the halo and the H = 511 overlap rows then cost 1.2x.  (512 lanes x 16 at
+// two blocks per CU spills: 112 B of scratch.)  FLTEE_FC_PER16=0 keeps 4,096 (A/B).
+#ifndef FLTEE_FC_PER16
+#define FLTEE_FC_PER16 1
+#endif
+template <int NT, int PER, int FINAL, int XMAX, int BPC = FLTEE_FC_BLOCKS>
+__global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
                                                             uint32_t M, uint32_t d, uint32_t G,
                                                             uint32_t S, uint32_t Hr,
@@ -534,14 +542,17 @@ template <int PER, int F, int X>
 static hipError_t fc_launch(unsigned grid, size_t lds, hipStream_t s, const uint64_t *A, uint64_t *B,
                             size_t L, size_t M, size_t d, uint32_t G, uint32_t S, size_t Hr,
                             uint64_t ntiles, float coef, float *out, uint32_t lim, uint32_t *status) {
-    constexpr int NT = 512;
-    static bool attr = false;  // 26-37 KB of window
+    // PER 16 stands for the 8,192-record window: 1,024 lanes x 8, one block per CU
+    constexpr int NT = PER > 8 ? 1024 : 512;
+    constexpr int BPC = PER > 8 ? 1 : FLTEE_FC_BLOCKS;
+    constexpr int PL = PER > 8 ? 8 : PER;
+    static bool attr = false;  // 26-74 KB of window
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PER, F, X>,
+        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PL, F, X, BPC>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((fold_compact_first<NT, PER, F, X>), dim3(grid), dim3(NT), lds, s, A, B,
+    hipLaunchKernelGGL((fold_compact_first<NT, PL, F, X, BPC>), dim3(grid), dim3(NT), lds, s, A, B,
                        (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles,
                        coef, out, lim, status);
     return hipGetLastError();
@@ -590,21 +601,28 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
             break;
         }
     }
-    const uint32_t CAP = NT * per, S = CAP - H;
+    // a wide halo (two window slots per lane) on an array of >= 2 tiles per block slot:
+    // 8,192-record windows, two blocks per CU (see fold_compact_first)
+    if (FLTEE_FC_PER16 && per == 8 && Hr + 1 > NT && (L + NT * 16 - H - 1) / (NT * 16 - H) >= 2 * 512)
+        per = 16;
+    const uint32_t bpc = per > 8 ? 1u : (uint32_t)FLTEE_FC_BLOCKS;
+    const uint32_t CAP = NT * per, S = CAP - H;  // (per 16: 1,024 lanes x 8)
     const uint64_t ntiles = (L + S - 1) / S;
     const bool last = G == nlev;
-    const unsigned grid = (unsigned)(ntiles < 256u * FLTEE_FC_BLOCKS ? ntiles : 256u * FLTEE_FC_BLOCKS);
+    const unsigned grid = (unsigned)(ntiles < 256u * bpc ? ntiles : 256u * bpc);
     const size_t lds = (Hr + CAP + 1) * 8;
-    // FLTEE_FC_BLOCKS resident blocks per CU must fit the 160 KiB LDS at the largest window
+    // the resident blocks per CU must fit the 160 KiB LDS at the largest window
     static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
-    if (lds * FLTEE_FC_BLOCKS > 160 * 1024) return hipErrorNotSupported;
+    static_assert((1023 + 8 * 1024 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU (8,192 records)");
+    if (lds * bpc > 160 * 1024) return hipErrorNotSupported;
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
-    const bool x1 = Hr + 1 <= NT;  // one window slot past CAP per lane, else two (Hr < 1024)
+    const bool x1 = Hr + 1 <= (per > 8 ? 1024u : NT);  // one window slot past CAP per lane, else two
     const int F = !last ? 0 : (accumulate ? 2 : 1);
     hipError_t e;
     if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
     else if (per == 6) e = fc_dispatch<6>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
-    else e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
+    else if (per == 8) e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
+    else e = fc_dispatch<16>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
     if (e != hipSuccess || last) return e;
     return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);
 }

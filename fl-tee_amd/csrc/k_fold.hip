@@ -197,12 +197,25 @@ uint32_t fold_run_limit(size_t halo) {
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
                              uint32_t *status, hipStream_t s) {
-    const size_t Hr = fold_context(halo);
-    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
     // runs of more than halo + 1 entries are reported, wherever they lie (fold_run_limit)
     const uint32_t lim = fold_run_limit(halo);
     if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
     const size_t span = end - origin;
+    if ((halo + 1 >= span || halo + 1 >= fold_len) && origin == 0 && pbase == 0) {
+        // a halo as long as the array (the exact-runs policy: the public worst case n*k + 1
+        // entries per run): ONE lane folds the whole array from position 0, the enclave's
+        // own sequential walk (advanced.rs:66-101) — exact for any run, span/16 stages
+        // whatever the data.  No halo to re-read, no run-length limit.
+        const size_t C1 = (span + FS_W - 1) / FS_W * FS_W;
+        if (C1 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        net_account((uint64_t)16 * span, "fold_stream_kernel", s);
+        hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
+                           0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
+                           0xFFFFFFFFu, status);
+        return hipGetLastError();
+    }
+    const size_t Hr = fold_context(halo);
+    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
     size_t C = 64;
     while (C < Hr) C <<= 1;
     // keep >= ~1024 waves: shorter chunks re-read more halo but put more loads in flight

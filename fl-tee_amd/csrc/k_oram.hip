@@ -1,40 +1,48 @@
 // k_oram.hip — path_oram as a tree Path ORAM on the GPU (oram.rs:64-118; the mobilecoin
 // PathORAM the enclave instantiates: bucket size Z = 4, stash 20, next_pow2(d) blocks).
 //
-// oram.rs:100-105 runs, for every uploaded record in upload order, oram.read(idx), adds
-// the value, and oram.write(idx) back; then reads blocks 0..d-1 (:111-113) and averages.
-// The blocks start at +0.0 (prepare(), :79-82).  Each ORAM access is one Path ORAM
-// access (Stefanov et al.): look the block's leaf up in the position map and give the
-// block a fresh random leaf; read the path root..leaf of that leaf into the pool (path
-// buckets + stash); take the block out of the pool, add, put it back with its new leaf;
-// evict greedily — every block goes to the deepest bucket of the path it may live in
-// (the buckets its own leaf's path shares with this path), four per bucket — and keep
-// what does not fit in the stash; write the whole path back.
+// The enclave's access sequence (oram.rs), which this runs one access for one access:
+//   prepare()            d writes of 0.0, blocks 0..d-1 (:79-82)
+//   per uploaded record  oram.read(idx), then oram.write(idx, value + val) (:100-105)
+//   readout              d reads, blocks 0..d-1 -> global_params (:111-113), then x 1f32/n
+// = A = 2 n k + 2 d accesses (FLTEE_OPT_ORAM_LAZY instead: one read-modify-write per
+// record, blocks created on first use, and the readout through `advanced`'s oblivious
+// network: n k accesses).  Each is one Path ORAM access (Stefanov et al.): the block's
+// current leaf, a fresh random leaf for it; read the path root..leaf into the pool (path
+// buckets + stash); take the block out (or +0.0: a block never written), put it back
+// with its new value and leaf; evict greedily — every block to the deepest bucket of
+// the path it may live in, four per bucket — keep what does not fit in the stash;
+// write the whole path back.
 //
-// GPU form: ONE persistent wave (the accesses are sequential: each path read needs the
-// previous access's path write; lane j holds pool entries j and 64 + j).  Its LDS holds
-// the position map (u16 leaves, N <= 2^16 blocks) and the stash; the tree of 4 (2N - 1)
-// 16-B slots (idx, leaf, f32 value) lives in HBM.  Obliviousness, as the enclave's (ZeroTrace-style) ORAM has it:
+// The position map.  The whole access sequence is known when the call starts (its
+// blocks are the public positions plus the uploaded indices, its fresh leaves come from
+// Philox4x32-10 under the call's seed), so the leaf each access finds its block under —
+// the fresh leaf of the previous access to the same block, or the block's initial random
+// leaf — is computed up front by two oblivious sorts: the keys (block << 32 | access) in
+// the order of the reference bitonic network (mode 1), each access linked to its
+// predecessor in the sorted order (a fixed-address pass), and the (access << 32 | leaf)
+// pairs sorted back into access order.  Every address in that is a function of the array
+// size (no position map read or written at a secret address: the recursive U32PositionMap
+// of the crate hides the same thing by another ORAM).  The accesses then read their leaf
+// at their own (public) index, so N is bounded by the path fitting the wave (<= 2^22
+// blocks, d up to 4M), not by an LDS map.
+//
+// GPU form of the accesses: ONE persistent wave (they are sequential: each path read
+// needs the previous access's path write; lane j holds pool entries j and 64 + j).  Its
+// LDS holds the stash and a ring of the next accesses' descriptors; the tree of
+// 4 (2N - 1) 16-B slots (idx, leaf, f32 value) lives in HBM.  Obliviousness, as the
+// enclave's (ZeroTrace-style) ORAM has it:
 //  * the HBM trace of an access is one whole path, root to a uniformly random leaf,
 //    written; read, the part of it below the buckets it shares with the previous
-//    access's path (a function of the two public random leaves);
-//  * the position map is read and written at one address per access by every lane of
-//    the wave at once (an LDS broadcast: no bank conflict, the same time for any
-//    address) — it never leaves the workgroup;
+//    accesses' paths (a function of the public random leaves);
 //  * inside the pool every step is branch-free over all Z (L + 1) + 20 entries: the
 //    block is found and taken out by compares and selects, eviction ranks come from
-//    wave ballots, and the new path and stash are GATHERED slot by slot by selects over
-//    every pool entry (fixed LDS addresses), never scattered.
-// Blocks are created lazily: a block not in the pool reads as +0.0, prepare()'s value,
-// and nothing is written for blocks never uploaded (the readout below gives them +0.0).
-// Leaves come from Philox4x32-10 under the call's seed (FLTEE_STREAM_ORAM).
-//
-// Readout (:111-113, d oblivious reads): every tree slot and the stash become one 8-B
-// record (idx, value) — empty slots a unique idx >= N — and `advanced`'s oblivious
-// network (sort, fold, compaction; engine.hip) puts block i's value (or +0.0) at out[i]:
-// each index appears once among the records, so its run is (i, +0.0) + the block, and
-// +0.0 + v == v (a sum that started at +0.0 is never -0.0).  The same bits as the
-// in-order sum of non_oblivious / baseline, and the oracle's fo_path_oram.
+//    wave ballots, and the new path and stash are GATHERED slot by slot through the
+//    register crossbar (ds_bpermute: no LDS bank), never scattered; LDS addresses are
+//    fixed per lane (stash) or the public access index (ring);
+//  * the readout's reads write out[i] at the public position i.
+// The output is the in-order f32 sum of each index's values from +0.0, x 1f32/n — bit for
+// bit the oracle's fo_path_oram (and non_oblivious / baseline).
 #include "common.h"
 
 namespace fltee {
@@ -42,7 +50,11 @@ namespace fltee {
 #define FLTEE_STREAM_ORAM 0x4F52414Du
 constexpr uint32_t kOramZ = 4, kOramStash = 20;
 constexpr uint32_t kOramEmpty = 0xFFFFFFFFu;
-constexpr uint32_t kOramMaxLog = 16;  // position map in LDS as u16 leaves
+constexpr uint32_t kOramMaxLog = 22;  // the path (Z (Lh + 1) + stash <= 128 entries) in one wave;
+                                      // slot offsets < 2^31 (buffer resource)
+// access kinds (the descriptor ring's top bits)
+constexpr uint32_t kOpPrep = 0, kOpRead = 1, kOpWrite = 2, kOpFinal = 3, kOpRmw = 4;
+constexpr uint32_t kOpShift = 28, kBlockMask = (1u << kOpShift) - 1u;
 
 __device__ __forceinline__ uint32_t oram_leaf(uint32_t k0, uint32_t k1, uint32_t ctr, uint32_t mask) {
     uint32_t c[4] = {ctr, FLTEE_STREAM_ORAM, 0u, 0u};
@@ -100,19 +112,68 @@ __device__ __forceinline__ void oram_store_slot(__amdgpu_buffer_rsrc_t rs, uint3
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// rec: nrec records (idx < N checked by the caller's range pass; clamped here);
+// The descriptor of access q (public q; the block of a record access is the record's idx):
+// REF (oram.rs's sequence): q < d prepare block q; then per record r two accesses (read,
+// write of idx_r); then the readout of block q - d - 2 nrec.  LAZY: record q, one RMW.
+__device__ __forceinline__ uint2 oram_desc(const uint2 *__restrict__ rec, uint32_t q, uint32_t nrec,
+                                           uint32_t d, bool ref, uint32_t mask) {
+    if (!ref) {
+        const uint2 r = rec[q];
+        return make_uint2((r.x & mask) | (kOpRmw << kOpShift), r.y);
+    }
+    if (q < d) return make_uint2(q | (kOpPrep << kOpShift), 0u);
+    const uint32_t u = q - d;
+    if (u < 2u * nrec) {
+        const uint2 r = rec[u >> 1];
+        return make_uint2((r.x & mask) | (((u & 1u) ? kOpWrite : kOpRead) << kOpShift), r.y);
+    }
+    return make_uint2((u - 2u * nrec) | (kOpFinal << kOpShift), 0u);
+}
+
+// Leaf precompute (see the header): keys[q] = block(q) << 32 | q for q < A, ~0 past it.
+__global__ void oram_keys_kernel(const uint2 *__restrict__ rec, uint32_t nrec, uint32_t d, uint32_t A,
+                                 uint32_t MA, uint32_t mask, int ref, uint64_t *__restrict__ keys) {
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < MA; q += gridDim.x * 256) {
+        uint64_t k = ~0ull;
+        if (q < A) {
+            const uint32_t a = oram_desc(rec, q, nrec, d, ref != 0, mask).x & kBlockMask;
+            k = ((uint64_t)a << 32) | q;
+        }
+        keys[q] = k;
+    }
+}
+
+// sorted (block, access) pairs -> (access << 32 | the leaf its block is found under): the
+// fresh leaf of the previous access to the block (the pair before it), else the block's
+// initial leaf.  Reads positions p - 1 and p: fixed addresses.
+__global__ void oram_link_kernel(const uint64_t *__restrict__ sorted, uint32_t A, uint32_t MA,
+                                 uint32_t k0, uint32_t k1, uint32_t mask, uint64_t *__restrict__ out) {
+    for (uint32_t p = blockIdx.x * 256 + threadIdx.x; p < MA; p += gridDim.x * 256) {
+        uint64_t v = ~0ull;
+        if (p < A) {
+            const uint64_t k = sorted[p], kp = p ? sorted[p - 1] : ~0ull;
+            const uint32_t blk = (uint32_t)(k >> 32);
+            const bool seen = p > 0 && (uint32_t)(kp >> 32) == blk;
+            const uint32_t x = oram_leaf(k0, k1, seen ? (uint32_t)kp : A + blk, mask);
+            v = ((uint64_t)(uint32_t)k << 32) | x;
+        }
+        out[p] = v;
+    }
+}
+
+// rec: the uploaded records (idx < N checked by the caller's range pass; masked here);
+// xs[q]: the leaf access q finds its block under (low word; oram_link + the sort back);
 // tree: 4 (2N - 1) slots (all empty on entry) followed by the 20 stash slots (written at
-// the end for the readout).  One wave: lane j holds pool entries j and 64 + j (the path
-// slots first, then the stash), as (idx, leaf, value) words — plain registers, never an
-// indexed array (which would go to scratch).
-// Per access, after its own path is in registers: the leaf of the access TWO ahead is read
-// (after this access's position-map write, so a repeated index sees its new leaf; the
-// next access's fresh leaf when both are the same block) and its path loads are issued,
-// to land during this access and the next; the buckets a path shares with the previous
-// one (the top levels: l <= Lh - bitlen(x ^ x')) are taken from that access's output, those
-// it shares with the one before only from that one's output (kept in registers), and only
-// the rest are loaded.  Each output lives in the same lanes (slot l*Z + z of any path).
-// A lane only ever stores and reloads its own slots, so program order orders them.
+// the end for the lazy readout).  One wave: lane j holds pool entries j and 64 + j (the
+// path slots first, then the stash), as (idx, leaf, value) words — plain registers, never
+// an indexed array (which would go to scratch).
+// Per access, after its own path is in registers: the path of the access TWO ahead has
+// its loads issued (its leaf is xs[q + 2]), to land during this access and the next; the
+// buckets a path shares with the previous one (the top levels: l <= Lh - bitlen(x ^ x'))
+// are taken from that access's output, those it shares with the one before only from
+// that one's output (kept in registers), and only the rest are loaded.  Each output lives
+// in the same lanes (slot l*Z + z of any path).  A lane only ever stores and reloads its
+// own slots, so program order orders them.
 // The eviction: every block's rank by (deepest legal level, pool index) from one ballot
 // pair per level (mbcnt), the rank each slot receives from the per-level counts (uniform),
 // the pool entry holding that rank by matching its 7 bits against one ballot per bit;
@@ -120,27 +181,33 @@ __device__ __forceinline__ void oram_store_slot(__amdgpu_buffer_rsrc_t rs, uint3
 // register crossbar: no LDS bank, so the same time for any pattern).  All lane-parallel
 // selects over fixed ballots: no per-slot scalar search (round 4: 1,810 SALU per access
 // before, `profiles/r04/oram_sq.txt`).
+// zlim (debug, default 4): blocks a bucket may take on eviction (0 forces the stash).
+template <bool REF, bool ACC>
 __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__ rec,
-                                                       uint32_t nrec, uint32_t Lh,
-                                                       uint4 *__restrict__ tree, uint32_t k0,
-                                                       uint32_t k1, uint32_t *status) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+                                                       uint32_t nrec, uint32_t d, uint32_t A,
+                                                       const uint64_t *__restrict__ xs,
+                                                       uint32_t Lh, uint4 *__restrict__ tree,
+                                                       uint32_t k0, uint32_t k1, uint32_t zlim,
+                                                       float coef, float *__restrict__ out,
+                                                       uint32_t *status) {
+    __shared__ __attribute__((aligned(16))) uint4 st[kOramStash];  // the stash
+    __shared__ uint2 rb[128];     // descriptors of the accesses in flight: a ring of 128
+    __shared__ uint32_t lb[128];  // their fresh leaves
+    __shared__ uint32_t xb[128];  // and the leaves their blocks are found under
     const uint32_t N = 1u << Lh, mask = N - 1u;
     const uint32_t P = kOramZ * (Lh + 1), POOL = P + kOramStash;
-    uint4 *st = reinterpret_cast<uint4 *>(smem);                   // the stash: kOramStash entries
-    uint2 *rb = reinterpret_cast<uint2 *>(st + kOramStash);        // records: a ring of 128
-    uint32_t *lb = reinterpret_cast<uint32_t *>(rb + 128);         // and their new leaves
-    uint16_t *pm = reinterpret_cast<uint16_t *>(lb + 128);         // N leaves
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t trs =
         __builtin_amdgcn_make_buffer_rsrc((void *)tree, (short)0, (int)(kOramZ * (2u * N - 1u) * 16u), 0x00020000);
-    for (uint32_t i = lane; i < N; i += 64) pm[i] = (uint16_t)oram_leaf(k0, k1, nrec + i, mask);
     if (lane < kOramStash) st[lane] = make_uint4(kOramEmpty, 0u, 0u, 0u);
-    // records q0 .. q0 + 63 into their half of the ring (a broadcast read per access
-    // afterwards): the record loads are waited for once per 64 accesses, off the access path
+    // accesses q0 .. q0 + 63 into their half of the ring (read by broadcast afterwards):
+    // the loads are waited for once per 64 accesses, off the access path
     auto batch = [&](uint32_t q0) {
-        rb[(q0 + lane) & 127u] = q0 + lane < nrec ? rec[q0 + lane] : make_uint2(0u, 0u);
-        lb[(q0 + lane) & 127u] = oram_leaf(k0, k1, q0 + lane, mask);
+        const uint32_t q = q0 + lane;
+        const bool ok = q < A;
+        rb[q & 127u] = ok ? oram_desc(rec, q, nrec, d, REF, mask) : make_uint2(0u, 0u);
+        lb[q & 127u] = oram_leaf(k0, k1, q, mask);
+        xb[q & 127u] = ok ? (uint32_t)xs[q] : 0u;
     };
     batch(0);
     batch(64);
@@ -154,21 +221,20 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
     // the deepest level the paths to leaves u and v share
     auto top = [&](uint32_t u, uint32_t v) { return Lh - (32u - (uint32_t)__clz((int)(u ^ v))); };
     uint32_t over = 0;
+    float last = 0.0f;  // REF: the value the read before a write returned (oram.rs:101-103)
     const OramLane none = {kOramEmpty, 0u, 0u, kOramEmpty, 0u, 0u};
     // cur: access q's path; nxt1: the loads of access q+1's path (its buckets not shared
     // with the paths of q or q-1); keep: access q-1's output
     OramLane cur = none, nxt1 = none, keep = none;
     uint32_t x = 0, x1 = 0, xp = 0;  // the leaves of accesses q, q+1, q-1
-    if (nrec) {
-        x = pm[rb[0].x & mask];  // every lane reads the same words: broadcasts
+    if (A) {
+        x = xb[0];
         oram_load_path(trs, x, Lh, lane, p0, p1, cur);
         xp = x;  // no access -1: its buckets are never taken (top(xp, x1) = top(x, x1))
         x1 = x;
     }
-    if (nrec > 1) {
-        // access 1's leaf, as the position map will hold it after access 0's update
-        const uint32_t ra = rb[0].x & mask, rb1 = rb[1].x & mask;
-        x1 = rb1 == ra ? lb[0] : (uint32_t)pm[rb1];
+    if (A > 1) {
+        x1 = xb[1];
         const uint32_t t01 = top(x, x1);
         oram_load_path(trs, x1, Lh, lane, p0 && lev0 > t01, p1 && lev1 > t01, nxt1);
     }
@@ -181,11 +247,10 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
     // wait for it) is ever made.
     auto access = [&](uint32_t q, OramLane &nin, OramLane &nout) {
         const uint2 r = rb[q & 127u];
-        const uint32_t a = r.x & mask;
+        const uint32_t a = r.x & kBlockMask, op = r.x >> kOpShift;
         const float w = __uint_as_float(r.y);
         const uint32_t nleaf = lb[q & 127u];
-        if (lane == 0) pm[a] = (uint16_t)nleaf;  // the block's fresh leaf
-        if ((q & 63u) == 0 && q) {  // records q + 64 .. q + 127 into the half q - 64 .. q - 1 left
+        if ((q & 63u) == 0 && q) {  // accesses q + 64 .. q + 127 into the half q - 64 .. q - 1 left
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             batch(q + 64);
@@ -193,15 +258,12 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
-        // two accesses ahead: access q+2's leaf (after this access's position-map write;
-        // access q+1's own fresh leaf when it is the same block) and its path's loads — only
-        // the buckets it shares with neither path q nor path q+1 (which come from those
-        // accesses' outputs; which levels is a function of the public leaves).  A load then
-        // has a whole access more to land, and never waits behind the stores of the
-        // buckets just written.
-        const bool more2 = q + 2 < nrec;
-        const uint32_t an1 = rb[(q + 1) & 127u].x & mask, an2 = rb[(q + 2) & 127u].x & mask;
-        const uint32_t x2 = more2 ? (an2 == an1 ? lb[(q + 1) & 127u] : (uint32_t)pm[an2]) : x1;
+        // two accesses ahead: access q+2's path loads — only the buckets it shares with
+        // neither path q nor path q+1 (which come from those accesses' outputs; which
+        // levels is a function of the public leaves).  A load then has a whole access more
+        // to land, and never waits behind the stores of the buckets just written.
+        const bool more2 = q + 2 < A;
+        const uint32_t x2 = more2 ? xb[(q + 2) & 127u] : x1;
         const uint32_t sk2 = max(top(x1, x2), top(x, x2));
         oram_load_path(trs, x2, Lh, lane, more2 && p0 && lev0 > sk2, more2 && p1 && lev1 > sk2, nout);
         // the pool: this path (registers) and the stash (LDS)
@@ -214,7 +276,7 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
             const uint4 e = v1 ? st[s1i] : make_uint4(kOramEmpty, 0u, 0u, 0u);
             a1 = e.x, l1 = e.y, w1 = e.z;
         }
-        // read: the block (at most one entry holds it), or +0.0
+        // the block (at most one entry holds it), or +0.0 (never written)
         const bool m0 = a0 == a, m1 = a1 == a;
         // the holder's value by one readlane at the ballot's lowest set bit (uniform), not a
         // 6-step shuffle reduction (each step a crossbar round trip)
@@ -224,8 +286,15 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         const uint32_t hl1 = (uint32_t)__builtin_ffsll((long long)bm1) - 1u;
         const uint32_t vb0 = (uint32_t)__builtin_amdgcn_readlane((int)w0, (int)(hl0 & 63u));
         const uint32_t vb1 = (uint32_t)__builtin_amdgcn_readlane((int)w1, (int)(hl1 & 63u));
-        const uint32_t vb = bm0 ? vb0 : vb1;
-        const float nv = __fadd_rn(found ? __uint_as_float(vb) : 0.0f, w);
+        const float fv = found ? __uint_as_float(bm0 ? vb0 : vb1) : 0.0f;
+        // the value the block keeps (the access kind is public: a function of q)
+        float nv = fv;                                  // read / readout
+        if (op == kOpPrep) nv = 0.0f;                   // prepare(): write 0.0
+        if (op == kOpRead) last = fv;                   // oram.read(idx)
+        if (op == kOpWrite) nv = __fadd_rn(last, w);    // oram.write(idx, read + val)
+        if (op == kOpRmw) nv = __fadd_rn(fv, w);        // LAZY: one access per record
+        if (REF && op == kOpFinal && lane == 0)         // global_params[i] = oram.read(i)
+            out[a] = ACC ? __fadd_rn(out[a], fv) : __fmul_rn(fv, coef);
         a0 = m0 ? kOramEmpty : a0;
         a1 = m1 ? kOramEmpty : a1;
         // write: the block with its new leaf into the first free entry
@@ -235,7 +304,7 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         const bool i0 = fi == lane, i1 = fi == 64u + lane;
         a0 = i0 ? a : a0, l0 = i0 ? nleaf : l0, w0 = i0 ? __float_as_uint(nv) : w0;
         a1 = i1 ? a : a1, l1 = i1 ? nleaf : l1, w1 = i1 ? __float_as_uint(nv) : w1;
-        // eviction: the deepest level each block may take on this path (lm), four per
+        // eviction: the deepest level each block may take on this path (lm), zlim (4) per
         // bucket, deepest first.  The blocks ranked by (lm descending, pool index): level
         // l then takes the next min(4, #(lm >= l) - placed) ranks, the stash the rest —
         // the greedy's count at every level, whichever blocks it picks, so the same
@@ -259,7 +328,7 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
             rank0 = e0 ? before + below0 : rank0;
             rank1 = e1 ? before + c0 + below1 : rank1;
             before += c0 + (uint32_t)__popcll(mv1);
-            const uint32_t pl = min(kOramZ, before - placed);
+            const uint32_t pl = min(zlim, before - placed);
             // level l's first rank and count, kept in lane l
             tfirst = lane == (uint32_t)l ? placed : tfirst;
             tcount = lane == (uint32_t)l ? pl : tcount;
@@ -355,11 +424,11 @@ __global__ __launch_bounds__(64) void oram_tree_kernel(const uint2 *__restrict__
         x1 = x2;
     };
     OramLane nxt2 = none;
-    for (uint32_t q = 0; q < nrec; q += 2) {
+    for (uint32_t q = 0; q < A; q += 2) {
         access(q, nxt1, nxt2);
-        if (q + 1 < nrec) access(q + 1, nxt2, nxt1);
+        if (q + 1 < A) access(q + 1, nxt2, nxt1);
     }
-    // the stash, after the tree, for the readout
+    // the stash, after the tree, for the lazy readout
     if (lane < kOramStash) tree[(size_t)kOramZ * (2u * N - 1u) + lane] = st[lane];
     if (__ballot(over != 0) && lane == 0) atomicOr(status, FLTEE_DEV_ERR_ORAM_STASH);
 }
@@ -379,6 +448,9 @@ __global__ void oram_records_kernel(const uint4 *__restrict__ tree, size_t ns, u
     }
 }
 
+static uint32_t g_oram_zlim = kOramZ;  // fltee_debug_set_oram_bucket (tests: force the stash)
+void set_oram_bucket(int z) { g_oram_zlim = z < 0 ? 0u : (z > (int)kOramZ ? kOramZ : (uint32_t)z); }
+
 size_t oram_slots(size_t d) {
     const size_t N = next_pow2_sz(d ? d : 1);
     return kOramZ * (2 * N - 1) + kOramStash;
@@ -386,27 +458,52 @@ size_t oram_slots(size_t d) {
 
 bool oram_supported(size_t d) { return next_pow2_sz(d ? d : 1) <= ((size_t)1 << kOramMaxLog); }
 
-hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, void *tree, uint64_t seed,
-                            uint64_t *records, uint32_t *status, hipStream_t s) {
-    if (!oram_supported(d) || nrec > 0xFFFFFFFFull) return hipErrorInvalidValue;
+size_t oram_accesses(size_t nrec, size_t d, bool lazy) { return lazy ? nrec : 2 * nrec + 2 * d; }
+
+hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, void *tree,
+                            uint64_t seed, uint64_t *keys, uint64_t *keys2, uint64_t *records,
+                            float coef, bool accumulate, float *out, uint32_t *status,
+                            hipStream_t s) {
+    const size_t A = oram_accesses(nrec, d, lazy);
+    if (!oram_supported(d) || A >= 0x7FFFFFFFull - ((size_t)1 << kOramMaxLog)) return hipErrorInvalidValue;
     const size_t N = next_pow2_sz(d ? d : 1);
-    const uint32_t Lh = log2_pow2(N);
+    const uint32_t Lh = log2_pow2(N), mask = (uint32_t)N - 1u;
     const size_t ns = oram_slots(d);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     size_t blocks = (ns + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(oram_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4 *)tree, ns);
-    const size_t lds = kOramStash * 16 + 128 * 8 + 128 * 4 + N * 2;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)oram_tree_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
+    if (A == 0) {
+        if (lazy)
+            hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                               (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
+        return hipGetLastError();
     }
-    hipLaunchKernelGGL(oram_tree_kernel, dim3(1), dim3(64), lds, s, (const uint2 *)rec,
-                       (uint32_t)nrec, Lh, (uint4 *)tree, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       status);
-    hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
+    // the leaves: keys sorted by (block, access), linked, sorted back by access
+    const size_t MA = next_pow2_sz(A);
+    size_t kb = (MA + 255) / 256;
+    if (kb > 65536) kb = 65536;
+    hipLaunchKernelGGL(oram_keys_kernel, dim3((unsigned)kb), dim3(256), 0, s, (const uint2 *)rec,
+                       (uint32_t)nrec, (uint32_t)d, (uint32_t)A, (uint32_t)MA, mask, lazy ? 0 : 1, keys);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = bitonic_sort(keys, MA, 1, 0, s, A);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(oram_link_kernel, dim3((unsigned)kb), dim3(256), 0, s, keys, (uint32_t)A,
+                       (uint32_t)MA, k0, k1, mask, keys2);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = bitonic_sort(keys2, MA, 1, 0, s, A);
+    if (e != hipSuccess) return e;
+#define OT_GO(REF_, ACC_)                                                                          \
+    hipLaunchKernelGGL((oram_tree_kernel<REF_, ACC_>), dim3(1), dim3(64), 0, s, (const uint2 *)rec, \
+                       (uint32_t)nrec, (uint32_t)d, (uint32_t)A, (const uint64_t *)keys2, Lh,       \
+                       (uint4 *)tree, k0, k1, g_oram_zlim, coef, out, status)
+    if (lazy) OT_GO(false, false);
+    else if (accumulate) OT_GO(true, true);
+    else OT_GO(true, false);
+#undef OT_GO
+    if (lazy)
+        hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                           (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ OPT_ACCUMULATE = 0x8
 OPT_NO_AVERAGE = 0x10
 OPT_K_REQ = 0x20
 OPT_ORAM_TREE = 0x40
+OPT_ORAM_LAZY = 0x80
 
 
 class DeviceOpts(ctypes.Structure):
@@ -92,6 +93,7 @@ SIGNATURES = {
     "fltee_ordered_list_device": (_U32, [_P, _S, _S, _F, _P, _P]),
     "fltee_debug_set_seed": (None, [_U64]),
     "fltee_set_path_oram_tree": (None, [ctypes.c_int]),
+    "fltee_set_advanced_exact_runs": (None, [ctypes.c_int]),
     "fltee_version": (ctypes.c_char_p, []),
     "fltee_device_init_multi": (_U32, [_P, ctypes.c_int, _P]),
     "fltee_device_count": (ctypes.c_int, [_U64]),
@@ -99,6 +101,8 @@ SIGNATURES = {
 EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_aes_block": (None, [_P, _P, _P]),
     "fltee_debug_set_dense_variant": (None, [ctypes.c_int]),
+    "fltee_debug_set_oram_bucket": (None, [ctypes.c_int]),
+    "fltee_debug_read_floor": (ctypes.c_int, [_P, _S, _P, ctypes.c_uint, _P]),
     "fltee_debug_network_plan": (_S, [_U32, _U32, _U32, ctypes.c_int, _P, _S]),
     "fltee_debug_pad_units": (None, [_U32] * 8 + [_P]),
     "fltee_debug_set_advanced_compaction": (None, [ctypes.c_int]),
@@ -129,7 +133,10 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
                 "(the aggregation path has no CPU fallback)")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        ab = bool(os.environ.get("FLTEE_LIB"))  # an A/B build of an older source may lack a hook
         for name, (res, args) in {**SIGNATURES, **EXTRA_SIGNATURES}.items():
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

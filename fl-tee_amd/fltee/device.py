@@ -38,11 +38,11 @@ def unpack_records(rec):
 
 def opts(*, dense=False, dp=False, clip=False, accumulate=False, no_average=False, sigma=1.12,
          clipping=1.0, seed=0, k_req=None, batch=0, n_avg=0, fold_halo=0, status=None,
-         oram_tree=False):
+         oram_tree=False, oram_lazy=False):
     o = L.DeviceOpts()
     o.flags = ((L.OPT_DENSE if dense else 0) | (L.OPT_DP if dp else 0) | (L.OPT_CLIP if clip else 0)
                | (L.OPT_ACCUMULATE if accumulate else 0) | (L.OPT_NO_AVERAGE if no_average else 0)
-               | (L.OPT_ORAM_TREE if oram_tree else 0))
+               | (L.OPT_ORAM_TREE if oram_tree else 0) | (L.OPT_ORAM_LAZY if oram_lazy else 0))
     o.sigma, o.clipping, o.seed = sigma, clipping, seed
     if k_req is not None:
         o.flags |= L.OPT_K_REQ

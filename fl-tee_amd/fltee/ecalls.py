@@ -114,3 +114,11 @@ def set_path_oram_tree(on):
     """aggregation_alg 5 through the ECALLs: the tree Path ORAM (oram.rs:64-118) when on, the
     output-equivalent oblivious sweep (default) when off (fltee_set_path_oram_tree)."""
     L.lib().fltee_set_path_oram_tree(1 if on else 0)
+
+
+def set_advanced_exact_runs(on):
+    """aggregation_alg 1 and 6 through the ECALLs when some index has a run of more than
+    n + 1 entries (a client repeated an index): off (default) rejects the call with 0x2
+    after the one fixed-cost fold; on folds any run exactly, as advanced.rs:66-101 does,
+    at the public worst-case cost (fltee_set_advanced_exact_runs)."""
+    L.lib().fltee_set_advanced_exact_runs(1 if on else 0)

@@ -155,8 +155,14 @@ fltee_status_t ecall_client_size_optimized_secure_aggregation(
                                       (advanced.rs:70 uses the REQUEST's k; 0 when
                                       fl_main.py sends dense uploads without --alpha) */
 #define FLTEE_OPT_ORAM_TREE 0x40u  /* path_oram as a tree Path ORAM (oram.rs:64-118: Z = 4,
-                                      stash 20, next_pow2(d) <= 2^16 blocks) instead of the
+                                      stash 20, next_pow2(d) <= 2^22 blocks) running oram.rs's
+                                      access sequence (d prepare writes, read + write per
+                                      record, d readout reads) instead of the
                                       output-equivalent oblivious sweep */
+#define FLTEE_OPT_ORAM_LAZY 0x80u  /* with ORAM_TREE: one read-modify-write access per record,
+                                      blocks created on first use, readout by an oblivious
+                                      sort of the tree's slots (n*k accesses instead of
+                                      2*n*k + 2*d) */
 
 typedef struct fltee_device_opts {
     uint32_t flags;     /* FLTEE_OPT_* */
@@ -321,10 +327,17 @@ fltee_status_t fltee_ordered_list_device(const void *d_list, size_t lc, size_t d
 
 /* Test hooks: deterministic RNG seed for sampling / nips19 / DP (0 = off). */
 /* The ECALLs' path_oram (aggregation_alg 5): on = the tree Path ORAM of oram.rs:64-118
- * (Z = 4, stash 20, next_pow2(d) <= 2^16 blocks; k_oram.hip), off (default) = the
- * output-equivalent oblivious sweep.  Both give the in-order sum bit for bit.  The device
- * API selects it per call with FLTEE_OPT_ORAM_TREE. */
+ * (Z = 4, stash 20, next_pow2(d) blocks, oram.rs's access sequence; k_oram.hip) where
+ * next_pow2(d) <= 2^22, the sweep beyond; off (default) = the output-equivalent oblivious
+ * sweep.  Both give the in-order sum bit for bit.  The device API selects it per call
+ * with FLTEE_OPT_ORAM_TREE. */
 void fltee_set_path_oram_tree(int on);
+/* The ECALLs' advanced and alg 6 when some index has a run of more than n + 1 entries
+ * (a client repeated an index inside its upload; fl_main.py's top-k never does):
+ * off (default) = the call is rejected with 0x2 after the one fixed-cost fold pass;
+ * on = the enclave's exact fold for ANY run length (advanced.rs:66-101), at the public
+ * worst-case cost: one sequential walk of the whole sorted array whatever the data. */
+void fltee_set_advanced_exact_runs(int on);
 void fltee_debug_set_seed(uint64_t seed);
 /* Library build/version string. */
 const char *fltee_version(void);

@@ -14,11 +14,14 @@ idx = torch.argsort(torch.rand(n, d, generator=g, device="cuda"), dim=1)[:, :k].
 vals = torch.randn(n, k, generator=g, device="cuda") * 0.01
 rec = (idx | (vals.view(torch.int32).to(torch.int64) << 32)).reshape(-1).contiguous()
 out = torch.empty(d, dtype=torch.float32, device="cuda")
-for r in range(3):
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    D.aggregate(5, rec, n, k, d, out=out, oram_tree=True, seed=3 + r)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    print(f"n={n} k={k} d={d}: {t * 1e3:.2f} ms, {t * 1e6 / (n * k):.3f} us/access", flush=True)
+for lazy in (False, True):
+    A = n * k if lazy else 2 * n * k + 2 * d  # oram.rs's sequence: d + 2 n k + d accesses
+    for r in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        D.aggregate(5, rec, n, k, d, out=out, oram_tree=True, oram_lazy=lazy, seed=3 + r)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        print(f"{'lazy' if lazy else 'ref '} n={n} k={k} d={d}: {A} accesses, {t * 1e3:.2f} ms, "
+              f"{t * 1e6 / A:.3f} us/access", flush=True)
 assert D.status() == 0

@@ -181,3 +181,60 @@ def test_group_nips19_declined_shape_same_seed(enclaves, oracle, w):
     c = dict(client_ids=ids, d=d, k=k, n=n, name=f"tiny_nips19_{w}")
     one = run(enclaves[1], c, 2, enc)
     assert np.array_equal(one.view(np.uint32), run(enclaves[w], c, 2, enc).view(np.uint32))
+
+
+def test_group_exact_runs_policy_and_dense_order(enclaves, oracle):
+    """fltee_set_advanced_exact_runs(1): the long run above is folded exactly on every eid
+    (the one-GPU sequential walk; the group path declines) and alg 6 likewise — the
+    oracle's advanced bit for bit.  Dense-sized uploads out of position: baseline and
+    path_oram reject with 0x2 on every eid (fixed cost), non_oblivious reruns exactly."""
+    from fltee import _lib as L
+    from fltee.ecalls import set_advanced_exact_runs, set_debug_seed
+    rng = np.random.default_rng(5)
+    n, k, d = 6, 700, 900
+    ids = np.arange(600, 600 + n, dtype=np.uint32)
+    recs = []
+    for i in range(n):
+        w = np.zeros(k, dtype=oracle.WEIGHT)
+        w["idx"] = rng.permutation(d)[:k]
+        w["val"] = rng.normal(0, 0.01, k).astype(np.float32)
+        if i == 2:
+            w["idx"][:300] = 11  # a run of ~300 entries
+        recs.append(w)
+    allw = np.concatenate(recs)
+    enc = oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
+    ref, st = oracle.advanced(k, allw, d, n)
+    assert st == 0
+    set_advanced_exact_runs(True)
+    try:
+        for w in (1, 2, 8):
+            c = dict(client_ids=ids, d=d, k=k, n=n, name=f"exact{w}")
+            out = run(enclaves[w], c, 1, enc)
+            assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), w
+            o6 = run(enclaves[w], c, 6, enc, batch=4)
+            assert np.array_equal(o6.view(np.uint32), run(enclaves[1], c, 6, enc, batch=4).view(np.uint32))
+    finally:
+        set_advanced_exact_runs(False)
+    # dense-sized, out of position
+    d2 = 640
+    plain = []
+    for _ in ids:
+        p = np.zeros(d2, dtype=oracle.WEIGHT)
+        p["idx"] = rng.permutation(d2)
+        p["val"] = rng.normal(0, 1, d2).astype(np.float32)
+        plain.append(p)
+    enc2 = oracle.encrypt_clients(ids, [p.tobytes() for p in plain])
+    exp, _ = oracle.non_oblivious(np.concatenate(plain), d2, n)
+    for w in (1, 2, 8):
+        for alg in (3, 4, 5):
+            E = enclaves[w]
+            _fl[0] += 1
+            set_debug_seed(SEED)
+            assert E.ecall_fl_init(_fl[0], ids, d2, d2, 1.12, 1.0, 0.1, 1.0, alg, 0, 0) == (0, 0)
+            assert E.ecall_start_round(_fl[0], 0, n)[:2] == (0, 0)
+            st, rv, out, _ = E.ecall_secure_aggregation(_fl[0], 0, ids, enc2, d2, d2, alg)
+            set_debug_seed(0)
+            if alg == 4:
+                assert (st, rv) == (0, 0) and np.array_equal(out.view(np.uint32), exp.view(np.uint32))
+            else:
+                assert (st, rv) == (0, L.ERROR_INVALID_PARAMETER) and not out.any()

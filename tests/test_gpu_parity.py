@@ -115,14 +115,38 @@ def test_sparse_bit_exact(dev, oracle, n, d, k, alg):
     assert st == 0 and bits_equal(out, ref)
 
 
-def test_sparse_repeated_index_flagged(dev):
+@pytest.mark.parametrize("alg", [3, 4, 5])
+def test_sparse_repeated_index_exact(dev, alg):
+    # baseline / path_oram's ordered sweep and non_oblivious's scatter: exact, no flag
     idx = np.array([1, 1, 2, 3], np.uint32)
     rec = cuda_records(dev, idx, np.ones(4, np.float32))
-    dev.aggregate(3, rec, 2, 2, 8)
-    assert dev.status() & 0x4                      # baseline sweep: needs the sequential rerun
-    out = dev.aggregate(4, rec, 2, 2, 8).cpu().numpy()  # non_oblivious handles it exactly
+    out = dev.aggregate(alg, rec, 2, 2, 8).cpu().numpy()
     assert dev.status() == 0
     assert out.tolist() == [0, 1.0, 0.5, 0.5, 0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("n,d,k", [(3, 700, 300), (30, 50890, 5089), (5, 70000, 3000), (2, 1_100_000, 200)])
+@pytest.mark.parametrize("alg", [3, 5])
+def test_sweep_ordered_repeats_bit_exact(dev, oracle, n, d, k, alg):
+    """The ordered sweep (baseline / path_oram on sparse uploads) against the oracle's
+    in-order sum with heavy repeats inside clients (runs of up to k of one index), the
+    64-lane and 256-lane block shapes, partial chunks, accumulate."""
+    import torch
+    rng = np.random.default_rng(n * 7 + k)
+    idx = rng.integers(0, min(d, 97), n * k).astype(np.uint32)  # many repeats
+    idx[::3] = rng.integers(0, d, len(idx[::3])).astype(np.uint32)
+    val = rng.normal(0, 1, n * k).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    out = dev.aggregate(alg, rec, n, k, d).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.non_oblivious(oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+    prev = torch.from_numpy(rng.normal(0, 1, d).astype(np.float32)).cuda()
+    acc = prev.clone()
+    dev.aggregate(alg, rec, n, k, d, out=acc, accumulate=True)
+    assert dev.status() == 0
+    sums, _ = oracle.non_oblivious(oracle.as_weights(idx, val), d, 1)
+    assert bits_equal(acc.cpu().numpy(), prev.cpu().numpy() + sums)
 
 
 def test_non_oblivious_scatter_repeat_flag_is_per_call(dev, oracle):

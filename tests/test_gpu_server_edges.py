@@ -105,9 +105,12 @@ def test_single_client_dense(enclave, oracle, alg):
     assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
 
 
-def test_dense_out_of_order_falls_back_to_scatter(enclave, oracle):
-    # k == d but the records are permuted: the dense kernel reports it and the
-    # ECALL layer reruns the scatter semantics (still bit-exact)
+def test_dense_out_of_order(enclave, oracle):
+    # k == d but the records are permuted.  non_oblivious (a plain scatter in the
+    # reference): the dense kernel reports it and the ECALL reruns with scatter semantics
+    # (bit-exact).  baseline / path_oram (fixed-cost in the reference): rejected with 0x2
+    # after the one fixed-cost pass, no data-dependent relaunch — where the
+    # reference would return the in-order sum the oracle computes here.
     rng = np.random.default_rng(4)
     d = 500
     ids = np.array([1, 2, 3], np.uint32)
@@ -118,14 +121,21 @@ def test_dense_out_of_order_falls_back_to_scatter(enclave, oracle):
     enc = oracle.encrypt_clients(ids, plain)
     for alg in (3, 4, 5):
         (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 80 + alg, ids, d, d, alg, enc)
-        assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref)
+        assert st == 0 and ost == 0 and ref.any()  # the reference's defined result
+        if alg == 4:
+            assert rv == 0 and bits_equal(out, ref)
+        else:
+            assert rv == 0x2 and not out.any()
 
 
 def test_repeated_index_within_client(enclave, oracle):
-    # a client repeats an index: baseline's oblivious sweep reruns sequentially (exact);
-    # advanced's one fold (halo n) sees index 3 with n + 2 entries (two from client 1,
-    # one from client 2, the initial entry) and the call is rejected with 0x2 (DESIGN §7:
-    # fixed cost, no rerun); with client 2 not sending 3 every run fits: exact
+    # a client repeats an index: baseline / path_oram's ordered sweep is exact for any
+    # upload (fixed cost); advanced's one fold (halo n) sees index 3 with n + 2 entries (two
+    # from client 1, one from client 2, the initial entry) and the call is rejected with
+    # 0x2 (fixed cost, no rerun) — the reference returns the oracle's `ref`,
+    # which the exact-runs policy gives bit for bit; with client 2 not sending 3 every run
+    # fits: exact by default
+    from fltee.ecalls import set_advanced_exact_runs
     ids = np.array([1, 2], np.uint32)
     w1 = oracle.as_weights(np.array([3, 3, 5], np.uint32), np.array([0.1, 0.2, 0.3], np.float32))
     w2 = oracle.as_weights(np.array([3, 4, 5], np.uint32), np.array([1e-8, 0.5, 0.7], np.float32))
@@ -133,7 +143,13 @@ def test_repeated_index_within_client(enclave, oracle):
     for alg in (1, 3, 4, 5):
         (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 90 + alg, ids, 8, 3, alg, enc)
         if alg == 1:
-            assert (st, rv, ost) == (0, 0x2, 0) and not out.any()
+            assert (st, rv, ost) == (0, 0x2, 0) and not out.any() and ref[3] != 0
+            set_advanced_exact_runs(True)
+            try:
+                (st, rv, out, _), (ost, ref2, _) = both(enclave, oracle, 190 + alg, ids, 8, 3, alg, enc)
+            finally:
+                set_advanced_exact_runs(False)
+            assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref2) and bits_equal(ref, ref2)
             continue
         assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref), alg
     w2 = oracle.as_weights(np.array([2, 4, 5], np.uint32), np.array([1e-8, 0.5, 0.7], np.float32))
