@@ -138,7 +138,8 @@ def compact_line(full):
                              "client_producers_ms": _r(nr["client_producers"]["ms"])}
     ot = full.get("oram_tree")
     if ot and ot.get("rows"):
-        line["oram_tree"] = {f"n{r['n']}_k{r['k']}": {"ms": _r(r["ms"]), "ref_x": _r(r["speedup"], 3)}
+        line["oram_tree"] = {f"n{r['n']}_k{r['k']}": {"ms": _r(r["ms"]), "accesses": r["accesses"],
+                                                     "ref_x": _r(r["speedup"], 3)}
                              for r in ot["rows"]}
     if full.get("detail"):
         line["detail"] = full["detail"]

@@ -254,23 +254,28 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     const size_t rpc = bpc / 8;
     const size_t rkb = (n * 44 * 4 + 15) / 16 * 16, cb = n * bpc;
     const size_t d4 = (d * 4 + 15) / 16 * 16;
-    if (!c->stage.reserve(rkb + cb + 16) || !c->records.reserve(n * rpc * 8 + 16) ||
-        !c->outbuf.reserve(d4 + 16) || !c->pin_in.reserve(rkb + cb + 16) || !c->pin_out.reserve(d4 + 16))
+    // one device buffer [out: d4][status: 16][round keys: rkb][ciphertext: cb]: the H2D
+    // covers status .. ciphertext (the status word arrives as zeros: no memset launch),
+    // the D2H covers out .. status
+    if (!c->stage.reserve(d4 + 16 + rkb + cb + 16) || !c->records.reserve(n * rpc * 8 + 16) ||
+        !c->pin_in.reserve(16 + rkb + cb + 16) || !c->pin_out.reserve(d4 + 16))
         return FLTEE_ERROR_OUT_OF_MEMORY;
-    for (auto &ev : c->call_ev)
-        if (!ev && hipEventCreate(&ev) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    for (int i = 0; i < 3; ++i)
+        if (!c->call_ev[i] && hipEventCreate(&c->call_ev[i]) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     uint8_t *pin = (uint8_t *)c->pin_in.ptr;
-    aes128_session_round_keys(ids, n, (uint32_t *)pin);  // session_key_store.rs:21-22
-    if (cb) std::memcpy(pin + rkb, enc, cb);
+    std::memset(pin, 0, 16);                                   // the status word
+    aes128_session_round_keys(ids, n, (uint32_t *)(pin + 16));  // session_key_store.rs:21-22
+    if (cb) std::memcpy(pin + 16 + rkb, enc, cb);
     const double t1 = now_s();
     hipStream_t s = c->stream;
     uint8_t *stage = (uint8_t *)c->stage.ptr;
-    float *d_out = (float *)c->outbuf.ptr;
-    uint32_t *d_st = (uint32_t *)((uint8_t *)c->outbuf.ptr + d4);
+    float *d_out = (float *)stage;
+    uint32_t *d_st = (uint32_t *)(stage + d4);
+    const uint8_t *d_rk = stage + d4 + 16, *d_cipher = d_rk + rkb;
     if (hipEventRecord(c->call_ev[0], s) != hipSuccess ||
-        hipMemcpyAsync(stage, pin, rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(stage + d4, pin, 16 + rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipEventRecord(c->call_ev[1], s) != hipSuccess ||
-        (cb && launch_aes_ctr(stage + rkb, n, bpc, rpc, (const uint32_t *)stage, (uint8_t *)c->records.ptr,
+        (cb && launch_aes_ctr(d_cipher, n, bpc, rpc, (const uint32_t *)d_rk, (uint8_t *)c->records.ptr,
                               s) != hipSuccess) ||
         hipEventRecord(c->call_ev[2], s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
@@ -279,13 +284,12 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     if (alg == FLTEE_ALG_OPTIMIZED) o.flags &= ~FLTEE_OPT_K_REQ;
     uint32_t st = FLTEE_SUCCESS;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        if (attempt && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, s, d_st);
         if (st != FLTEE_SUCCESS) return st;
         if (cfg.dp && launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
-        if (hipEventRecord(c->call_ev[3], s) != hipSuccess ||
-            hipMemcpyAsync(c->pin_out.ptr, d_out, d4 + 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (hipMemcpyAsync(c->pin_out.ptr, d_out, d4 + 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
         bool retry = false;
@@ -430,9 +434,14 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     DeviceCtx *c = eid_ctx(eid);
     if (!c) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
     const size_t d = num_of_parameters;
-    std::memset(updated_parameters_data, 0, d * sizeof(float));  // Enclave_t.c:626
+    // Enclave_t.c:626 zero-fills [out]: every successful path writes all of it, so the
+    // zeros are written where a call fails (200 KB at MLP-MNIST: ~10 us saved per call)
     std::memset(execution_time_results, 0, 3 * sizeof(float));
-    auto fail = [&](uint32_t st) { *retval = st; return FLTEE_SUCCESS; };
+    auto fail = [&](uint32_t st) {
+        std::memset(updated_parameters_data, 0, d * sizeof(float));
+        *retval = st;
+        return FLTEE_SUCCESS;
+    };
     auto it = g_cfg.find(fl_id);
     if (it == g_cfg.end()) return fail(FLTEE_ERROR_UNEXPECTED);
     FLConfig &cfg = it->second;
@@ -569,9 +578,12 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
     DeviceCtx *c = eid_ctx(eid);
     if (!c) return FLTEE_ERROR_INVALID_ENCLAVE_ID;
     const size_t d = num_of_parameters, k = num_of_sparse_parameters, n = client_size;
-    std::memset(updated_parameters_data, 0, d * sizeof(float));
     std::memset(execution_time_results, 0, 3 * sizeof(float));
-    auto fail = [&](uint32_t st) { *retval = st; return FLTEE_SUCCESS; };
+    auto fail = [&](uint32_t st) {  // [out] zero-filled where the call fails (see above)
+        std::memset(updated_parameters_data, 0, d * sizeof(float));
+        *retval = st;
+        return FLTEE_SUCCESS;
+    };
     auto it = g_cfg.find(fl_id);
     if (it == g_cfg.end()) return fail(FLTEE_ERROR_UNEXPECTED);
     FLConfig &cfg = it->second;

@@ -32,9 +32,9 @@ struct DeviceCtx {
     size_t mat_clean = 0, mat_clean_cap = 0;
     void *mat_clean_ptr = nullptr;
     Buffer cipher, records, round_keys, outbuf;         // ECALL staging
-    Buffer stage;                                        // small ECALLs: round keys + ciphertext
+    Buffer stage;                                        // small ECALLs: out, status, keys, ciphertext
     HostBuffer pin_in, pin_out;                          // small ECALLs: pinned staging both ways
-    hipEvent_t call_ev[4] = {};                          // small ECALLs: the phase timers
+    hipEvent_t call_ev[3] = {};                          // small ECALLs: the phase timers
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel;                               // nips19's selected list
     Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch

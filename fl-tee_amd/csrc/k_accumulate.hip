@@ -691,9 +691,8 @@ hipError_t launch_dense_accumulate(const void *rec, size_t n, size_t d, float co
 // for 1,024 SIMDs), 256-lane blocks sharing each chunk when there are waves to spare.
 // Positions past nrec read as (u32::MAX, +0.0), which no output j < d matches.
 constexpr int SO_CH = 1024;  // records per LDS chunk (8 KB)
-#ifndef FLTEE_SWEEP_CMPX
-#define FLTEE_SWEEP_CMPX 1
-#endif
+// (Round 5, rejected: EXEC-masked adds — v_cmpx + v_add + EXEC restore, two VALU per
+// record — 2.06 vs 1.22 ms at MLP-MNIST n = 30: each EXEC write stalls the next VALU.)
 
 template <int NT, bool ACC>
 __global__ __launch_bounds__(NT) void sweep_ordered(const uint2 *__restrict__ rec, uint32_t nrec,
@@ -734,57 +733,51 @@ __global__ __launch_bounds__(NT) void sweep_ordered(const uint2 *__restrict__ re
         // into loads under an EXEC mask of the matching lanes): four compares into four
         // SGPR-pair masks, then the four selects, so every mask is read four VALU after it
         // is written; the adds stay in upload order
+        // 16 records: the compare / select / add of each record by hand, software-pipelined
+        // (hipcc puts every compare in VCC, then needs two wait states before the select
+        // that reads it, chains the adds back to back, and turns selects of loaded values
+        // into loads under an EXEC mask of the matching lanes).  Steady state, record i:
+        // compare i + 2 (its own SGPR-pair mask), select i, add i - 1 — every mask is read
+        // four instructions after it is written and consecutive adds of the chain stand
+        // two instructions apart; the adds stay in upload order.
+        auto add8 = [&](const u32x4_t &a0, const u32x4_t &a1, const u32x4_t &a2, const u32x4_t &a3) {
+            uint64_t m0, m1, m2;
+            uint32_t t0, t1;
+            asm volatile(
+                "v_cmp_eq_u32_e64 %[m0], %[i0], %[j]\n\t"
+                "v_cmp_eq_u32_e64 %[m1], %[i1], %[j]\n\t"
+                "v_cmp_eq_u32_e64 %[m2], %[i2], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t0], 0, %[v0], %[m0]\n\t"
+                "v_cmp_eq_u32_e64 %[m0], %[i3], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t1], 0, %[v1], %[m1]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
+                "v_cmp_eq_u32_e64 %[m1], %[i4], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t0], 0, %[v2], %[m2]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
+                "v_cmp_eq_u32_e64 %[m2], %[i5], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t1], 0, %[v3], %[m0]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
+                "v_cmp_eq_u32_e64 %[m0], %[i6], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t0], 0, %[v4], %[m1]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
+                "v_cmp_eq_u32_e64 %[m1], %[i7], %[j]\n\t"
+                "v_cndmask_b32_e64 %[t1], 0, %[v5], %[m2]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
+                "v_cndmask_b32_e64 %[t0], 0, %[v6], %[m0]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
+                "v_cndmask_b32_e64 %[t1], 0, %[v7], %[m1]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t1]"
+                : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [t0] "=&v"(t0),
+                  [t1] "=&v"(t1)
+                : [i0] "v"(a0.x), [v0] "v"(a0.y), [i1] "v"(a0.z), [v1] "v"(a0.w), [i2] "v"(a1.x),
+                  [v2] "v"(a1.y), [i3] "v"(a1.z), [v3] "v"(a1.w), [i4] "v"(a2.x), [v4] "v"(a2.y),
+                  [i5] "v"(a2.z), [v5] "v"(a2.w), [i6] "v"(a3.x), [v6] "v"(a3.y), [i7] "v"(a3.z),
+                  [v7] "v"(a3.w), [j] "v"(j));
+        };
         auto add = [&](const u32x4_t (&r)[8]) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const u32x4_t x = r[2 * g], y = r[2 * g + 1];
-#if FLTEE_SWEEP_CMPX
-                // EXEC-masked adds: v_cmpx sets EXEC to the lanes whose j is the record's
-                // idx, the add runs on those lanes only, EXEC is restored — two VALU per
-                // record instead of three.  The instruction stream and every VALU op's
-                // cost are the same whatever the data (a masked-off lane's slot is
-                // issued all the same); the lanes left out hold acc + 0.0 == acc.
-                uint64_t sv;
-                asm volatile(
-                    "s_mov_b64 %1, exec\n\t"
-                    "v_cmpx_eq_u32_e32 %2, %10\n\t"
-                    "v_add_f32_e32 %0, %0, %3\n\t"
-                    "s_mov_b64 exec, %1\n\t"
-                    "v_cmpx_eq_u32_e32 %4, %10\n\t"
-                    "v_add_f32_e32 %0, %0, %5\n\t"
-                    "s_mov_b64 exec, %1\n\t"
-                    "v_cmpx_eq_u32_e32 %6, %10\n\t"
-                    "v_add_f32_e32 %0, %0, %7\n\t"
-                    "s_mov_b64 exec, %1\n\t"
-                    "v_cmpx_eq_u32_e32 %8, %10\n\t"
-                    "v_add_f32_e32 %0, %0, %9\n\t"
-                    "s_mov_b64 exec, %1"
-                    : "+v"(acc), "=&s"(sv)
-                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w),
-                      "v"(j)
-                    : "vcc");
-#else
-                uint64_t m0, m1, m2, m3;
-                uint32_t t0, t1, t2, t3;
-                asm volatile(
-                    "v_cmp_eq_u32_e64 %0, %8, %16\n\t"
-                    "v_cmp_eq_u32_e64 %1, %10, %16\n\t"
-                    "v_cmp_eq_u32_e64 %2, %12, %16\n\t"
-                    "v_cmp_eq_u32_e64 %3, %14, %16\n\t"
-                    "v_cndmask_b32_e64 %4, 0, %9, %0\n\t"
-                    "v_cndmask_b32_e64 %5, 0, %11, %1\n\t"
-                    "v_cndmask_b32_e64 %6, 0, %13, %2\n\t"
-                    "v_cndmask_b32_e64 %7, 0, %15, %3"
-                    : "=&s"(m0), "=&s"(m1), "=&s"(m2), "=&s"(m3), "=&v"(t0), "=&v"(t1), "=&v"(t2),
-                      "=&v"(t3)
-                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(y.x), "v"(y.y), "v"(y.z), "v"(y.w),
-                      "v"(j));
-                acc = __fadd_rn(acc, __uint_as_float(t0));
-                acc = __fadd_rn(acc, __uint_as_float(t1));
-                acc = __fadd_rn(acc, __uint_as_float(t2));
-                acc = __fadd_rn(acc, __uint_as_float(t3));
-#endif
-            }
+            add8(r[0], r[1], r[2], r[3]);
+            add8(r[4], r[5], r[6], r[7]);
         };
         rd(ra, 0);
         for (int q = 0; q < SO_CH / 2; q += 16) {

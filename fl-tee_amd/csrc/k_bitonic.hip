@@ -183,6 +183,76 @@ __device__ __forceinline__ bool keyed_swap(uint32_t kb, uint32_t dq) {
     return (int32_t)((kb ^ dq) * 0x9E3779B1u) < 0;
 }
 
+// The keyed comparator read from a table (round 5, FLTEE_KEYED_TABLE).  With kb = p0 ^
+// dir ^ key and dq = q << dlog (p0 has zeros at dq's bits, dq < 2^31): kb & dq = key & dq,
+// so (kb ^ dq) * K = kb * K + C(dq) with C(dq) = keyed_c(key, dq) — one product per group
+// and step (X) and, per compare-exchange, one v_add of a per-(step, q) constant and the
+// sign test, instead of a v_xor, a half-rate v_mul_lo_u32 and the sign test: 6 VALU issue
+// slots per compare-exchange instead of 9.  The constants of every step a network can run
+// — T[ilog][jlog][lv][q] = keyed_c(step_key(seed, ilog, jlog), q << (jlog - lv)), the
+// group's steps lv = 0..3 at distance 2^(jlog - lv) — sit in a per-device table of 256 KB
+// built for the network's seed before its first pass (keyed_table_prepare, stream-
+// ordered), and a step's 16 constants come in as one scalar load (s_load_dwordx16) into
+// SGPRs: no VALU, no LDS.  Every address is a function of (ilog, jlog, lv) — public — and
+// the bits are the same (a ring identity mod 2^32).  Groups of more than 16 records (the
+// register passes of 5 and 6 steps) keep the direct form.
+// Measured and REJECTED (off by default): C4 8.45 vs 7.85 ms, bit-identical
+// (`profiles/r05/ab/ab5_keyed_table_c4_rejected.jsonl`).  The asm has a quarter of the
+// multiplies (222 vs 846 v_mul_lo_u32 in the first pass), but every scalar load is counted
+// in the same lgkm counter as the LDS reads and returns out of order, so each use of a row
+// waits for ALL outstanding LDS reads (lgkmcnt(0): 116 such waits in the pass against 63
+// in the index sort's) — the LDS rounds lose their overlap.
+#ifndef FLTEE_KEYED_TABLE
+#define FLTEE_KEYED_TABLE 0
+#endif
+__device__ const uint32_t *g_keyed_tab;  // this device's table (set once per device)
+typedef __attribute__((address_space(4))) const uint32_t kt_u32;  // scalar (constant) loads
+__device__ __forceinline__ const kt_u32 *keyed_row(uint32_t ilog, uint32_t jlog, uint32_t lv) {
+    return (const kt_u32 *)g_keyed_tab + ((((ilog & 31u) << 5) | (jlog & 31u)) * 4u + lv) * 16u;
+}
+constexpr uint32_t kKeyedTabEntries = 32u * 32u * 4u * 16u;
+
+__global__ void keyed_table_kernel(uint32_t *__restrict__ tab, uint32_t seed) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kKeyedTabEntries) return;
+    const uint32_t q = i & 15u, lv = (i >> 4) & 3u, jlog = (i >> 6) & 31u, ilog = i >> 11;
+    uint32_t c = 0;
+    if (lv <= jlog) c = keyed_c(shuffle_step_key(seed, ilog, jlog), q << (jlog - lv));
+    tab[i] = c;
+}
+
+struct KeyedTab {
+    uint32_t *ptr = nullptr;
+    uint32_t seed = 0;
+    bool valid = false;
+};
+static KeyedTab g_kt[64];
+
+// the table for `seed` on the current device, ahead of the network's launches on s (a
+// device's networks run on one stream at a time: the library's calls are serialised)
+static hipError_t keyed_table_prepare(uint32_t seed, hipStream_t s) {
+    if (!FLTEE_KEYED_TABLE) return hipSuccess;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0 || dev >= 64) return e != hipSuccess ? e : hipErrorInvalidDevice;
+    KeyedTab &t = g_kt[dev];
+    if (!t.ptr) {
+        e = hipMalloc(&t.ptr, kKeyedTabEntries * 4);
+        if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_keyed_tab), &t.ptr, sizeof(t.ptr));
+        if (e != hipSuccess) {
+            t.ptr = nullptr;
+            return e;
+        }
+        t.valid = false;
+    }
+    if (t.valid && t.seed == seed) return hipSuccess;
+    hipLaunchKernelGGL(keyed_table_kernel, dim3(kKeyedTabEntries / 256), dim3(256), 0, s, t.ptr, seed);
+    e = hipGetLastError();
+    t.seed = seed;
+    t.valid = e == hipSuccess;
+    return e;
+}
+
 // Run steps lv = R-1..0 (distance 2^(dlog+lv)) of stage ilog on one group of 2^R
 // records held in v[], whose first record sits at global position p0.  The group
 // spans 2^(dlog+R) <= 2^ilog aligned positions, so the direction bit (l & i) == 0
@@ -198,7 +268,11 @@ __device__ __forceinline__ void group_steps(uint64_t (&v)[1 << R], uint32_t p0, 
         const uint32_t key = MODE == 2 ? shuffle_step_key(seed, ilog, dlog + lv) : 0u;
         const uint32_t X = (MODE == 2 && FLTEE_KEYED_SPLIT) ? (p0 ^ key) * 0x9E3779B1u : 0u;
         const uint32_t kb = pdir ^ key;
+        constexpr bool kTab = MODE == 2 && FLTEE_KEYED_TABLE && R <= 4;
+        const uint32_t XT = kTab ? kb * 0x9E3779B1u : 0u;
+        const kt_u32 *row = kTab ? keyed_row(ilog, dlog + (uint32_t)lv, (uint32_t)lv) : nullptr;
         auto decide = [&](int q, int qm) -> bool {
+            if constexpr (kTab) return (int32_t)(XT + row[q]) < 0;
             if constexpr (MODE == 2 && FLTEE_KEYED_SPLIT)
                 return asc ^ ((int32_t)(X + keyed_c(key, (uint32_t)q << dlog)) < 0);
             if constexpr (MODE == 2 && FLTEE_KEYED_DIRFOLD) return keyed_swap(kb, (uint32_t)q << dlog);
@@ -2019,6 +2093,10 @@ static hipError_t sort_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_t
     const TileCfg c = make_cfg(mlog, slog);
     if (!g_pad_skip) valid = 0;
     hipError_t e;
+    if constexpr (MODE == 2) {
+        e = keyed_table_prepare(seed, s);
+        if (e != hipSuccess) return e;
+    }
     if (c.tlog <= 6) {  // tiles of <= 64 records: every stage is one register pass
         for (uint32_t ilog = 1; ilog <= slog; ++ilog) {
             e = launch_global<MODE>(data, mlog, ilog, ilog - 1, (int)ilog, seed, s, pbase,
@@ -2048,6 +2126,10 @@ static hipError_t merge_impl(uint64_t *data, size_t m, uint32_t seed, hipStream_
                              uint32_t ilog, uint32_t pbase) {
     const uint32_t mlog = log2_pow2(m);
     if (mlog == 0) return hipSuccess;
+    if constexpr (MODE == 2) {
+        const hipError_t e = keyed_table_prepare(seed, s);
+        if (e != hipSuccess) return e;
+    }
     const TileCfg c = make_cfg(mlog, mlog);
     if (c.tlog <= 6)
         return launch_global<MODE>(data, mlog, ilog, mlog - 1, (int)mlog, seed, s, pbase);
@@ -2132,6 +2214,10 @@ static hipError_t sort_gen_impl(uint64_t *data, size_t m, uint32_t seed, const S
     const TileCfg c0 = make_cfg(mlog, mlog);
     if (c0.tlog <= 6) return hipErrorNotSupported;
     if (sink.cnt && !last_pass_is_direct_merge(m)) return hipErrorNotSupported;
+    if constexpr (MODE == 2) {
+        const hipError_t e = keyed_table_prepare(seed, s);
+        if (e != hipSuccess) return e;
+    }
     // the padded array's records (advanced: records ++ initial entries; nips19: records ++
     // dummies); past them only (u32::MAX, +0.0) pads
     const uint64_t nvalid = (uint64_t)g.nrec + (GEN == 1 ? (uint64_t)g.d : (uint64_t)g.d * g.tf);
@@ -2227,6 +2313,10 @@ hipError_t bitonic_steps_range(uint64_t *data, size_t m, uint32_t mode, uint32_t
     if (m > ((size_t)1 << 29)) return hipErrorInvalidValue;
     const uint32_t mlog = log2_pow2(m);
     if (jtop >= mlog || jbot > jtop || jtop >= ilog) return hipErrorInvalidValue;
+    if (mode == 2) {
+        const hipError_t e = keyed_table_prepare(seed, s);
+        if (e != hipSuccess) return e;
+    }
     const int kMaxGlobalR = kRegMaxSteps;
     int top = (int)jtop;
     while (top >= (int)jbot) {

@@ -361,13 +361,16 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_PF
 #define FLTEE_FC_PF 0
 #endif
-// Round 5: 8,192-record windows (1,024 lanes x 8, one block per CU: 16 waves, <= 128
-// VGPRs) for the wide-halo arrays (C5: Hr = 1,008 against 4,096 records per tile — the
-// window re-read 1.42x the records it compacts, 2.14 GB of PMC traffic against 1.76 GB
-// launch-side): the halo and the H = 511 overlap rows then cost 1.2x.  (512 lanes x 16 at
-// two blocks per CU spills: 112 B of scratch.)  FLTEE_FC_PER16=0 keeps 4,096 (A/B).
+// Round 5, measured and not kept (FLTEE_FC_PER16=1): 8,192-record windows (1,024 lanes x
+// 8, one block per CU: 16 waves, <= 128 VGPRs) for the wide-halo arrays (C5: Hr = 1,008
+// against 4,096 records per tile — the window re-read 1.42x the records it compacts, 2.14
+// GB of PMC traffic against 1.76 GB launch-side), the halo and the H = 511 overlap rows
+// then costing 1.2x: 1,356-1,358 vs 1,097-1,098 us per pass (A/B in one process,
+// `profiles/r05/ab/ab3_fold_window8192_c5_rejected.jsonl`) — one 1,024-lane block per CU
+// has too few waves to hide the window load that three 512-lane blocks hide.  (512 lanes
+// x 16 at two blocks per CU spills: 112 B of scratch.)
 #ifndef FLTEE_FC_PER16
-#define FLTEE_FC_PER16 1
+#define FLTEE_FC_PER16 0
 #endif
 template <int NT, int PER, int FINAL, int XMAX, int BPC = FLTEE_FC_BLOCKS>
 __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,

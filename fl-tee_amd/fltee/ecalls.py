@@ -77,7 +77,7 @@ class Enclave:
                                  num_of_parameters, num_of_sparse_parameters, aggregation_alg):
         ids = np.ascontiguousarray(client_ids, dtype=np.uint32)
         enc = _as_u8(encrypted_parameters)
-        out = np.full(num_of_parameters, np.nan, dtype=np.float32)
+        out = np.empty(num_of_parameters, dtype=np.float32)  # written whole by the call
         times = np.full(3, np.nan, dtype=np.float32)
         rv = ctypes.c_uint32(0xFFFFFFFF)
         st = self.lib.ecall_secure_aggregation(
