@@ -238,12 +238,16 @@ hipError_t launch_apply_clip(void *rec, size_t n, size_t k, const float *coef, h
 void aes128_expand_key(const uint8_t key[16], uint32_t rk[44]);
 // the round keys of the n clients' session keys (constant time, 8 keys per circuit pass)
 void aes128_session_round_keys(const uint32_t *ids, size_t n, uint32_t *rk);
+// zero_word (optional): a device word the kernel sets to 0 (a status word, without a
+// memset launch)
 hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                           size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
-                          hipStream_t s);
+                          hipStream_t s, uint32_t *zero_word = nullptr);
 // the bytes [16 * block_off, ...) of each client's payload; idx_sub subtracted from each idx
+void set_aes_variant(int v);  // 0: by size, 1: quad kernel, 2: byte-per-lane kernel
 hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                                 size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
-                                uint64_t block_off, uint32_t idx_sub, hipStream_t s);
+                                uint64_t block_off, uint32_t idx_sub, hipStream_t s,
+                                uint32_t *zero_word = nullptr);
 
 }  // namespace fltee

@@ -236,16 +236,36 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
 
 // Small calls (payload <= kStagedBytes) on one GPU with ONE host synchronisation: the
 // round keys (computed straight into pinned memory) and the ciphertext (one memcpy into
-// it) cross PCIe in one DMA, the AES-CTR kernel and the aggregation follow on the
-// stream, and the f32[d] output comes back in one DMA together with the device status
-// word (it sits right after the output in HBM) — then one stream sync.  The large-payload
-// path (pageable 64 MB chunks with the decryption pipelined under the copies) pays a
-// stream sync per phase; here the fixed cost is the API calls and one round trip.
-// Timers (execution_time_results, lib.rs:280-353): [0] = the host staging + the H2D,
-// [1] = the AES kernel (hipEvents), [2] = the rest of the call (alg 6: [1] = decrypt +
-// aggregate, [2] = 0, lib.rs:425-592).  alg: an ECALL alg, or FLTEE_ALG_OPTIMIZED with
-// batch.
+// it) are read by the AES-CTR kernel, the aggregation follows on the stream, and the
+// f32[d] output comes back together with the device status word (it sits right after the
+// output in HBM) — then one stream sync.  Both crossings avoid the runtime's copy
+// commands, whose start on the GPU trailed the previous command by ~10 us each (the
+// small-call kernel traces, profiles/r05/small_ecall/): payloads up to kZeroCopyBytes
+// are read by the AES kernel straight from the pinned buffer over PCIe (its loads are
+// issued before its rounds), larger ones cross in one DMA; the output leaves through a
+// copy kernel storing into pinned memory.  The large-payload path (pageable 64 MB
+// chunks with the decryption pipelined under the copies) pays a stream sync per phase.
+// Timers (execution_time_results, lib.rs:280-353): [0] = the host staging (+ the H2D
+// when there is one), [1] = the AES kernel (hipEvents), [2] = the rest of the call (alg
+// 6: [1] = decrypt + aggregate, [2] = 0, lib.rs:425-592).  alg: an ECALL alg, or
+// FLTEE_ALG_OPTIMIZED with batch.
 constexpr size_t kStagedBytes = (size_t)16 << 20;
+constexpr size_t kZeroCopyBytes = (size_t)256 << 10;
+
+__global__ __launch_bounds__(256) void copy_out_kernel(const uint4 *__restrict__ src,
+                                                       uint4 *__restrict__ dst, size_t n16) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+        dst[i] = src[i];
+}
+
+static hipError_t launch_copy_out(const void *src, void *dst, size_t bytes, hipStream_t s) {
+    const size_t n16 = (bytes + 15) / 16;  // both ends 16-B aligned, padded
+    size_t blocks = (n16 + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(copy_out_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4 *)src,
+                       (uint4 *)dst, n16);
+    return hipGetLastError();
+}
 
 static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, size_t n,
                              const uint8_t *enc, size_t bpc, size_t d, size_t k_req, size_t batch,
@@ -254,11 +274,12 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     const size_t rpc = bpc / 8;
     const size_t rkb = (n * 44 * 4 + 15) / 16 * 16, cb = n * bpc;
     const size_t d4 = (d * 4 + 15) / 16 * 16;
-    // one device buffer [out: d4][status: 16][round keys: rkb][ciphertext: cb]: the H2D
-    // covers status .. ciphertext (the status word arrives as zeros: no memset launch),
-    // the D2H covers out .. status
-    if (!c->stage.reserve(d4 + 16 + rkb + cb + 16) || !c->records.reserve(n * rpc * 8 + 16) ||
-        !c->pin_in.reserve(16 + rkb + cb + 16) || !c->pin_out.reserve(d4 + 16))
+    const bool zero_copy = cb > 0 && 16 + rkb + cb <= kZeroCopyBytes;
+    // device [out: d4][status: 16][round keys: rkb][ciphertext: cb] (keys and ciphertext
+    // only for a DMA); pinned in [16 zeros][round keys][ciphertext], out [out][status]
+    if (!c->stage.reserve(d4 + 16 + (zero_copy ? 0 : rkb + cb) + 16) ||
+        !c->records.reserve(n * rpc * 8 + 16) || !c->pin_in.reserve(16 + rkb + cb + 16) ||
+        !c->pin_out.reserve(d4 + 16))
         return FLTEE_ERROR_OUT_OF_MEMORY;
     for (int i = 0; i < 3; ++i)
         if (!c->call_ev[i] && hipEventCreate(&c->call_ev[i]) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
@@ -271,12 +292,18 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     uint8_t *stage = (uint8_t *)c->stage.ptr;
     float *d_out = (float *)stage;
     uint32_t *d_st = (uint32_t *)(stage + d4);
-    const uint8_t *d_rk = stage + d4 + 16, *d_cipher = d_rk + rkb;
-    if (hipEventRecord(c->call_ev[0], s) != hipSuccess ||
-        hipMemcpyAsync(stage + d4, pin, 16 + rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipEventRecord(c->call_ev[1], s) != hipSuccess ||
+    const uint8_t *d_rk = zero_copy ? (const uint8_t *)c->pin_in.dptr + 16 : stage + d4 + 16;
+    const uint8_t *d_cipher = d_rk + rkb;
+    if (hipEventRecord(c->call_ev[0], s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (!zero_copy) {  // the status word arrives as zeros with the keys and the ciphertext
+        if (hipMemcpyAsync(stage + d4, pin, 16 + rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess)
+            return FLTEE_ERROR_UNEXPECTED;
+    } else if (!cb && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) {
+        return FLTEE_ERROR_UNEXPECTED;
+    }
+    if (hipEventRecord(c->call_ev[1], s) != hipSuccess ||
         (cb && launch_aes_ctr(d_cipher, n, bpc, rpc, (const uint32_t *)d_rk, (uint8_t *)c->records.ptr,
-                              s) != hipSuccess) ||
+                              s, zero_copy ? d_st : nullptr) != hipSuccess) ||
         hipEventRecord(c->call_ev[2], s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     fltee_device_opts o = ecall_opts(alg == FLTEE_ALG_OPTIMIZED ? FLTEE_ALG_ADVANCED : alg, n, rpc, d,
@@ -289,11 +316,12 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
         if (st != FLTEE_SUCCESS) return st;
         if (cfg.dp && launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
-        if (hipMemcpyAsync(c->pin_out.ptr, d_out, d4 + 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (launch_copy_out(d_out, c->pin_out.dptr, d4 + 16, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
         bool retry = false;
-        st = status_to_retval(*(const uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg, &retry);
+        st = status_to_retval(*(const volatile uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg,
+                              &retry);
         if (!retry) break;
         o.flags &= ~FLTEE_OPT_DENSE;  // non_oblivious: scatter semantics
     }

@@ -17,7 +17,8 @@ struct Buffer {
 
 // grow-only pinned host memory (the ECALL's staging: one DMA each way per call)
 struct HostBuffer {
-    void *ptr = nullptr;
+    void *ptr = nullptr;   // host address
+    void *dptr = nullptr;  // the same pinned bytes as kernels address them (zero-copy)
     size_t cap = 0;
     bool reserve(size_t bytes);
 };

@@ -30,10 +30,14 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
 
 // Sparse non_oblivious: scatter into per-client rows (k_accumulate.hip) when the
 // [n][d] row matrix costs less HBM traffic than the stable sort it replaces
-// (rows: ~8*n*d bytes; sort: >= 16*M bytes per pass, tens of passes).
+// (rows: ~8*n*d bytes; sort: >= 16*M bytes per pass), or when the rows are small enough
+// (<= 2^24 cells, 128 MB of traffic: ~25 us) that the counting sort's nine launches and
+// its count readback cost more than they move (round 5: MLP-MNIST n = 3, k = 508 took
+// ~100 us through the sort, `profiles/r05/small_ecall/`).
 static bool use_scatter_rows(size_t n, size_t k, size_t d) {
     const size_t cells = n * d;
-    return cells <= ((size_t)1 << 30) && cells <= 64 * next_pow2_sz(n * k);
+    return cells <= ((size_t)1 << 30) &&
+           (cells <= ((size_t)1 << 24) || cells <= 64 * next_pow2_sz(n * k));
 }
 
 static DeviceCtx g_ctx[kMaxDevices];
@@ -116,10 +120,11 @@ bool Buffer::reserve(size_t bytes) {
 bool HostBuffer::reserve(size_t bytes) {
     if (bytes <= cap) return true;
     if (ptr) (void)hipHostFree(ptr);
-    ptr = nullptr;
+    ptr = dptr = nullptr;
     cap = 0;
     const size_t want = bytes + bytes / 8 + 4096;
     if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) { ptr = nullptr; return false; }
+    if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess) dptr = ptr;  // one address space
     cap = want;
     return true;
 }
@@ -882,6 +887,7 @@ extern "C" void fltee_set_advanced_exact_runs(int on) {
 }
 // test hook: blocks a bucket of the tree ORAM takes on eviction (4; 0 forces the stash)
 extern "C" void fltee_debug_set_oram_bucket(int z) { fltee::set_oram_bucket(z); }
+extern "C" void fltee_debug_set_aes_variant(int v) { fltee::set_aes_variant(v); }
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes

@@ -728,56 +728,36 @@ __global__ __launch_bounds__(NT) void sweep_ordered(const uint2 *__restrict__ re
 #pragma unroll
             for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const u32x4_t *>(t4 + q + i);
         };
-        // 16 records: the selects by hand (hipcc puts every compare in VCC, then needs two
-        // wait states before the select that reads it, and turns selects of loaded values
-        // into loads under an EXEC mask of the matching lanes): four compares into four
-        // SGPR-pair masks, then the four selects, so every mask is read four VALU after it
-        // is written; the adds stay in upload order
-        // 16 records: the compare / select / add of each record by hand, software-pipelined
-        // (hipcc puts every compare in VCC, then needs two wait states before the select
-        // that reads it, chains the adds back to back, and turns selects of loaded values
-        // into loads under an EXEC mask of the matching lanes).  Steady state, record i:
-        // compare i + 2 (its own SGPR-pair mask), select i, add i - 1 — every mask is read
-        // four instructions after it is written and consecutive adds of the chain stand
-        // two instructions apart; the adds stay in upload order.
-        auto add8 = [&](const u32x4_t &a0, const u32x4_t &a1, const u32x4_t &a2, const u32x4_t &a3) {
-            uint64_t m0, m1, m2;
-            uint32_t t0, t1;
+        // 4 records at a time by hand: four compares into four SGPR-pair masks, the four
+        // selects, the four adds in upload order, so every mask is read four VALU after it
+        // is written (hipcc puts every compare in VCC, then needs two wait states before the
+        // select that reads it, and turns selects of loaded values into loads under an EXEC
+        // mask of the matching lanes).  (Round 5: a software-pipelined form — compare i + 2,
+        // select i, add i - 1 — measured 2 % slower: `profiles/r05/ab/ab6_*`.)
+        auto add4 = [&](const u32x4_t &a0, const u32x4_t &a1) {
+            uint64_t m0, m1, m2, m3;
+            uint32_t t0, t1, t2, t3;
             asm volatile(
                 "v_cmp_eq_u32_e64 %[m0], %[i0], %[j]\n\t"
                 "v_cmp_eq_u32_e64 %[m1], %[i1], %[j]\n\t"
                 "v_cmp_eq_u32_e64 %[m2], %[i2], %[j]\n\t"
+                "v_cmp_eq_u32_e64 %[m3], %[i3], %[j]\n\t"
                 "v_cndmask_b32_e64 %[t0], 0, %[v0], %[m0]\n\t"
-                "v_cmp_eq_u32_e64 %[m0], %[i3], %[j]\n\t"
                 "v_cndmask_b32_e64 %[t1], 0, %[v1], %[m1]\n\t"
+                "v_cndmask_b32_e64 %[t2], 0, %[v2], %[m2]\n\t"
+                "v_cndmask_b32_e64 %[t3], 0, %[v3], %[m3]\n\t"
                 "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
-                "v_cmp_eq_u32_e64 %[m1], %[i4], %[j]\n\t"
-                "v_cndmask_b32_e64 %[t0], 0, %[v2], %[m2]\n\t"
                 "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
-                "v_cmp_eq_u32_e64 %[m2], %[i5], %[j]\n\t"
-                "v_cndmask_b32_e64 %[t1], 0, %[v3], %[m0]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
-                "v_cmp_eq_u32_e64 %[m0], %[i6], %[j]\n\t"
-                "v_cndmask_b32_e64 %[t0], 0, %[v4], %[m1]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
-                "v_cmp_eq_u32_e64 %[m1], %[i7], %[j]\n\t"
-                "v_cndmask_b32_e64 %[t1], 0, %[v5], %[m2]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
-                "v_cndmask_b32_e64 %[t0], 0, %[v6], %[m0]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t1]\n\t"
-                "v_cndmask_b32_e64 %[t1], 0, %[v7], %[m1]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t0]\n\t"
-                "v_add_f32_e32 %[acc], %[acc], %[t1]"
-                : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [t0] "=&v"(t0),
-                  [t1] "=&v"(t1)
+                "v_add_f32_e32 %[acc], %[acc], %[t2]\n\t"
+                "v_add_f32_e32 %[acc], %[acc], %[t3]"
+                : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+                  [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
                 : [i0] "v"(a0.x), [v0] "v"(a0.y), [i1] "v"(a0.z), [v1] "v"(a0.w), [i2] "v"(a1.x),
-                  [v2] "v"(a1.y), [i3] "v"(a1.z), [v3] "v"(a1.w), [i4] "v"(a2.x), [v4] "v"(a2.y),
-                  [i5] "v"(a2.z), [v5] "v"(a2.w), [i6] "v"(a3.x), [v6] "v"(a3.y), [i7] "v"(a3.z),
-                  [v7] "v"(a3.w), [j] "v"(j));
+                  [v2] "v"(a1.y), [i3] "v"(a1.z), [v3] "v"(a1.w), [j] "v"(j));
         };
         auto add = [&](const u32x4_t (&r)[8]) {
-            add8(r[0], r[1], r[2], r[3]);
-            add8(r[4], r[5], r[6], r[7]);
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) add4(r[i], r[i + 1]);
         };
         rd(ra, 0);
         for (int q = 0; q < SO_CH / 2; q += 16) {

@@ -288,7 +288,8 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
                                                           const uint32_t *__restrict__ rks,
                                                           uint8_t *__restrict__ plain,
                                                           uint64_t block_off, uint32_t idx_sub,
-                                                          uint64_t wpc) {
+                                                          uint64_t wpc, uint32_t *__restrict__ zero_word) {
+    if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
     const uint32_t lane = threadIdx.x & 63, col = lane & 3, g = lane >> 2;
     const uint64_t bpcl = (rpc + 1) / 2;  // 16-byte blocks per client
     const uint64_t waves = (uint64_t)n * wpc;
@@ -300,6 +301,11 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
         const uint64_t c = gu / wpc;
         const uint64_t W = (w0 + (gu - c * wpc)) * kAesWindow4;
         const uint32_t *rk = rks + c * 44 + col;  // this lane's column of every round key
+        // all eleven round-key words up front, in one round trip (a load per round inside
+        // the loop put ten dependent memory latencies on a small call's critical path)
+        uint32_t rkw[11];
+#pragma unroll
+        for (int R = 0; R < 11; ++R) rkw[R] = rk[4 * R];
         const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
         // counter block BE128(W + g + 16 j): column 3 = counter bits 0-31, column 2 =
         // bits 32-63, columns 0-1 zero; bits 0-3 = g, 4-8 = j, the rest W's
@@ -316,15 +322,17 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
                 const uint32_t v2 = 0u - ((whi >> t) & 1u);
                 s[r][i] = col == 3 ? v3 : col == 2 ? v2 : 0u;
             }
-        ark_col(s, rk[0]);
+        ark_col(s, rkw[0]);
 #pragma unroll 1
         for (int R = 1; R < 10; ++R) {
-            const uint32_t w = rk[4 * R] ^ 0x63636363u;  // the S-boxes' 0x63, folded
+            const uint32_t w = rkw[1] ^ 0x63636363u;  // the S-boxes' 0x63, folded
+#pragma unroll
+            for (int i = 1; i < 10; ++i) rkw[i] = rkw[i + 1];  // the next round's word first
             sub_shift_col(s);
             mix_ark_col(s, w);
         }
         sub_shift_col(s);
-        ark_col(s, rk[40] ^ 0x63636363u);
+        ark_col(s, rkw[1] ^ 0x63636363u);
         // rows 8 r + i -> word j = keystream word `col` of block j
         transpose32(&s[0][0]);
         const uint8_t *cbase = cipher + c * bpc + 4 * col;
@@ -343,33 +351,226 @@ __global__ __launch_bounds__(256) void aes_ctr_bs4_kernel(const uint8_t *__restr
     }
 }
 
+// ------------------------------------------------- byte-per-lane bitsliced kernel
+// For small payloads the quad kernel's latency is one wave's instruction stream: ~7k VALU
+// per wave (four S-boxes per lane per round), ~20 us even for 12 KB, whatever the size
+// below a chip's worth of waves.  This form spreads a 32-block slice over 16 lanes, one
+// state byte per lane, so a lane runs one S-box per round (119 v_bitop3) and the round's
+// stream is ~4x shorter; it costs ~1.4x the lane-instructions per block, so it only runs
+// where the quad kernel leaves SIMDs idle (launch_aes_ctr_slice).
+//   lane = 16 G + 4 r + p: G = slice group of the wave (0-3), r = AES row, p = physical
+//   column.  ShiftRows is not applied to the data: after t of them, row r's logical
+//   column c sits at p = (c + r t) mod 4, so MixColumns for (r, c) reads row r + D of the
+//   same logical column from lane 4 (r + D) + (p + D t) mod 4 of its row: a DPP row
+//   rotation by 4 D then a quad rotation by D t — uniform across lanes for fixed D, t.
+//   Counter block of slice bit b in group G: W + 32 G + b (W: the wave's 128-block
+//   window), so plane i of byte (r, c) is counter bit (15 - 4c - r) * 8 + i: bits 0-4 =
+//   b (constant patterns), 5-6 = G, 7- = W.  The keystream goes through 2 KB of LDS per
+//   wave (byte stores), each lane then XORs two whole 16-B blocks: 32 B contiguous per lane.
+constexpr int kAesWindowR = 128;  // counter blocks per wave: 4 groups x 32 slices
+constexpr uint64_t kAesRowBelowWaves = 1024;  // quad-kernel waves: one per SIMD
+
+__device__ __forceinline__ uint32_t row_rot(uint32_t v, int quads) {
+    // lane L of each 16-lane row reads lane (L + 4 quads) mod 16 (row_ror:16-4q)
+    switch (quads & 3) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + 12, 0xf, 0xf, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + 8, 0xf, 0xf, false);
+    case 3: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x120 + 4, 0xf, 0xf, false);
+    default: return v;
+    }
+}
+
+// SubBytes, then MixColumns + AddRoundKey at ShiftRows count t (TM = t mod 4) on the
+// lane's byte; wr = the lane's round-key word shifted so its row's byte is bits 24-31
+template <int TM>
+__device__ __forceinline__ void round_row(uint32_t x[8], uint32_t wr) {
+    aes_sbox_bs(x);
+    uint32_t a1[8], a2[8], a3[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        a1[i] = quad_rot(row_rot(x[i], 1), (1 * TM) & 3);
+        a2[i] = quad_rot(row_rot(x[i], 2), (2 * TM) & 3);
+        a3[i] = quad_rot(row_rot(x[i], 3), (3 * TM) & 3);
+    }
+    uint32_t u[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u[i] = x[i] ^ a1[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        // 2 a0 ^ 3 a1 ^ a2 ^ a3 = xtime(a0 ^ a1) ^ a1 ^ a2 ^ a3; xtime bit i = u_{i-1}
+        // (+ u_7 for i = 0, 1, 3, 4: 0x1b)
+        const uint32_t v = xor3(a1[i], a2[i], a3[i]);
+        const uint32_t k = sext_bit(wr, 24 + i);
+        if (i == 0) x[i] = xor3(v, u[7], k);
+        else if (i == 1 || i == 3 || i == 4) x[i] = xor3(v, u[i - 1], u[7]) ^ k;
+        else x[i] = xor3(v, u[i - 1], k);
+    }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void aes_ctr_row_kernel(const uint8_t *__restrict__ cipher,
+                                                          size_t n, size_t bpc, size_t rpc,
+                                                          const uint32_t *__restrict__ rks,
+                                                          uint8_t *__restrict__ plain,
+                                                          uint64_t block_off, uint32_t idx_sub,
+                                                          uint64_t wpc, uint32_t *__restrict__ zero_word) {
+    if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0u;
+    __shared__ __attribute__((aligned(16))) uint8_t ks_lds[4][kAesWindowR * 16];
+    uint8_t *ks = ks_lds[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63, G = lane >> 4, r = (lane >> 2) & 3, p = lane & 3;
+    const uint64_t bpcl = (rpc + 1) / 2;  // 16-byte blocks per client
+    const uint64_t waves = (uint64_t)n * wpc;
+    const uint64_t w0 = block_off / kAesWindowR;
+    for (uint64_t gw = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gw < waves;
+         gw += (uint64_t)gridDim.x * 4) {
+        const uint64_t gu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(gw >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)gw);
+        const uint64_t c = gu / wpc;
+        const uint64_t W = (w0 + (gu - c * wpc)) * kAesWindowR;
+        // this lane's two output blocks (window-local 2 lane, 2 lane + 1): their
+        // ciphertext words first, so the loads overlap the rounds
+        const uint8_t *cbase = cipher + c * bpc;
+        uint32_t cw[8];
+        bool ok[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t ctr = W + 2 * lane + h;
+            const bool in = ctr >= block_off && ctr - block_off < bpcl;
+            const uint64_t b = in ? ctr - block_off : 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                ok[4 * h + w] = in && 2 * b + (w >> 1) < rpc;  // the half last block
+                const uint8_t *src = cbase + 16 * b + 4 * w;
+                cw[4 * h + w] = !ok[4 * h + w] ? 0u
+                                : ALIGNED      ? *reinterpret_cast<const uint32_t *>(src)
+                                               : ld_u32_bytes(src);
+            }
+        }
+        // round-key words: after R ShiftRows the lane's logical column is (p - r R) mod 4
+        const uint32_t *rk = rks + c * 44;
+        uint32_t rkw[11];
+#pragma unroll
+        for (int R = 0; R < 11; ++R) rkw[R] = rk[4 * R + ((p - r * (uint32_t)R) & 3u)] << (8 * r);
+        // counter planes: byte (r, c = p) of block W + 32 G + b, b = slice bit
+        uint32_t x[8];
+        const uint32_t wlo = (uint32_t)W, whi = (uint32_t)(W >> 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int t = (int)((15 - 4 * p - r) * 8) + i;  // counter bit of this plane
+            const uint32_t pat = t == 0 ? 0xaaaaaaaau : t == 1 ? 0xccccccccu : t == 2 ? 0xf0f0f0f0u
+                               : t == 3 ? 0xff00ff00u : 0xffff0000u;
+            const uint32_t wb = t < 32 ? (wlo >> (t & 31)) & 1u : t < 64 ? (whi >> (t & 31)) & 1u : 0u;
+            x[i] = t < 5 ? pat : t < 7 ? 0u - ((G >> (t - 5)) & 1u) : 0u - wb;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] ^= sext_bit(rkw[0], 24 + i);
+        // rounds 1-9 (t = R), MixColumns' rotations fixed per t mod 4: two passes of
+        // rounds 4 i + 1 .. 4 i + 4 (t mod 4 = 1, 2, 3, 0), then round 9
+#pragma unroll 1
+        for (int it = 0; it < 2; ++it) {
+            round_row<1>(x, rkw[1] ^ 0x63636363u);
+            round_row<2>(x, rkw[2] ^ 0x63636363u);
+            round_row<3>(x, rkw[3] ^ 0x63636363u);
+            round_row<0>(x, rkw[4] ^ 0x63636363u);
+#pragma unroll
+            for (int i = 1; i < 7; ++i) rkw[i] = rkw[i + 4];  // the next four rounds' words
+        }
+        round_row<1>(x, rkw[1] ^ 0x63636363u);  // round 9; rkw[2] = round 10's word
+        aes_sbox_bs(x);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] ^= sext_bit(rkw[2] ^ 0x63636363u, 24 + i);
+        // 8 x 32 bit transpose (three butterfly levels): byte q of x[i] = the keystream
+        // byte of slice b = 8 q + i
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            const int sh = 1 << l;
+            const uint32_t m = l == 0 ? 0x55555555u : l == 1 ? 0x33333333u : 0x0f0f0f0fu;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i & sh) continue;
+                const uint32_t t = ((x[i] >> sh) ^ x[i + sh]) & m;
+                x[i + sh] ^= t;
+                x[i] ^= t << sh;
+            }
+        }
+        // byte (r, c) of block 32 G + b at 16 (32 G + b) + 4 c + r; after ten ShiftRows
+        // the lane's logical column is (p - 2 r) mod 4
+        const uint32_t cfin = (p - 2 * r) & 3u;
+        uint8_t *kb = ks + 16 * 32 * G + 4 * cfin + r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) kb[16 * (8 * q + i)] = (uint8_t)(x[i] >> (8 * q));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint4 k0 = reinterpret_cast<const uint4 *>(ks)[2 * lane];
+        const uint4 k1 = reinterpret_cast<const uint4 *>(ks)[2 * lane + 1];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the next window's stores after every read
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t kw[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+        uint8_t *dbase = plain + c * rpc * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint64_t ctr = W + 2 * lane + h;
+            const uint64_t b = ctr >= block_off ? ctr - block_off : 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if (ok[4 * h + w])
+                    *reinterpret_cast<uint32_t *>(dbase + 16 * b + 4 * w) =
+                        (cw[4 * h + w] ^ kw[4 * h + w]) - ((w & 1) ? 0u : idx_sub);
+        }
+    }
+}
+
+static int g_aes_variant = 0;  // 0: by size, 1: the quad kernel, 2: the byte-per-lane kernel
+void set_aes_variant(int v) { g_aes_variant = v; }
+
 hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                                 size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
-                                uint64_t block_off, uint32_t idx_sub, hipStream_t s) {
+                                uint64_t block_off, uint32_t idx_sub, hipStream_t s,
+                                uint32_t *zero_word) {
     const size_t bpcl = (rec_per_client + 1) / 2;
     if (n == 0 || bpcl == 0) return hipSuccess;
     const bool aligned = bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0;
     // windows of 512 counter blocks (absolute counter space) touching each client's slice
     const uint64_t wpc = (block_off + bpcl - 1) / kAesWindow4 - block_off / kAesWindow4 + 1;
     const uint64_t waves = (uint64_t)n * wpc;
+    // the byte-per-lane kernel while the quad kernel would leave SIMDs without a wave
+    const bool row = g_aes_variant == 2 || (g_aes_variant == 0 && waves < kAesRowBelowWaves);
+    if (row) {
+        const uint64_t wpcr = (block_off + bpcl - 1) / kAesWindowR - block_off / kAesWindowR + 1;
+        uint64_t rblocks = ((uint64_t)n * wpcr + 3) / 4;
+        if (rblocks > 16384) rblocks = 16384;
+        if (aligned)
+            hipLaunchKernelGGL(aes_ctr_row_kernel<true>, dim3((unsigned)rblocks), dim3(256), 0, s,
+                               cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
+                               block_off, idx_sub, wpcr, zero_word);
+        else
+            hipLaunchKernelGGL(aes_ctr_row_kernel<false>, dim3((unsigned)rblocks), dim3(256), 0, s,
+                               cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
+                               block_off, idx_sub, wpcr, zero_word);
+        return hipGetLastError();
+    }
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 16384) blocks = 16384;  // grid-stride beyond 16 waves per SIMD
     if (aligned)
         hipLaunchKernelGGL(aes_ctr_bs4_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
                            cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
-                           block_off, idx_sub, wpc);
+                           block_off, idx_sub, wpc, zero_word);
     else
         hipLaunchKernelGGL(aes_ctr_bs4_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
                            cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
-                           block_off, idx_sub, wpc);
+                           block_off, idx_sub, wpc, zero_word);
     return hipGetLastError();
 }
 
 hipError_t launch_aes_ctr(const uint8_t *cipher, size_t n, size_t bytes_per_client,
                           size_t rec_per_client, const uint32_t *round_keys, uint8_t *plain,
-                          hipStream_t s) {
+                          hipStream_t s, uint32_t *zero_word) {
     return launch_aes_ctr_slice(cipher, n, bytes_per_client, rec_per_client, round_keys, plain, 0,
-                                0, s);
+                                0, s, zero_word);
 }
 
 }  // namespace fltee

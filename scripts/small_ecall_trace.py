@@ -1,7 +1,7 @@
 """Small-payload ECALLs for a kernel trace: each (n, k, alg) runs `reps`
 host-inclusive calls of ecall_secure_aggregation, the groups 50 ms apart so a trace splits
 by time; one JSON line per group with the host wall times and the ECALL's phase timers.
-    rocprofv3 --kernel-trace -d gpurun_out/x -o run -- python3 scripts/small_ecall_trace.py"""
+    rocprofv3 --kernel-trace -d gpurun_out/x -o run -- python3 scripts/small_ecall_trace.py [reps] [n:k ...]"""
 import json
 import sys
 import time
@@ -16,6 +16,8 @@ from fltee.ecalls import Enclave  # noqa: E402
 ALGS = {"advanced": 1, "baseline": 3, "non_oblivious": 4, "path_oram": 5}
 shapes = [(3, 508), (30, 508), (3, 5089), (300, 508), (30, 5089)]
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+if len(sys.argv) > 2:
+    shapes = [tuple(int(x) for x in a.split(":")) for a in sys.argv[2:]]
 d = 50890
 dev = torch.device("cuda", 0)
 E = Enclave(0)

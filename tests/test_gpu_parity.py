@@ -745,14 +745,25 @@ def test_gpu_decrypt_reference_client_payloads(dev, name):
     assert out.cpu().numpy().tobytes() == fx["plaintext"].tobytes()
 
 
-# The bitsliced kernel takes 2048-block counter windows per wave (64 lanes x 32 slices):
-# slices shorter than a window, ending one record into a window, a half last block (odd
-# record count), several clients per window row, unaligned slices (bpc % 8 != 0) and
-# 32-bit client ids.
+# The bitsliced kernels take counter windows per wave (the quad kernel 512 blocks: 16
+# quads x 32 slices; the byte-per-lane kernel 128: 4 x 16 lanes x 32 slices): slices
+# shorter than a window, ending one record into a window, a half last block (odd record
+# count), several clients per window row, unaligned slices (bpc % 8 != 0) and 32-bit
+# client ids — through each kernel (variant 1 quad, 2 byte-per-lane, 0 by size).
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("n,bpc", [(1, 8), (3, 24), (2, 16 * 2048), (2, 16 * 2048 + 8),
                                    (5, 16 * 2048 * 2 - 8), (7, 40712), (4, 8 * 5089 + 3),
-                                   (3, 16 * 4096 + 13)])
-def test_gpu_decrypt_bitsliced_windows(dev, oracle, n, bpc):
+                                   (3, 16 * 4096 + 13), (2, 16 * 128 + 8), (9, 16 * 127)])
+def test_gpu_decrypt_bitsliced_windows(dev, oracle, n, bpc, variant):
+    from fltee import _lib
+    _lib.lib().fltee_debug_set_aes_variant(variant)
+    try:
+        _decrypt_windows_case(dev, oracle, n, bpc)
+    finally:
+        _lib.lib().fltee_debug_set_aes_variant(0)
+
+
+def _decrypt_windows_case(dev, oracle, n, bpc):
     import torch
     rng = np.random.default_rng(bpc * 31 + n)
     ids = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
