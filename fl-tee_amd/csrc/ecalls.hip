@@ -234,21 +234,23 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     return FLTEE_ERROR_INVALID_PARAMETER;
 }
 
-// Small calls (payload <= kStagedBytes) on one GPU with ONE host synchronisation: the
-// round keys (computed straight into pinned memory) and the ciphertext (one memcpy into
-// it) are read by the AES-CTR kernel, the aggregation follows on the stream, and the
-// f32[d] output comes back together with the device status word (it sits right after the
-// output in HBM) — then one stream sync.  Both crossings avoid the runtime's copy
-// commands, whose start on the GPU trailed the previous command by ~10 us each (the
-// small-call kernel traces, profiles/r05/small_ecall/): payloads up to kZeroCopyBytes
-// are read by the AES kernel straight from the pinned buffer over PCIe (its loads are
-// issued before its rounds), larger ones cross in one DMA; the output leaves through a
-// copy kernel storing into pinned memory.  The large-payload path (pageable 64 MB
-// chunks with the decryption pipelined under the copies) pays a stream sync per phase.
-// Timers (execution_time_results, lib.rs:280-353): [0] = the host staging (+ the H2D
-// when there is one), [1] = the AES kernel (hipEvents), [2] = the rest of the call (alg
-// 6: [1] = decrypt + aggregate, [2] = 0, lib.rs:425-592).  alg: an ECALL alg, or
-// FLTEE_ALG_OPTIMIZED with batch.
+// Small calls (payload <= kStagedBytes) on one GPU with ONE host synchronisation. The
+// round keys are computed straight into pinned memory and read from there by the AES-CTR
+// kernel (which also zeroes the status word); the ciphertext is read the same way up to
+// kZeroCopyBytes (one host memcpy into the pinned buffer; the kernel issues its loads
+// before its rounds), and above that crosses in one DMA straight from the caller's
+// buffer (the runtime's pageable path pipelines its own staging: 1.2 MB in 47 us against
+// 67 us through a memcpy into our pinned buffer + a DMA, `profiles/r05/small_ecall/
+// h2d_probe_r05l.jsonl`).  The aggregation follows on the stream, and the f32[d] output
+// leaves with the device status word (it sits right after the output in HBM) through a
+// copy kernel storing into pinned memory — then one stream sync.  The runtime's copy
+// commands started ~10 us after the command before them in the kernel traces of small
+// calls (`profiles/r05/small_ecall/`), so the small path avoids them.  The large-payload
+// path (pageable 64 MB chunks with the decryption pipelined under the copies) pays a
+// stream sync per phase.  Timers (execution_time_results, lib.rs:280-353): [0] = the
+// host staging + the H2D (when there is one), [1] = the AES kernel (hipEvents), [2] =
+// the rest of the call (alg 6: [1] = decrypt + aggregate, [2] = 0, lib.rs:425-592).
+// alg: an ECALL alg, or FLTEE_ALG_OPTIMIZED with batch.
 constexpr size_t kStagedBytes = (size_t)16 << 20;
 constexpr size_t kZeroCopyBytes = (size_t)256 << 10;
 
@@ -274,36 +276,32 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     const size_t rpc = bpc / 8;
     const size_t rkb = (n * 44 * 4 + 15) / 16 * 16, cb = n * bpc;
     const size_t d4 = (d * 4 + 15) / 16 * 16;
-    const bool zero_copy = cb > 0 && 16 + rkb + cb <= kZeroCopyBytes;
-    // device [out: d4][status: 16][round keys: rkb][ciphertext: cb] (keys and ciphertext
-    // only for a DMA); pinned in [16 zeros][round keys][ciphertext], out [out][status]
-    if (!c->stage.reserve(d4 + 16 + (zero_copy ? 0 : rkb + cb) + 16) ||
-        !c->records.reserve(n * rpc * 8 + 16) || !c->pin_in.reserve(16 + rkb + cb + 16) ||
-        !c->pin_out.reserve(d4 + 16))
+    const bool zero_copy = 16 + rkb + cb <= kZeroCopyBytes;
+    // device [out: d4][status: 16][ciphertext: cb, DMA only]; pinned in [16][round keys:
+    // rkb][ciphertext: cb, zero-copy only], pinned out [out: d4][status: 16]
+    if (!c->stage.reserve(d4 + 16 + (zero_copy ? 0 : cb) + 16) ||
+        !c->records.reserve(n * rpc * 8 + 16) ||
+        !c->pin_in.reserve(16 + rkb + (zero_copy ? cb : 0) + 16) || !c->pin_out.reserve(d4 + 16))
         return FLTEE_ERROR_OUT_OF_MEMORY;
     for (int i = 0; i < 3; ++i)
         if (!c->call_ev[i] && hipEventCreate(&c->call_ev[i]) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     uint8_t *pin = (uint8_t *)c->pin_in.ptr;
-    std::memset(pin, 0, 16);                                   // the status word
     aes128_session_round_keys(ids, n, (uint32_t *)(pin + 16));  // session_key_store.rs:21-22
-    if (cb) std::memcpy(pin + 16 + rkb, enc, cb);
-    const double t1 = now_s();
+    if (cb && zero_copy) std::memcpy(pin + 16 + rkb, enc, cb);
+    const double t1 = now_s();  // host staging done; the DMA (if any) is timed by events
     hipStream_t s = c->stream;
     uint8_t *stage = (uint8_t *)c->stage.ptr;
     float *d_out = (float *)stage;
     uint32_t *d_st = (uint32_t *)(stage + d4);
-    const uint8_t *d_rk = zero_copy ? (const uint8_t *)c->pin_in.dptr + 16 : stage + d4 + 16;
-    const uint8_t *d_cipher = d_rk + rkb;
-    if (hipEventRecord(c->call_ev[0], s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-    if (!zero_copy) {  // the status word arrives as zeros with the keys and the ciphertext
-        if (hipMemcpyAsync(stage + d4, pin, 16 + rkb + cb, hipMemcpyHostToDevice, s) != hipSuccess)
-            return FLTEE_ERROR_UNEXPECTED;
-    } else if (!cb && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) {
+    const uint32_t *d_rk = (const uint32_t *)((const uint8_t *)c->pin_in.dptr + 16);
+    const uint8_t *d_cipher = zero_copy ? (const uint8_t *)d_rk + rkb : stage + d4 + 16;
+    if (hipEventRecord(c->call_ev[0], s) != hipSuccess ||
+        (!zero_copy && hipMemcpyAsync(stage + d4 + 16, enc, cb, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (!cb && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess))
         return FLTEE_ERROR_UNEXPECTED;
-    }
     if (hipEventRecord(c->call_ev[1], s) != hipSuccess ||
-        (cb && launch_aes_ctr(d_cipher, n, bpc, rpc, (const uint32_t *)d_rk, (uint8_t *)c->records.ptr,
-                              s, zero_copy ? d_st : nullptr) != hipSuccess) ||
+        (cb && launch_aes_ctr(d_cipher, n, bpc, rpc, d_rk, (uint8_t *)c->records.ptr, s, d_st) !=
+                   hipSuccess) ||
         hipEventRecord(c->call_ev[2], s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     fltee_device_opts o = ecall_opts(alg == FLTEE_ALG_OPTIMIZED ? FLTEE_ALG_ADVANCED : alg, n, rpc, d,
