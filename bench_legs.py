@@ -33,6 +33,10 @@ WORKLOADS = {
                 desc="MLP-MNIST n=30 alpha=0.1, baseline on sparse uploads (the ordered sweep)"),
     "b3000": dict(alg=3, n=3000, d=50890, k=5089,
                   desc="the reference's published n=3000 shape, baseline (the ordered sweep)"),
+    "a3s": dict(alg=1, n=3, d=50890, k=508,
+                desc="exp5's smallest advanced row: MLP-MNIST n=3 alpha=0.01 (M = 2^16)"),
+    "a30": dict(alg=1, n=30, d=50890, k=5089,
+                desc="exp5's MLP-MNIST n=30 alpha=0.1 advanced row (M = 2^18)"),
     "c3": dict(alg=1, n=100, d=50890, k=5089,
                desc="configs[2]: MLP-MNIST num_users=1000 frac=0.1 alpha=0.1 (n=100), advanced"),
     "c4": dict(alg=2, n=300, d=44964, k=4496, dp=True,
