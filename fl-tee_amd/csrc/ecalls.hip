@@ -295,7 +295,8 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     uint32_t *d_st = (uint32_t *)(stage + d4);
     const uint32_t *d_rk = (const uint32_t *)((const uint8_t *)c->pin_in.dptr + 16);
     const uint8_t *d_cipher = zero_copy ? (const uint8_t *)d_rk + rkb : stage + d4 + 16;
-    if (hipEventRecord(c->call_ev[0], s) != hipSuccess ||
+    // (no H2D to time on the zero-copy path: no marker in front of the first kernel)
+    if ((!zero_copy && hipEventRecord(c->call_ev[0], s) != hipSuccess) ||
         (!zero_copy && hipMemcpyAsync(stage + d4 + 16, enc, cb, hipMemcpyHostToDevice, s) != hipSuccess) ||
         (!cb && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess))
         return FLTEE_ERROR_UNEXPECTED;
@@ -326,7 +327,7 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     if (st) return st;
     std::memcpy(host_out, c->pin_out.ptr, d * 4);
     float h2d = 0, aes = 0;
-    (void)hipEventElapsedTime(&h2d, c->call_ev[0], c->call_ev[1]);
+    if (!zero_copy) (void)hipEventElapsedTime(&h2d, c->call_ev[0], c->call_ev[1]);
     (void)hipEventElapsedTime(&aes, c->call_ev[1], c->call_ev[2]);
     const float wall = (float)(now_s() - t0);
     times[0] = (float)(t1 - t0) + h2d * 1e-3f;

@@ -1351,6 +1351,13 @@ constexpr int kRegMaxSteps = 6;
 #define FLTEE_MIN_TILES_LOG 8
 #endif
 constexpr uint32_t kMinTilesLog = FLTEE_MIN_TILES_LOG;
+// ... but no tile under 2^FLTEE_TILE_FLOOR records for that: below 2^20 records fewer,
+// larger tiles win on launch count (round 5, `profiles/r05/ab/ab7_tile_floor_*.jsonl`,
+// floors 11 / 12 / 13: 2^16 records 0.071 / 0.062 / 0.076 ms, 2^18 0.107 / 0.087 / 0.115;
+// 2^14 tiles were slower at every size)
+#ifndef FLTEE_TILE_FLOOR
+#define FLTEE_TILE_FLOOR 12
+#endif
 // Narrowest strided-tile row, log2: 16 records = 128-B row segments (W = 8: 14.09 vs
 // 14.03 ms at 2^27, W = 4: 14.66, W = 2: 16.37).
 constexpr int kMinWLog = 4;
@@ -1700,7 +1707,7 @@ static TileCfg make_cfg(uint32_t mlog, uint32_t slog) {
     if (tlog > slog) tlog = slog;
     const uint32_t mt = kMinTilesLog;
     if (tlog == 14 && mlog - tlog < mt) tlog = 13;
-    while (tlog > 11 && tlog <= 13 && (mlog - tlog) < mt) --tlog;  // >= 2^mt tiles
+    while (tlog > FLTEE_TILE_FLOOR && tlog <= 13 && (mlog - tlog) < mt) --tlog;  // >= 2^mt tiles
     c.tlog = tlog;
     if (tlog <= 6) return c;
     const uint32_t T = 1u << tlog;
