@@ -32,14 +32,53 @@
 
 namespace fltee {
 
-constexpr uint64_t CP_DUMMY = 0xFFFFFFFFull;  // c = u32::MAX (never selected), +0.0
+// FLTEE_CP_PICK: 1 = compares + selects; 2 = the staying value as bit operations; 3
+// (default) = bit operations only, no compare (see cp_pick)
+#ifndef FLTEE_CP_PICK
+#define FLTEE_CP_PICK 3
+#endif
+// an unselected slot in flight: c = 2^31 (bit j clear at every level j <= 28, so it never
+// moves; form 1's u32::MAX carried the same meaning through its top-bit test), +0.0
+constexpr uint64_t CP_DUMMY = FLTEE_CP_PICK == 3 ? 0x80000000ull : 0xFFFFFFFFull;
+constexpr uint64_t CP_PAD = 0xFFFFFFFFull;  // a pad record (idx u32::MAX, +0.0) outside the array
 
 // In flight the key is not idx but c = p0 - idx, the record's total left shift
-// (p0 = its position after the fold), u32::MAX for records that are not selected
-// (idx >= d).  Level j moves a record iff bit j of c is set (c < 2^31 <= the top
-// bit of a dummy, which therefore never moves and never stays).
+// (p0 = its position after the fold), CP_DUMMY for records that are not selected
+// (idx >= d).  Level j moves a record iff bit j of c is set (c < 2^29; a dummy never
+// moves, and a slot it occupies stays a dummy).
+//
+// cp_pick (round 5, `profiles/r05/ab/ab10_*`): form 2 builds the staying value with bit
+// operations — the leaving record's slot becomes the dummy by the sign-extended bit j of
+// its c (v_bfe_i32) OR-ed into c and AND-NOT-ed out of the value (v_bfi_b32) — and keeps
+// one compare for the mover (bit j set, top bit clear); form 3 drops that compare too: with
+// the dummy at c = 2^31 the mover is just bit j of c (j <= 28 since L < 2^29), and both
+// selects are v_bfi_b32 on sign-extended bits — six VALU per pick, no lane-mask write
+// (form 1: two compares, four selects, and the wait states between a compare and its
+// select).  All three move the same records: bit-identical outputs.
 __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint32_t j) {
     const uint32_t cs = (uint32_t)self, cr = (uint32_t)right;
+    if constexpr (FLTEE_CP_PICK == 3) {
+        uint32_t lo, hi, e, em;
+        const uint32_t dmy = 0x80000000u;
+        asm("v_bfe_i32 %2, %4, %8, 1\n\t"        // e = ~0 iff self leaves (bit j of its c)
+            "v_bfe_i32 %3, %6, %8, 1\n\t"        // em = ~0 iff right moves in
+            "v_bfi_b32 %0, %2, %9, %4\n\t"       // stay c: the dummy's when self leaves
+            "v_bfi_b32 %1, %2, 0, %5\n\t"        // stay val: +0.0 when self leaves
+            "v_bfi_b32 %0, %3, %6, %0\n\t"       // right's c if it moves in
+            "v_bfi_b32 %1, %3, %7, %1"             // right's val if it moves in
+            : "=&v"(lo), "=&v"(hi), "=&v"(e), "=&v"(em)
+            : "v"(cs), "v"((uint32_t)(self >> 32)), "v"(cr), "v"((uint32_t)(right >> 32)), "s"(j),
+              "s"(dmy));
+        return ((uint64_t)hi << 32) | lo;
+    }
+    if constexpr (FLTEE_CP_PICK == 2) {
+        uint32_t e, shi;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(e) : "v"(cs), "s"(j));
+        asm("v_bfi_b32 %0, %1, 0, %2" : "=v"(shi) : "v"(e), "v"((uint32_t)(self >> 32)));
+        const uint64_t stay = ((uint64_t)shi << 32) | (cs | e);
+        const uint32_t m = 1u << j;
+        return (cr & (m | 0x80000000u)) == m ? right : stay;
+    }
     const bool mv = ((cr >> j) & ~(cr >> 31)) & 1u;
     const bool st = !((cs >> j) & 1u);
     return mv ? right : (st ? self : CP_DUMMY);
@@ -372,6 +411,19 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_PER16
 #define FLTEE_FC_PER16 0
 #endif
+// FLTEE_FC_FIXED_WALK (round 5, default): the fold's lane walks have a trip count fixed by
+// the public sizes — every lane walks its slots plus lim (the longest legal run, n + 1)
+// with selects, instead of stopping at the end of its last run, whose position follows the
+// data (the run lengths: how many clients sent each index).  That walk grows with n, so
+// the fused kernel takes it only up to kFixedWalkMax; longer runs go to the streaming
+// fold (fixed Hr + C + 16 steps per lane) + the compaction.  A/B (`profiles/r05/ab/ab9_*`,
+// `ab10_*`, with cp_pick form 3): C3 (lim 101) 0.147 vs 0.135 ms with the data-dependent
+// walk; C5 (lim 1,001) through the streaming fold 12.33 vs 12.07 ms — the fused fixed
+// walk there took 11.4 ms alone.
+#ifndef FLTEE_FC_FIXED_WALK
+#define FLTEE_FC_FIXED_WALK 1
+#endif
+constexpr uint32_t kFixedWalkMax = 128;
 template <int NT, int PER, int FINAL, int XMAX, int BPC = FLTEE_FC_BLOCKS>
 __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
@@ -401,7 +453,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             const bool ok = p >= 0 && p < (long long)M && t + i * NT < Wn;
             const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
                 rs, (int)(ok ? (uint32_t)p * 8u : 0u), 0, 0);
-            pf[i] = ok ? (((uint64_t)x.y << 32) | x.x) : CP_DUMMY;
+            pf[i] = ok ? (((uint64_t)x.y << 32) | x.x) : CP_PAD;
         }
     };
     uint32_t tile = blockIdx.x;
@@ -430,7 +482,10 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             float acc = 0.0f;
             uint32_t k = 0;
             uint64_t rn = win[x0 < Wn ? x0 : Wn - 1];
-            for (uint32_t y = x0; y < Wn; ++y) {
+            // FLTEE_FC_FIXED_WALK: every lane walks exactly to x1 + lim (lim = the longest
+            // legal run, public), so the loop's trip count no longer follows the data
+            const uint32_t yend = FLTEE_FC_FIXED_WALK ? min(x1 + lim, Wn) : Wn;
+            for (uint32_t y = x0; y < yend; ++y) {
                 const int p = pw + (int)y;
                 const bool valid = p >= 0 && p < (int)L;
                 const uint64_t r = rn;
@@ -438,6 +493,18 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 const uint32_t ky = (uint32_t)r;
                 const bool head = y == 0 || p == 0 || ky != prevk;
                 prevk = ky;
+                if (FLTEE_FC_FIXED_WALK) {
+                    const bool ext = valid && !head;
+                    const float sum = __fadd_rn(acc, rec_val(r));
+                    if (run && !ext) win[y - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;
+                    acc = run && ext ? sum : acc;
+                    run = run && ext;
+                    const bool start = y < x1 && valid && head;
+                    acc = start ? rec_val(r) : acc;
+                    k = start ? ky : k;
+                    run = run || start;
+                    continue;
+                }
                 if (run) {
                     if (valid && !head) {
                         acc = __fadd_rn(acc, rec_val(r));
@@ -592,6 +659,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     // levels, as slow as 4 of 5, `ab11_*`.)
     if (!g_fold_compact || d == 0 || L <= d || Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
         return hipErrorNotSupported;
+    if (FLTEE_FC_FIXED_WALK && lim > kFixedWalkMax) return hipErrorNotSupported;  // streaming fold
     const uint32_t nlev = bitlen(L - d);
     const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1;
     // records per lane: the fewest (4, 6 or 8) that still leave at most one tile per CU —
