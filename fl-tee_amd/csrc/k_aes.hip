@@ -532,7 +532,8 @@ hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_pe
                                 uint64_t block_off, uint32_t idx_sub, hipStream_t s,
                                 uint32_t *zero_word) {
     const size_t bpcl = (rec_per_client + 1) / 2;
-    if (n == 0 || bpcl == 0) return hipSuccess;
+    if (n == 0 || bpcl == 0)  // nothing to decrypt; the word still has to read 0
+        return zero_word ? hipMemsetAsync(zero_word, 0, 4, s) : hipSuccess;
     const bool aligned = bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0;
     // windows of 512 counter blocks (absolute counter space) touching each client's slice
     const uint64_t wpc = (block_off + bpcl - 1) / kAesWindow4 - block_off / kAesWindow4 + 1;

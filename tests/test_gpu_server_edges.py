@@ -95,6 +95,24 @@ def test_ragged_payload(enclave, oracle, alg):
 
 
 @pytest.mark.parametrize("alg", [1, 3, 4, 5])
+def test_sub_record_payload_after_a_rejected_call(enclave, oracle, alg):
+    # 4 bytes per client: lib.rs:305 floors to zero records, so nothing is decrypted — the
+    # small-call path still has to clear the status word the rejected call before it left
+    # set (an index out of range).
+    ids = np.array([3, 4], np.uint32)
+    d, k = 50, 5
+    bad = [oracle.as_weights(np.array([0, 1, 2, 3, 99], np.uint32),
+                             np.ones(5, np.float32)).tobytes()] * 2
+    fl = 70 + alg
+    (st, rv, _, _), (ost, _, _) = both(enclave, oracle, fl, ids, d, k, 4,  # non_oblivious
+                                        oracle.encrypt_clients(ids, bad))
+    assert st == 0 and rv == ost == 2
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, fl + 100, ids, d, k, alg, b"\x05" * 8)
+    assert (st, rv) == (0, ost) == (0, 0)
+    assert bits_equal(out, ref) and not out.any()
+
+
+@pytest.mark.parametrize("alg", [1, 3, 4, 5])
 def test_single_client_dense(enclave, oracle, alg):
     rng = np.random.default_rng(10 + alg)
     d = 777
