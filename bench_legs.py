@@ -37,6 +37,8 @@ WORKLOADS = {
                 desc="exp5's smallest advanced row: MLP-MNIST n=3 alpha=0.01 (M = 2^16)"),
     "a30": dict(alg=1, n=30, d=50890, k=5089,
                 desc="exp5's MLP-MNIST n=30 alpha=0.1 advanced row (M = 2^18)"),
+    "a300": dict(alg=1, n=300, d=50890, k=508,
+                 desc="exp5's MLP-MNIST n=300 alpha=0.01 advanced row (M = 2^18, runs up to 301)"),
     "c3": dict(alg=1, n=100, d=50890, k=5089,
                desc="configs[2]: MLP-MNIST num_users=1000 frac=0.1 alpha=0.1 (n=100), advanced"),
     "c4": dict(alg=2, n=300, d=44964, k=4496, dp=True,

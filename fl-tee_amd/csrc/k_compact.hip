@@ -411,19 +411,28 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_PER16
 #define FLTEE_FC_PER16 0
 #endif
-// FLTEE_FC_FIXED_WALK (round 5, default): the fold's lane walks have a trip count fixed by
-// the public sizes — every lane walks its slots plus lim (the longest legal run, n + 1)
-// with selects, instead of stopping at the end of its last run, whose position follows the
-// data (the run lengths: how many clients sent each index).  That walk grows with n, so
+// FLTEE_FC_FIXED_WALK (round 5): the fold's lane walks have a trip count fixed by the
+// public sizes, instead of stopping at the end of the lane's last run, whose position
+// follows the data (the run lengths: how many clients sent each index).  1: every lane
+// walks its slots plus lim (the longest legal run, n + 1) forward from its heads with
+// selects and conditional stores; 2 (default): every lane walks back lim slots and forward
+// through its own, branch-free, and stores its own slots' sums after a barrier.  That walk grows with n, so
 // the fused kernel takes it only up to kFixedWalkMax; longer runs go to the streaming
 // fold (fixed Hr + C + 16 steps per lane) + the compaction.  A/B (`profiles/r05/ab/ab9_*`,
 // `ab10_*`, with cp_pick form 3): C3 (lim 101) 0.147 vs 0.135 ms with the data-dependent
 // walk; C5 (lim 1,001) through the streaming fold 12.33 vs 12.07 ms — the fused fixed
 // walk there took 11.4 ms alone.
 #ifndef FLTEE_FC_FIXED_WALK
-#define FLTEE_FC_FIXED_WALK 1
+#define FLTEE_FC_FIXED_WALK 2
 #endif
-constexpr uint32_t kFixedWalkMax = 128;
+#ifndef FLTEE_FC_WALK_MAX
+#define FLTEE_FC_WALK_MAX 128
+#endif
+constexpr uint32_t kFixedWalkMax = FLTEE_FC_WALK_MAX;
+// form 2's LDS read-ahead depth (1: the next slot only)
+#ifndef FLTEE_FC_RA
+#define FLTEE_FC_RA 1
+#endif
 template <int NT, int PER, int FINAL, int XMAX, int BPC = FLTEE_FC_BLOCKS>
 __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
@@ -468,6 +477,67 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        if constexpr (FLTEE_FC_FIXED_WALK == 2) {
+            // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
+            // in-order sum of its run up to that slot: a walk from x0 - lim (every legal run
+            // of an owned slot starts after it), lim + chunk steps whatever the data, no
+            // branch, the next slot's LDS read issued a step ahead.  The sums go to their own
+            // LDS array (sums[], after the window), so no lane overwrites what another still
+            // reads; a run's last slot then holds the run's sum — all the compaction reads.
+            float *sums = reinterpret_cast<float *>(win + Wn);
+            const int x0 = (int)(t * chunk), ys = x0 - (int)lim;
+            const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
+            auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
+            uint32_t prevk = 0xFFFFFFFFu;
+            bool have = false;
+            float acc = 0.0f;
+            // (bitwise tests: short-circuit ones turned into EXEC-mask juggling)
+            auto step = [&](uint64_t r, int y) {
+                const uint32_t p = (uint32_t)(pw + y);  // a position < 0 wraps past L
+                const bool valid = ((uint32_t)y < Wn) & (p < L);
+                const uint32_t ky = (uint32_t)r;
+                const bool cont = have & valid & (p != 0u) & (ky == prevk);
+                const float v = rec_val(r);
+                acc = cont ? __fadd_rn(acc, v) : v;
+                prevk = ky;
+                have = valid;
+            };
+            if constexpr (FLTEE_FC_RA > 1) {
+                // one loop of lim + chunk steps (the same count in every lane), FLTEE_FC_RA
+                // LDS reads in flight ahead of the step that uses them
+                const uint32_t T = lim + chunk;
+                uint64_t ring[FLTEE_FC_RA];
+#pragma unroll
+                for (int k = 0; k < FLTEE_FC_RA; ++k) ring[k] = rd(ys + k);
+                for (uint32_t s0 = 0; s0 < T; s0 += FLTEE_FC_RA) {
+#pragma unroll
+                    for (int k = 0; k < FLTEE_FC_RA; ++k) {
+                        const uint32_t q = s0 + (uint32_t)k;
+                        const uint64_t r = ring[k];
+                        ring[k] = rd(ys + (int)q + FLTEE_FC_RA);
+                        if (q < T) {
+                            const int y = ys + (int)q;
+                            step(r, y);
+                            if (q >= lim && y < (int)Wn) sums[y] = acc;
+                        }
+                    }
+                }
+            } else {
+                uint64_t rn = rd(ys);
+                for (uint32_t q = 0; q < lim; ++q) {  // the same trip count in every lane
+                    const uint64_t r = rn;
+                    rn = rd(ys + (int)q + 1);
+                    step(r, ys + (int)q);
+                }
+                for (uint32_t i = 0; i < chunk; ++i) {
+                    const int y = x0 + (int)i;
+                    const uint64_t r = rn;
+                    rn = rd(y + 1);
+                    step(r, y);
+                    if (y < (int)Wn) sums[y] = acc;
+                }
+            }
+        } else
         // Each lane owns window slots [x0, x1) and folds the runs whose heads lie there,
         // left to right: one loop that goes past x1 only to finish its last run, so a
         // wave's trip count is about chunk + the longest run (a loop per head nested in
@@ -540,9 +610,10 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             const uint32_t idx = (uint32_t)r;
             over |= f < S && p < (long long)L && p >= (long long)lim && (uint32_t)win[x - lim] == idx;
             const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-            v[i] = (p < (long long)L && idx < d && end)
-                       ? ((r & 0xFFFFFFFF00000000ull) | (uint32_t)((uint32_t)p - idx))
-                       : CP_DUMMY;
+            const uint64_t hi = FLTEE_FC_FIXED_WALK == 2
+                                    ? (uint64_t)__float_as_uint(reinterpret_cast<const float *>(win + Wn)[x]) << 32
+                                    : (r & 0xFFFFFFFF00000000ull);
+            v[i] = (p < (long long)L && idx < d && end) ? (hi | (uint32_t)((uint32_t)p - idx)) : CP_DUMMY;
         }
         if (over) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
         __syncthreads();
@@ -681,7 +752,8 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const uint64_t ntiles = (L + S - 1) / S;
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 256u * bpc ? ntiles : 256u * bpc);
-    const size_t lds = (Hr + CAP + 1) * 8;
+    // the window, and (fixed walk, form 2) the run sums beside it
+    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK == 2 ? (Hr + CAP + 1) * 4 : 0);
     // the resident blocks per CU must fit the 160 KiB LDS at the largest window
     static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
     static_assert((1023 + 8 * 1024 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU (8,192 records)");

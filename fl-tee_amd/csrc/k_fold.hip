@@ -194,6 +194,9 @@ uint32_t fold_run_limit(size_t halo) {
     return halo + 1 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(halo + 1);
 }
 
+#ifndef FLTEE_FS_DOUBLE_WAVES
+#define FLTEE_FS_DOUBLE_WAVES 1024
+#endif
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
                              uint32_t *status, hipStream_t s) {
@@ -223,7 +226,7 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     while (C > FS_W && span / (64 * C) < 1024) C >>= 1;
     // one doubling more while >= 1024 waves remain: less halo re-read (C5: 2048 instead
     // of 1024, 620 vs 643 us; 4096: 700 us, 8192: 1220 us — too few waves in flight)
-    if (C >= Hr && span / (64 * 2 * C) >= 1024) C <<= 1;
+    if (C >= Hr && span / (64 * 2 * C) >= FLTEE_FS_DOUBLE_WAVES) C <<= 1;
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     net_account((uint64_t)16 * span, "fold_stream_kernel", s);
