@@ -64,7 +64,8 @@ def compact_line(full):
     if rf:
         line["roofline"] = {k: _r(rf.get(k), 5) for k in
                             ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
-                             "kernel_ms", "algorithmic_bytes", "rocprof_avg_us")
+                             "kernel_ms", "algorithmic_bytes", "rocprof_avg_us", "read_floor_gbs",
+                             "frac_of_floor")
                             if k in rf}
     cb = full.get("cpu_baseline")
     if cb:
@@ -393,6 +394,12 @@ def main():
                               note="cold: inputs rotated over > 1.5 x 256 MiB; best of the trials "
                                    "(kernel_ms) and their median (kernel_ms_median)"),
                 read_floor=floor)
+            # the headline kernel against a plain streaming read of its own 804 MB, same run:
+            # the practical ceiling beside the 8 TB/s peak
+            if "roofline" in full:
+                nsf = read_floor(torch, algo_bytes, device, reps=2, steps=20)
+                full["roofline"]["read_floor_gbs"] = nsf["gbs"]
+                full["roofline"]["frac_of_floor"] = nsf["us"] / 1e6 / kern
             if not args.no_cpu_baseline and not args.no_cpu_configs:
                 gms = {nm: e["kernel_ms"] for nm, e in full["extra"].items()}
                 full["cpu_baseline_configs"] = cpu_baseline_configs(gms)

@@ -425,10 +425,18 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_FIXED_WALK
 #define FLTEE_FC_FIXED_WALK 2
 #endif
+// The fixed walk's bound: lim <= 128 at any size, <= 320 on arrays of <= 2^20 records,
+// where the streaming fold's launch and latency cost more than the longer walk (MLP-MNIST
+// n = 300, lim 301: 0.101 vs 0.138 ms, `profiles/r05/ab/ab12_*`); 320 keeps three windows
+// + sums per CU in the 160 KiB of LDS.
 #ifndef FLTEE_FC_WALK_MAX
 #define FLTEE_FC_WALK_MAX 128
 #endif
+#ifndef FLTEE_FC_WALK_MAX_SMALL
+#define FLTEE_FC_WALK_MAX_SMALL 320
+#endif
 constexpr uint32_t kFixedWalkMax = FLTEE_FC_WALK_MAX;
+constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
 // form 2's LDS read-ahead depth (1: the next slot only)
 #ifndef FLTEE_FC_RA
 #define FLTEE_FC_RA 1
@@ -730,7 +738,9 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     // levels, as slow as 4 of 5, `ab11_*`.)
     if (!g_fold_compact || d == 0 || L <= d || Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
         return hipErrorNotSupported;
-    if (FLTEE_FC_FIXED_WALK && lim > kFixedWalkMax) return hipErrorNotSupported;  // streaming fold
+    if (FLTEE_FC_FIXED_WALK && lim > kFixedWalkMax &&
+        !(lim <= kFixedWalkMaxSmall && M <= ((size_t)1 << 20)))
+        return hipErrorNotSupported;  // the streaming fold
     const uint32_t nlev = bitlen(L - d);
     const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1;
     // records per lane: the fewest (4, 6 or 8) that still leave at most one tile per CU —
