@@ -216,3 +216,53 @@ def test_nips19_uses_request_k(enclave, oracle, k_req):
     assert (st, rv, ost) == (0, 0, 0)
     assert bits_equal(out, ref)
     set_debug_seed(0)
+
+
+@pytest.mark.parametrize("alg", [1, 6])
+def test_small_calls_replay_their_captured_graph(enclave, oracle, alg):
+    """From the second call of one shape on, a small `advanced` / alg-6 ECALL replays its
+    device work as a captured graph (ecalls.hip staged_ecall): every call must still read
+    its own payload — new values, a rejected upload (status word) in between, another
+    shape in between — and match the oracle bit for bit."""
+    rng = np.random.default_rng(90 + alg)
+    d, k = 3000, 40
+
+    def payload(ids, kk, dup=False):
+        plain = []
+        for _ in ids:
+            idx = rng.choice(d, kk, replace=False).astype(np.uint32)
+            if dup:
+                idx[1] = idx[0]  # a repeated index: a run of n + 2 entries is possible
+            plain.append(oracle.as_weights(idx, rng.normal(0, 1, kk).astype(np.float32)).tobytes())
+        return oracle.encrypt_clients(ids, plain)
+
+    def call(fl, ids, kk, enc):
+        O = oracle.OracleEnclave(seed=SEED)
+        run_round(enclave, ids, d, kk, alg, enc, fl)
+        O.fl_init(fl, ids, d, kk, 1.12, 1.0, 0.1, 1.0, alg)
+        O.start_round(fl, 0, len(ids))
+        if alg == 6:
+            st, rv, out, _ = enclave.ecall_client_size_optimized_secure_aggregation(
+                fl, 0, 2, ids, enc, d, kk, 6)
+            ost, ref, _ = O.client_size_optimized_secure_aggregation(fl, 0, 2, ids, enc, d, kk, 6)
+        else:
+            st, rv, out, _ = enclave.ecall_secure_aggregation(fl, 0, ids, enc, d, kk, alg)
+            ost, ref, _ = O.secure_aggregation(fl, 0, ids, enc, d, kk, alg)
+        return st, rv, out, ost, ref
+
+    ids = np.array([11, 12, 13, 14, 15], np.uint32)
+    fl = 900 + 20 * alg
+    for r in range(6):
+        kk = 25 if r == 3 else k  # round 3: another shape, then back
+        dup = r == 4 and len(ids) == 1
+        st, rv, out, ost, ref = call(fl + r, ids, kk, payload(ids, kk, dup))
+        assert st == 0 and rv == ost == 0, (r, rv, ost)
+        assert bits_equal(out, ref), r
+    # a run longer than n + 1 through the replayed graph: the status word still reaches
+    # the retval (0x2), and the next call of the shape is clean again
+    one = np.array([21], np.uint32)
+    for r in range(3):
+        st, rv, out, ost, ref = call(fl + 10 + r, one, k, payload(one, k, dup=(r == 1)))
+        assert st == 0 and rv == (2 if r == 1 else 0)
+        if r != 1:
+            assert ost == 0 and bits_equal(out, ref)
