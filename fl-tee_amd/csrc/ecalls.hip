@@ -252,8 +252,6 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
 // the rest of the call (alg 6: [1] = decrypt + aggregate, [2] = 0, lib.rs:425-592).
 // alg: an ECALL alg, or FLTEE_ALG_OPTIMIZED with batch.
 constexpr size_t kStagedBytes = (size_t)16 << 20;
-static int g_capture_fail = 0;            // fltee_debug_call_graphs: the last capture's failure
-static uint64_t g_graph_launches = 0;     // ... and the replays so far
 constexpr size_t kZeroCopyBytes = (size_t)256 << 10;
 
 __global__ __launch_bounds__(256) void copy_out_kernel(const uint4 *__restrict__ src,
@@ -321,56 +319,14 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
         return launch_copy_out(d_out, c->pin_out.dptr, d4 + 16, s) == hipSuccess
                    ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
     };
-    // Launch-bound shapes: `advanced` / alg 6 on a small payload is ~12 kernels of a few
-    // us each, and the host's launch calls (4-7 us each) set the pace
-    // (`profiles/r05/small_ecall/after_r05i_*`).  From the second call of one shape on,
-    // its device work (no host sync inside, no per-call argument: the zero-copy path, no
-    // DP) is captured once as a graph and replayed with one launch.  The call's bytes
-    // change, the addresses do not (a buffer that moves changes buffer_epoch, the key).
-    const bool graphable = zero_copy && cb > 0 && !cfg.dp &&
-                           (alg == FLTEE_ALG_ADVANCED || alg == FLTEE_ALG_OPTIMIZED);
-    const uint64_t key[8] = {alg, n, bpc, d, k_req, batch,
-                             (uint64_t)exact_runs_default() | ((uint64_t)oram_tree_default() << 1),
-                             buffer_epoch()};
-    if (graphable && std::memcmp(c->call_key, key, sizeof key) != 0) {
-        if (c->call_graph) (void)hipGraphExecDestroy(c->call_graph);
-        c->call_graph = nullptr;
-        std::memcpy(c->call_key, key, sizeof key);
-        c->call_seen = 0;
-        c->call_graph_bad = false;
-    }
-    if (graphable) ++c->call_seen;
-    if (graphable && !c->call_graph && !c->call_graph_bad && c->call_seen >= 2) {
-        hipGraph_t g = nullptr;
-        hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
-        int step = 1;
-        if (e == hipSuccess) {
-            const uint32_t q = enqueue(false);
-            const hipError_t e2 = hipStreamEndCapture(s, &g);
-            step = q != FLTEE_SUCCESS ? 2 : e2 != hipSuccess ? 3 : !g ? 4 : 0;
-            e = q != FLTEE_SUCCESS ? hipGetLastError() : e2;
-            if (step == 0) {
-                e = hipGraphInstantiate(&c->call_graph, g, nullptr, nullptr, 0);
-                if (e != hipSuccess) step = 5;
-            }
-            if (g) (void)hipGraphDestroy(g);
-        }
-        g_capture_fail = step ? step * 1000 + (int)e : 0;
-        if (step) {  // not capturable here: this shape keeps plain launches
-            c->call_graph = nullptr;
-            c->call_graph_bad = true;
-            (void)hipGetLastError();
-        }
-    }
-    if (graphable && c->call_graph) ++g_graph_launches;
+    // (Round 5, measured and not kept: this device work captured once per call shape as a
+    // graph and replayed with one launch — MLP-MNIST n = 3 `advanced` 99-119 vs 101-110 us
+    // per call: the replay still dispatches kernel by kernel, `profiles/r05/small_ecall/
+    // graph_replay_r05g2.jsonl`.)
     uint32_t st = FLTEE_SUCCESS;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (attempt == 0 && graphable && c->call_graph) {
-            if (hipGraphLaunch(c->call_graph, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-        } else {
-            st = enqueue(attempt > 0);
-            if (st != FLTEE_SUCCESS) return st;
-        }
+        st = enqueue(attempt > 0);
+        if (st != FLTEE_SUCCESS) return st;
         if (hipStreamSynchronize(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         bool retry = false;
         st = status_to_retval(*(const volatile uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg,
@@ -834,14 +790,6 @@ extern "C" int fltee_debug_session_round_keys(const uint32_t *ids, size_t n, uin
 
 // CPU self-test hook: one AES-128 block with the library's tables (no GPU).
 namespace fltee { void aes128_encrypt_block_host(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]); }
-// small-call graphs (staged_ecall): replays so far, and the last failed capture as
-// step * 1000 + hipError (0: none)
-extern "C" void fltee_debug_call_graphs(uint64_t *replays, int *last_capture_failure) {
-    std::lock_guard<std::recursive_mutex> lk(api_mutex());
-    if (replays) *replays = g_graph_launches;
-    if (last_capture_failure) *last_capture_failure = g_capture_fail;
-}
-
 extern "C" void fltee_debug_aes_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
     fltee::aes128_encrypt_block_host(key, in, out);
 }

@@ -23,9 +23,6 @@ struct HostBuffer {
     bool reserve(size_t bytes);
 };
 
-// bumped whenever a grow-only buffer moves (captured graphs hold its pointers)
-uint64_t buffer_epoch();
-
 struct DeviceCtx {
     bool ready = false;
     int device = -1;
@@ -39,12 +36,6 @@ struct DeviceCtx {
     Buffer stage;                                        // small ECALLs: out, status, keys, ciphertext
     HostBuffer pin_in, pin_out;                          // small ECALLs: pinned staging both ways
     hipEvent_t call_ev[3] = {};                          // small ECALLs: the phase timers
-    // small ECALLs: the device work of one call shape captured as a graph and replayed
-    // (ecalls.hip staged_ecall); call_key = the shape, call_seen = its calls so far
-    hipGraphExec_t call_graph = nullptr;
-    uint64_t call_key[8] = {};
-    uint32_t call_seen = 0;
-    bool call_graph_bad = false;
     Buffer ws_client, ws_client_coef;                   // client-side producers
     Buffer ws_cnt, ws_sel;                               // nips19's selected list
     Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch

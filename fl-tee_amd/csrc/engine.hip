@@ -106,12 +106,8 @@ DeviceCtx *current_ctx() {
     return device_ctx(dev);
 }
 
-static std::atomic<uint64_t> g_buffer_epoch{0};
-uint64_t buffer_epoch() { return g_buffer_epoch.load(); }
-
 bool Buffer::reserve(size_t bytes) {
     if (bytes <= cap) return true;
-    ++g_buffer_epoch;  // a pointer changes: captured call graphs are stale
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
@@ -123,7 +119,6 @@ bool Buffer::reserve(size_t bytes) {
 
 bool HostBuffer::reserve(size_t bytes) {
     if (bytes <= cap) return true;
-    ++g_buffer_epoch;
     if (ptr) (void)hipHostFree(ptr);
     ptr = dptr = nullptr;
     cap = 0;

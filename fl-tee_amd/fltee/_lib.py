@@ -103,7 +103,6 @@ EXTRA_SIGNATURES = {  # test hooks not in the public header
     "fltee_debug_set_dense_variant": (None, [ctypes.c_int]),
     "fltee_debug_set_oram_bucket": (None, [ctypes.c_int]),
     "fltee_debug_set_aes_variant": (None, [ctypes.c_int]),
-    "fltee_debug_call_graphs": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]),
     "fltee_debug_read_floor": (ctypes.c_int, [_P, _S, _P, ctypes.c_uint, _P]),
     "fltee_debug_network_plan": (_S, [_U32, _U32, _U32, ctypes.c_int, _P, _S]),
     "fltee_debug_pad_units": (None, [_U32] * 8 + [_P]),

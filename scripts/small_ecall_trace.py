@@ -48,13 +48,8 @@ for n, k in shapes:
                 walls.append(w * 1e6)
                 ph.append([float(x) * 1e3 for x in tt])
         p = np.mean(np.array(ph), axis=0)
-        import ctypes
-        from fltee import _lib
-        rep, fail = ctypes.c_uint64(0), ctypes.c_int(0)
-        _lib.lib().fltee_debug_call_graphs(ctypes.byref(rep), ctypes.byref(fail))
         print(json.dumps(dict(n=n, k=k, alg=name, payload_bytes=n * k * 8, reps=reps,
                               wall_us_mean=float(np.mean(walls)), wall_us_min=float(np.min(walls)),
                               load_us=float(p[0]), decrypt_us=float(p[1]), aggregate_us=float(p[2]),
-                              t_start=t_start, graph_replays=rep.value,
-                              last_capture_failure=fail.value)), flush=True)
+                              t_start=t_start)), flush=True)
 E.destroy()

@@ -219,11 +219,11 @@ def test_nips19_uses_request_k(enclave, oracle, k_req):
 
 
 @pytest.mark.parametrize("alg", [1, 6])
-def test_small_calls_replay_their_captured_graph(enclave, oracle, alg):
-    """From the second call of one shape on, a small `advanced` / alg-6 ECALL replays its
-    device work as a captured graph (ecalls.hip staged_ecall): every call must still read
-    its own payload — new values, a rejected upload (status word) in between, another
-    shape in between — and match the oracle bit for bit."""
+def test_repeated_small_calls_of_one_shape(enclave, oracle, alg):
+    """Small `advanced` / alg-6 ECALLs of one shape, back to back, through the zero-copy
+    staging (ecalls.hip staged_ecall): every call must read its own payload — new values,
+    a rejected upload (status word) in between, another shape in between — and match the
+    oracle bit for bit."""
     rng = np.random.default_rng(90 + alg)
     d, k = 3000, 40
 
