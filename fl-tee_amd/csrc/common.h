@@ -159,11 +159,14 @@ size_t fold_context(size_t halo);  // records of context the fold re-reads: halo
 // property of the data alone, checked in the same single pass (no rerun: the caller
 // rejects the call); below it the sums are exact.
 uint32_t fold_run_limit(size_t halo);
+// cemit_d != 0: emit the compaction's first-pass form instead (run ends with idx < cemit_d
+// as (c = p - idx, sum), the rest as cdummy; whole arrays only: origin = pbase = 0)
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
-                             uint32_t *status, hipStream_t s);
+                             uint32_t *status, hipStream_t s, size_t cemit_d = 0,
+                             uint64_t cdummy = 0);
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
-                       uint32_t *status, hipStream_t s);
+                       uint32_t *status, hipStream_t s, size_t cemit_d = 0, uint64_t cdummy = 0);
 hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
                           hipStream_t s);
 // k_compact.hip
@@ -173,6 +176,10 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
                                        uint32_t *status, hipStream_t s);
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
                                   float *out, bool accumulate, hipStream_t s);
+// the same from launch_fold(..., cemit_d = d, compact_dummy())'s output
+uint64_t compact_dummy();
+hipError_t launch_compact_extract_converted(uint64_t *src, uint64_t *tmp, size_t L, size_t d,
+                                            float coef, float *out, bool accumulate, hipStream_t s);
 hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint64_t *buf,
                                  uint64_t *tmp, float coef, float *out, hipStream_t s);
 hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t m, uint64_t *keys,

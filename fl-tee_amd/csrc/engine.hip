@@ -315,6 +315,9 @@ static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, 
 }
 
 // `advanced` over n clients' records into out (coef or accumulate).
+#ifndef FLTEE_FOLD_CEMIT
+#define FLTEE_FOLD_CEMIT 1
+#endif
 static bool g_advanced_compaction = true;  // fltee_debug_set_advanced_compaction
 static bool g_nips19_fused_select = true;  // fltee_debug_set_nips19_fused_select (A/B)
 
@@ -343,6 +346,13 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         // read as the run-end test of L - 1), not the pads after it
         size_t mf = (L + 1 + 15) / 16 * 16;
         if (mf > M) mf = M;
+        // the fold emits the compaction's first-pass form (no conversion there, 16-B pairs;
+        // FLTEE_FOLD_CEMIT=0: the enclave's folded array, converted by that pass)
+        if (FLTEE_FOLD_CEMIT) {
+            e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s, d, compact_dummy());
+            if (e != hipSuccess) return e;
+            return launch_compact_extract_converted(B, A, L, d, coef, out, acc, s);
+        }
         e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s);
         if (e != hipSuccess) return e;
         return launch_compact_extract(B, A, L, d, coef, out, acc, s);

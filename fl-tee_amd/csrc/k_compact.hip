@@ -274,8 +274,9 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
 #define CP_GO(F, X, V)                                                                           \
     hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
                        d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
-    // 16-B slot pairs: rows of >= 2 residues, L even, both buffers 16-B aligned
-    const bool v2 = FLTEE_COMPACT_V2 && !first && logW >= 1 && L % 2 == 0 &&
+    // 16-B slot pairs: rows of >= 2 residues (or a contiguous tile of an even S: the
+    // converted first pass), L even, both buffers 16-B aligned
+    const bool v2 = FLTEE_COMPACT_V2 && !first && (logW >= 1 || S % 2 == 0) && L % 2 == 0 &&
                     (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
     if (first) {
         if (fin == 0) CP_GO(true, 0, false); else if (fin == 1) CP_GO(true, 1, false); else CP_GO(true, 2, false);
@@ -300,7 +301,7 @@ static uint32_t bitlen(uint64_t x) {
 // front of p); it sets the number of levels, bitlen(max_shift).
 static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t d,
                                  size_t max_shift, float coef, float *out, bool accumulate,
-                                 hipStream_t s, uint32_t j0_start = 0) {
+                                 hipStream_t s, uint32_t j0_start = 0, bool converted = false) {
     if (d == 0) return hipSuccess;
     const uint32_t nlev = bitlen(max_shift);
     if (nlev == 0) return launch_extract(src, d, coef, out, accumulate, s);
@@ -317,6 +318,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         if (j0 == 0) {
             logW = 0;
             S = CAP - H;
+            if (converted) S &= ~1u;  // even: 16-B slot pairs
         } else {
             logW = 4;  // 16 residues = 128-B row segments
             if (rows + H <= CAP >> logW) {  // one band: widen the rows instead
@@ -350,23 +352,30 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =
             small ? (blk >= 4
-                         ? launch_pass<512, 8, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                         ? launch_pass<512, 8, 8>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
                                                   out, (uint32_t)ntiles)
                      : blk == 3
-                         ? launch_pass<512, 8, 6>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                         ? launch_pass<512, 8, 6>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
                                                   out, (uint32_t)ntiles)
-                         : launch_pass<512, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L,
+                         : launch_pass<512, 8>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                (uint32_t)d, j0, G, logW, S, rows, ngroups, coef, out,
                                                (uint32_t)ntiles))
-                  : launch_pass<1024, 8>(j0 == 0, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
+                  : launch_pass<1024, 8>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L, (uint32_t)d, j0,
                                          G, logW, S, rows, ngroups, coef, out, (uint32_t)ntiles);
         if (e != hipSuccess) return e;
         uint64_t *x = cur; cur = oth; oth = x;
         j0 += G;
     }
     return hipSuccess;
+}
+
+uint64_t compact_dummy() { return CP_DUMMY; }
+
+hipError_t launch_compact_extract_converted(uint64_t *src, uint64_t *tmp, size_t L, size_t d,
+                                            float coef, float *out, bool accumulate, hipStream_t s) {
+    return compact_levels(src, tmp, L, d, L > d ? L - d : 0, coef, out, accumulate, s, 0, true);
 }
 
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,

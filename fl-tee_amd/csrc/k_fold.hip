@@ -77,13 +77,18 @@ __device__ __forceinline__ void wave_sync_lds() {
 // GPU's part of a position-sharded array, SURVEY §8e Option B): [0, origin) holds
 // >= Hr records of context from the previous range, and src[end] is the next
 // range's first record (or end + pbase >= fold_len).
-template <int DEPTH>
+// CEMIT (round 5): emit what the compaction's first pass would make of the folded array
+// — a run's last record as (sum, c = p - idx) when idx < dsel, every other position as the
+// compaction's unselected slot `cdummy` — so that pass needs no conversion (and may move
+// 16-B slot pairs); positions past fold_len are copied as before.
+template <int DEPTH, bool CEMIT = false>
 __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restrict__ src,
                                                          uint64_t *__restrict__ dst, long long m,
                                                          long long origin, long long end,
                                                          long long pbase, long long fold_len,
                                                          uint32_t Hr, uint32_t C, uint32_t lim,
-                                                         uint32_t *status) {
+                                                         uint32_t *status, uint32_t dsel = 0,
+                                                         uint64_t cdummy = 0) {
     __shared__ uint64_t win[2][64 * FS_ROW];
     const uint32_t l = threadIdx.x;
     const long long wave0 = origin + (long long)blockIdx.x * 64 * C;  // first position of lane 0
@@ -147,10 +152,17 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             const long long qg = q + pbase;
             const uint32_t ci = rec_idx(r[t]);
             const bool eq = started && ci == pre_idx;
-            const uint64_t emit =
-                (qg - 1 >= fold_len) ? prev
-                : (qg < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
-                                        : make_rec(pre_idx, pre_val);
+            uint64_t emit;
+            if constexpr (CEMIT) {
+                emit = (qg - 1 >= fold_len) ? prev
+                       : (qg < fold_len && eq) || pre_idx >= dsel
+                           ? cdummy
+                           : make_rec((uint32_t)(qg - 1) - pre_idx, pre_val);  // (c, sum)
+            } else {
+                emit = (qg - 1 >= fold_len) ? prev
+                       : (qg < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
+                                               : make_rec(pre_idx, pre_val);
+            }
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
             if (q >= 0 && qg >= 0) {
@@ -199,7 +211,10 @@ uint32_t fold_run_limit(size_t halo) {
 #endif
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
-                             uint32_t *status, hipStream_t s) {
+                             uint32_t *status, hipStream_t s, size_t cemit_d,
+                             uint64_t cdummy) {
+    const bool cemit = cemit_d != 0;
+    if (cemit && (origin != 0 || pbase != 0 || cemit_d > 0xFFFFFFFFull)) return hipErrorInvalidValue;
     // runs of more than halo + 1 entries are reported, wherever they lie (fold_run_limit)
     const uint32_t lim = fold_run_limit(halo);
     if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
@@ -212,9 +227,14 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
         const size_t C1 = (span + FS_W - 1) / FS_W * FS_W;
         if (C1 > 0x7FFFFFFFull) return hipErrorInvalidValue;
         net_account((uint64_t)16 * span, "fold_stream_kernel", s);
-        hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
-                           0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
-                           0xFFFFFFFFu, status);
+        if (cemit)
+            hipLaunchKernelGGL((fold_stream_kernel<2, true>), dim3(1), dim3(64), 0, s, src, dst,
+                               (long long)m, 0ll, (long long)end, 0ll, (long long)fold_len, 0u,
+                               (uint32_t)C1, 0xFFFFFFFFu, status, (uint32_t)cemit_d, cdummy);
+        else
+            hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
+                               0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
+                               0xFFFFFFFFu, status, 0u, 0ull);
         return hipGetLastError();
     }
     const size_t Hr = fold_context(halo);
@@ -234,22 +254,28 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     // about one wave per CU: latency-bound, prefetch deeper (2 or 4 stages were no faster
     // on the large arrays, profiles/r01/ab/fold_chunk_depth*.jsonl)
     const int depth = blocks <= 256 ? 2 : 1;
-#define FS_GO(D_)                                                                                  \
-    hipLaunchKernelGGL(fold_stream_kernel<D_>, dim3((unsigned)blocks), dim3(64), 0, s, src, dst,   \
-                       (long long)m, (long long)origin, (long long)end, pbase, (long long)fold_len, \
-                       (uint32_t)Hr, (uint32_t)C, lim, status)
-    if (depth == 2) FS_GO(2);
-    else FS_GO(1);
+#define FS_GO(D_, E_)                                                                              \
+    hipLaunchKernelGGL((fold_stream_kernel<D_, E_>), dim3((unsigned)blocks), dim3(64), 0, s, src,  \
+                       dst, (long long)m, (long long)origin, (long long)end, pbase,                \
+                       (long long)fold_len, (uint32_t)Hr, (uint32_t)C, lim, status,                \
+                       (uint32_t)cemit_d, cdummy)
+    if (depth == 2) {
+        if (cemit) FS_GO(2, true);
+        else FS_GO(2, false);
+    } else {
+        if (cemit) FS_GO(1, true);
+        else FS_GO(1, false);
+    }
 #undef FS_GO
     return hipGetLastError();
 }
 
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
-                       uint32_t *status, hipStream_t s) {
-    if (m == 1)  // nothing to fold: position 0 receives itself (:102-103)
+                       uint32_t *status, hipStream_t s, size_t cemit_d, uint64_t cdummy) {
+    if (m == 1 && !cemit_d)  // nothing to fold: position 0 receives itself (:102-103)
         return hipMemcpyAsync(dst, src, 8, hipMemcpyDeviceToDevice, s);
     if (m == 0 || (m & 1)) return hipErrorInvalidValue;  // m = next_pow2: 16-B windows
-    return launch_fold_range(src, dst, m, 0, m, 0, fold_len, halo, status, s);
+    return launch_fold_range(src, dst, m, 0, m, 0, fold_len, halo, status, s, cemit_d, cdummy);
 }
 
 template <bool ACC>
