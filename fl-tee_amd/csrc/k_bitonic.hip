@@ -125,6 +125,20 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 #ifndef FLTEE_TILE_W10
 #define FLTEE_TILE_W10 1
 #endif
+//   FLTEE_TILE_MINW14  the narrowest rows (log2 records) of a planned strided 2^14 tile: 4
+//   (128-B row segments) or 3 (64-B segments: 11 row steps per pass; the plan may then use
+//   rows of 2^8 too, compiled with it).  At M = 2^27 the plan drops from 23 to 22 launches,
+//   but the passes on 64-B rows run far slower (round 5, bit-identical: C5 12.29 -> 13.65
+//   ms, C4 7.85 -> 8.45 ms; tile passes 367 -> 447 us on average,
+//   `profiles/r05/ab/ab14_tile_rows_of_8_rejected.jsonl`), so 4 stays.
+#ifndef FLTEE_TILE_MINW14
+#define FLTEE_TILE_MINW14 4
+#endif
+//   FLTEE_TILE_MINW12  the same for the 512-lane 2^12 tiles (M <= 2^20: C3 13 -> 12 launches,
+//   0.1365 -> 0.1387 ms, same record)
+#ifndef FLTEE_TILE_MINW12
+#define FLTEE_TILE_MINW12 4
+#endif
 #ifndef FLTEE_DIRECT_MERGE
 #define FLTEE_DIRECT_MERGE 0
 #endif
@@ -1645,15 +1659,20 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
     // 14.03 ms at 2^27, the last round's 8-B stores land 2^dtile apart)
     // strided passes of the usual tile sizes, rows of 2^4 .. 2^7 (and, for 2^12 tiles, the
     // planned tiles' 2^8 .. 2^9, whose tails fill the consecutive bits): compile-time rounds
-    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= 4 && (1u << wlog) <= c.NT &&
+    const uint32_t wmin = c.NT == 1024 ? (uint32_t)FLTEE_TILE_MINW14 : (uint32_t)FLTEE_TILE_MINW12;
+    if (!SORT && ilog != 0 && wlog < c.tlog && wlog >= wmin && (1u << wlog) <= c.NT &&
         ((c.NT == 1024 && c.E == 16 && c.tlog == 14) || (c.NT == 512 && c.E == 8 && c.tlog == 12)) &&
-        (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512) || (FLTEE_TILE_W10 && c.NT == 1024 && wlog == 10))) {
+        (wlog <= 7 || (seg0 && MODE != 2 && c.NT <= 512) || (FLTEE_TILE_W10 && c.NT == 1024 && wlog == 10) ||
+         (FLTEE_TILE_MINW14 < 4 && c.NT == 1024 && wlog == 8))) {
 #define BT_ST_CASE(E_, NT_, TL_, W_)                                                               \
     case W_: return launch_tiles_e<MODE, SORT, E_, NT_, TL_, W_>(c.grid, c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, seg0, sw.in, c.hole_at, c.hole_len);
         if (c.NT == 1024) {
             switch (wlog) {
                 BT_ST_CASE(16, 1024, 14, 4) BT_ST_CASE(16, 1024, 14, 5) BT_ST_CASE(16, 1024, 14, 6)
                 BT_ST_CASE(16, 1024, 14, 7)
+#if FLTEE_TILE_MINW14 < 4
+                BT_ST_CASE(16, 1024, 14, 3) BT_ST_CASE(16, 1024, 14, 8)
+#endif
 #if FLTEE_TILE_W10
                 BT_ST_CASE(16, 1024, 14, 10)  // rows of 2^10 (the planned tails on 10 low bits)
 #endif
@@ -1663,6 +1682,9 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
             switch (wlog) {
                 BT_ST_CASE(8, 512, 12, 4) BT_ST_CASE(8, 512, 12, 5) BT_ST_CASE(8, 512, 12, 6)
                 BT_ST_CASE(8, 512, 12, 7)
+#if FLTEE_TILE_MINW12 < 4
+                BT_ST_CASE(8, 512, 12, 3)
+#endif
             default: break;
             }
             if constexpr (MODE != 2) {  // planned tiles only (the keyed shuffle runs per stage)
@@ -1899,9 +1921,16 @@ struct NetPass {
 };
 
 static std::vector<NetPass> plan_network(uint32_t mlog, uint32_t tlog, uint32_t NT, int rmax) {
-    const uint32_t minw = (uint32_t)kMinWLog;
+    const bool t14 = tlog == 14 && NT == 1024, t12 = tlog == 12 && NT == 512;
+    const uint32_t minw = t14 ? (uint32_t)FLTEE_TILE_MINW14
+                              : t12 ? (uint32_t)FLTEE_TILE_MINW12 : (uint32_t)kMinWLog;
     uint32_t ntl = 0;
     while ((1u << (ntl + 1)) <= NT) ++ntl;  // log2 NT: W <= NT for strided tiles
+    // narrower rows than 2^4: only the row widths launch_tiles has compile-time rounds for
+    auto w_ok = [&](uint32_t w) {
+        if (minw >= 4) return true;
+        return t14 ? ((w >= 3 && w <= 8) || (FLTEE_TILE_W10 && w == 10)) : (w >= 3 && w <= 9);
+    };
     // relative launch costs (MI355X rocprof, `profiles/r02/`): register passes R <= 4 one
     // unit (2^27: 268-280 us, 2^20: 4.5-5.2 us), R = 5 / 6 at 2^27 1.19 / 1.43; strided and
     // two-segment tiles 1.5 (2^27: 404 us) / 1.45 (2^20: 7.3 us); the direct contiguous merge
@@ -1959,7 +1988,7 @@ static std::vector<NetPass> plan_network(uint32_t mlog, uint32_t tlog, uint32_t 
         // middle of stage s (strided tile, low bits idle): steps b .. lo on the row bits
         for (uint32_t rows = 1; rows <= b && rows < tlog; ++rows) {
             const uint32_t lo = b - rows + 1, w = tlog - rows;
-            if (w < minw || w > ntl || lo < w) continue;
+            if (w < minw || w > ntl || lo < w || !w_ok(w)) continue;
             if (last_stage && lo < tlog) continue;
             NetPass p;
             p.ilogB = s; p.wlog = w; p.dtile = lo; p.stage = s;
@@ -1969,7 +1998,7 @@ static std::vector<NetPass> plan_network(uint32_t mlog, uint32_t tlog, uint32_t 
         if (s < mlog) {
             for (uint32_t rows = 1; rows < tlog; ++rows) {
                 const uint32_t w = tlog - rows;
-                if (w < b + 1 || w < minw || w > ntl) continue;
+                if (w < b + 1 || w < minw || w > ntl || !w_ok(w)) continue;
                 if (rows > s) break;
                 const uint32_t lo = s - rows + 1;
                 if (lo < w) continue;

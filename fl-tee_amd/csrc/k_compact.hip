@@ -39,7 +39,7 @@ namespace fltee {
 #endif
 // an unselected slot in flight: c = 2^31 (bit j clear at every level j <= 28, so it never
 // moves; form 1's u32::MAX carried the same meaning through its top-bit test), +0.0
-constexpr uint64_t CP_DUMMY = FLTEE_CP_PICK == 3 ? 0x80000000ull : 0xFFFFFFFFull;
+constexpr uint64_t CP_DUMMY = FLTEE_CP_PICK >= 3 ? 0x80000000ull : 0xFFFFFFFFull;
 constexpr uint64_t CP_PAD = 0xFFFFFFFFull;  // a pad record (idx u32::MAX, +0.0) outside the array
 
 // In flight the key is not idx but c = p0 - idx, the record's total left shift
@@ -57,6 +57,21 @@ constexpr uint64_t CP_PAD = 0xFFFFFFFFull;  // a pad record (idx u32::MAX, +0.0)
 // select).  All three move the same records: bit-identical outputs.
 __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint32_t j) {
     const uint32_t cs = (uint32_t)self, cr = (uint32_t)right;
+    if constexpr (FLTEE_CP_PICK == 4) {
+        // form 4: a dummy's val is left as it was (the final pass writes +0.0 for any dummy
+        // it outputs, cp_out), so the staying val needs no select: five VALU per pick
+        uint32_t lo, hi, e, em;
+        const uint32_t dmy = 0x80000000u;
+        asm("v_bfe_i32 %2, %4, %8, 1\n\t"        // e = ~0 iff self leaves
+            "v_bfe_i32 %3, %6, %8, 1\n\t"        // em = ~0 iff right moves in
+            "v_bfi_b32 %0, %2, %9, %4\n\t"       // stay c: the dummy's when self leaves
+            "v_bfi_b32 %0, %3, %6, %0\n\t"       // right's c if it moves in
+            "v_bfi_b32 %1, %3, %7, %5"             // right's val if it moves in, else self's
+            : "=&v"(lo), "=&v"(hi), "=&v"(e), "=&v"(em)
+            : "v"(cs), "v"((uint32_t)(self >> 32)), "v"(cr), "v"((uint32_t)(right >> 32)), "s"(j),
+              "s"(dmy));
+        return ((uint64_t)hi << 32) | lo;
+    }
     if constexpr (FLTEE_CP_PICK == 3) {
         uint32_t lo, hi, e, em;
         const uint32_t dmy = 0x80000000u;
@@ -82,6 +97,13 @@ __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint3
     const bool mv = ((cr >> j) & ~(cr >> 31)) & 1u;
     const bool st = !((cs >> j) & 1u);
     return mv ? right : (st ? self : CP_DUMMY);
+}
+
+// the value a final pass outputs for slot record r: +0.0 for a dummy (form 4 leaves a
+// dummy's val as it was; a position-sharded range outputs +0.0 where it holds no index)
+__device__ __forceinline__ float cp_out(uint64_t r) {
+    if constexpr (FLTEE_CP_PICK == 4) return ((uint32_t)r >> 31) ? 0.0f : rec_val(r);
+    return rec_val(r);
 }
 
 typedef unsigned int cp_u32x2 __attribute__((ext_vector_type(2)));
@@ -128,6 +150,11 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         return V2 ? 2u * (tid() + (i >> 1) * NT) + (i & 1u) : tid() + i * NT;
     };
     uint64_t pf[PER];
+    // the tile's rows in use: S + H (a pass over the output prefix only may use fewer than CAP
+    // slots); the other slots, and positions past L, load out of the buffer's range — no
+    // memory access, the dummy is selected when the tile lands
+    const uint32_t used = (S + H) << logW;
+    const uint32_t oob = L * 8u;
     // the loads only: the dummy for slots past L is selected when the tile lands (a use of
     // the loaded value here would make the compiler wait for the prefetch right away)
     auto prefetch = [&](uint32_t tl) {
@@ -136,7 +163,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             for (uint32_t i = 0; i < PER; i += 2) {
                 const uint64_t p = pos_of(tl, slot(i));  // even (W even), and p + 1 < L with p
                 const cp_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(
-                    rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
+                    rs, (int)(p < L && slot(i) < used ? (uint32_t)p * 8u : oob), 0, 0);
                 pf[i] = ((uint64_t)x.y << 32) | x.x;
                 pf[i + 1] = ((uint64_t)x.w << 32) | x.z;
             }
@@ -145,7 +172,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             for (uint32_t i = 0; i < PER; ++i) {
                 const uint64_t p = pos_of(tl, tid() + i * NT);
                 const cp_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(
-                    rs, (int)(p < L ? (uint32_t)p * 8u : 0u), 0, 0);
+                    rs, (int)(p < L && tid() + i * NT < used ? (uint32_t)p * 8u : oob), 0, 0);
                 pf[i] = ((uint64_t)x.y << 32) | x.x;
             }
         }
@@ -230,7 +257,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
                 if (FINAL == 0) {
                     if (p < L) dst[p] = sm[f];
                 } else if (p < d) {
-                    const float v = rec_val(sm[f]);
+                    const float v = cp_out(sm[f]);
                     out[p] = FINAL == 2 ? __fadd_rn(out[p], v) : __fmul_rn(v, coef);
                 }
             }
@@ -265,6 +292,10 @@ void set_compact_variant(int v) { g_compact_variant = v; }
 
 #ifndef FLTEE_COMPACT_V2
 #define FLTEE_COMPACT_V2 1
+#endif
+// the last levels as one pass over the output prefix (compact_levels)
+#ifndef FLTEE_CP_TAIL_MERGE
+#define FLTEE_CP_TAIL_MERGE 0
 #endif
 template <int NT, int PER, int MINB = 1>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
@@ -311,11 +342,43 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const bool small = g_compact_variant == 1 || (g_compact_variant == 2 && j0 == 0);
         const uint32_t CAP = small ? 4096 : 8192;
         const uint32_t gmax = j0 == 0 ? (small ? 9 : 10) : (small ? 5 : 6);
-        const uint32_t G = min(gmax, nlev - j0), H = (1u << G) - 1;
+        uint32_t G = min(gmax, nlev - j0), H = (1u << G) - 1;
         const uint64_t rows64 = (L + ((uint64_t)1 << j0) - 1) >> j0;
         const uint32_t rows = (uint32_t)rows64;
         uint32_t logW, S;
-        if (j0 == 0) {
+        // The last levels in one pass over the output prefix (FLTEE_CP_TAIL_MERGE): the final
+        // pass writes out[p] for p < d only, i.e. rows < ceil(d / 2^j0) of each residue
+        // class, and a record reaches row r from rows < r + 2^G.  So one band of those rows +
+        // 2^G - 1 halo rows per residue group covers every level left (G up to 10) when it
+        // fits a tile: e.g. C5's levels 19-26 (2 passes: 1.7 GB read + 0.9 GB written) as
+        // one pass reading the array once.
+        bool tail = false;
+        uint32_t tcap = CAP;
+        if (FLTEE_CP_TAIL_MERGE && j0 > 0 && nlev - j0 > G && nlev - j0 <= 10) {
+            const uint32_t Gt = nlev - j0, Ht = (1u << Gt) - 1;
+            const uint64_t so = (d + ((uint64_t)1 << j0) - 1) >> j0;  // output rows
+            // the widest rows (<= 16 residues, <= 2^j0) that fit 4,096 slots, or 8,192 (1,024
+            // lanes) when that gives 128-B rows on a large array
+            auto widest = [&](uint32_t cap) {
+                uint32_t lw = 0;
+                while (lw < 4 && lw < j0 && ((so + Ht) << (lw + 1)) <= cap) ++lw;
+                return ((so + Ht) << lw) <= cap ? (int)lw : -1;
+            };
+            int lw = widest(4096);
+            if (lw >= 0 && lw < 4 && L > ((size_t)1 << 21) && widest(8192) >= 4) {
+                lw = widest(8192);
+                tcap = 8192;
+            }
+            if (lw >= 0 && so < rows) {
+                tail = true;
+                G = Gt;
+                H = Ht;
+                logW = (uint32_t)lw;
+                S = (uint32_t)so;
+            }
+        }
+        if (tail) {
+        } else if (j0 == 0) {
             logW = 0;
             S = CAP - H;
             if (converted) S &= ~1u;  // even: 16-B slot pairs
@@ -330,7 +393,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
             if (logW > j0) logW = j0;
         }
         const uint32_t ngroups = (uint32_t)(((uint64_t)1 << j0) >> logW);
-        const uint64_t bands = (rows + S - 1) / S;
+        const uint64_t bands = tail ? 1 : (rows + S - 1) / S;  // tail: band 0 only
         uint64_t ntiles = bands * ngroups;
         if (ntiles == 0 || ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
         const bool last = (j0 + G == nlev);
@@ -344,14 +407,16 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
             const uint64_t g = (d + ((uint64_t)1 << logW) - 1) >> logW;
             if (g < live) live = g;
         }
-        net_account((uint64_t)(last ? 8 : 16) * L * live / ntiles, "compact_pass", s);
+        net_account(tail ? (uint64_t)8 * L + 4 * (uint64_t)d : (uint64_t)(last ? 8 : 16) * L * live / ntiles,
+                    "compact_pass", s);
         ntiles = live;
         // persistent grid = resident blocks: one 1024-lane block per CU (72-87 VGPRs), or two 512-lane ones
         const int blk = j0 == 0 ? kCompactFirstBlocks : kCompactBlocks;
-        const unsigned res = small ? 256u * (unsigned)blk : 256u;
+        const bool wide = tail ? tcap > 4096 : !small;
+        const unsigned res = !wide ? 256u * (unsigned)blk : 256u;
         const unsigned grid = (unsigned)(ntiles < res ? ntiles : res);
         const hipError_t e =
-            small ? (blk >= 4
+            !wide ? (blk >= 4
                          ? launch_pass<512, 8, 8>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
                                                   out, (uint32_t)ntiles)
@@ -493,8 +558,73 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             if (t + i * NT < Wn) win[t + i * NT] = pf[i];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
-        if constexpr (FLTEE_FC_FIXED_WALK == 2) {
+        // form 3 keeps its chunk in registers through the fold: the prefetch goes after it
+        constexpr bool kLatePf = FLTEE_FC_FIXED_WALK == 3;
+        if (FLTEE_FC_PF && !kLatePf) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        if constexpr (FLTEE_FC_FIXED_WALK == 3) {
+            // Form 3: form 2's sums without its lim-step walk.  Each lane owns window slots
+            // [x0, x0 + chunk) (in registers: values and "continues the run of the slot
+            // before" flags, read once) and folds them onto a carry — the sum of the run up
+            // to slot x0 - 1 — as acc = cont ? acc + v : v, the enclave's order.  The carry
+            // is the last sum of the lane before, exchanged through sums[] in rounds: after j
+            // rounds a lane's carry is exact when the run crossing into its chunk starts at
+            // most j lanes back, and a legal run (<= lim entries) starts at most
+            // ceil(lim / chunk) lanes back, so that many rounds (public) give every owned
+            // slot form 2's sum, bit for bit.  Per lane: (rounds + 1) x chunk selects and
+            // adds in registers instead of lim + chunk dependent LDS steps.
+            float *sums = reinterpret_cast<float *>(win + Wn);
+            constexpr uint32_t CH = PER + XMAX;  // >= chunk
+            const int x0 = (int)(t * chunk);
+            const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
+            auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
+            // the values are re-read from the window each round (LDS, independent of the
+            // chain): held in registers they push the PER = 6 kernels past 80 VGPRs
+            const float *wv = reinterpret_cast<const float *>(win) + 1;  // win[y]'s val: wv[2y]
+            auto val = [&](int y) { return wv[2 * min((uint32_t)max(y, 0), Wn - 1)]; };
+            bool cont[CH];
+            {
+                const int yb = x0 - 1;  // the slot before the chunk (y < 0: not a slot)
+                uint32_t prevk = (uint32_t)rd(yb);
+                bool have = (yb >= 0) & ((uint32_t)yb < Wn) & ((uint32_t)(pw + yb) < L);
+#pragma unroll
+                for (uint32_t i = 0; i < CH; ++i) {
+                    const int y = x0 + (int)i;
+                    const uint64_t r = rd(y);
+                    const uint32_t p = (uint32_t)(pw + y);  // a position < 0 wraps past L
+                    const bool valid = (i < chunk) & ((uint32_t)y < Wn) & (p < L);
+                    const uint32_t ky = (uint32_t)r;
+                    cont[i] = have & valid & (p != 0u) & (ky == prevk);
+                    prevk = ky;
+                    have = valid;
+                }
+            }
+            const uint32_t rounds = (lim + chunk - 1) / chunk;
+            const int ylast = x0 + (int)chunk - 1;
+            float carry = 0.0f;
+            for (uint32_t q = 0;; ++q) {
+                float acc = carry;
+                float vv[CH];
+#pragma unroll
+                for (uint32_t i = 0; i < CH; ++i) vv[i] = val(x0 + (int)i);
+                if (q == rounds) {
+#pragma unroll
+                    for (uint32_t i = 0; i < CH; ++i) {
+                        acc = cont[i] ? __fadd_rn(acc, vv[i]) : vv[i];
+                        const int y = x0 + (int)i;
+                        if (i < chunk && y < (int)Wn) sums[y] = acc;
+                    }
+                    break;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < CH; ++i)
+                    if (i < chunk) acc = cont[i] ? __fadd_rn(acc, vv[i]) : vv[i];
+                if (q) __syncthreads();  // the previous round's carry reads are done
+                if (ylast < (int)Wn) sums[ylast] = acc;
+                __syncthreads();
+                carry = x0 >= 1 && x0 - 1 < (int)Wn ? sums[x0 - 1] : 0.0f;
+            }
+            if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile compacts
+        } else if constexpr (FLTEE_FC_FIXED_WALK == 2) {
             // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
             // in-order sum of its run up to that slot: a walk from x0 - lim (every legal run
             // of an owned slot starts after it), lim + chunk steps whatever the data, no
@@ -627,7 +757,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             const uint32_t idx = (uint32_t)r;
             over |= f < S && p < (long long)L && p >= (long long)lim && (uint32_t)win[x - lim] == idx;
             const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-            const uint64_t hi = FLTEE_FC_FIXED_WALK == 2
+            const uint64_t hi = FLTEE_FC_FIXED_WALK >= 2
                                     ? (uint64_t)__float_as_uint(reinterpret_cast<const float *>(win + Wn)[x]) << 32
                                     : (r & 0xFFFFFFFF00000000ull);
             v[i] = (p < (long long)L && idx < d && end) ? (hi | (uint32_t)((uint32_t)p - idx)) : CP_DUMMY;
@@ -679,7 +809,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 if (FINAL == 0) {
                     if (p < (long long)L) dst[p] = sm[f];
                 } else if (p < (long long)d) {
-                    const float vv = rec_val(sm[f]);
+                    const float vv = cp_out(sm[f]);
                     out[p] = FINAL == 2 ? __fadd_rn(out[p], vv) : __fmul_rn(vv, coef);
                 }
             }
@@ -772,7 +902,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 256u * bpc ? ntiles : 256u * bpc);
     // the window, and (fixed walk, form 2) the run sums beside it
-    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK == 2 ? (Hr + CAP + 1) * 4 : 0);
+    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK >= 2 ? (Hr + CAP + 1) * 4 : 0);
     // the resident blocks per CU must fit the 160 KiB LDS at the largest window
     static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
     static_assert((1023 + 8 * 1024 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU (8,192 records)");
