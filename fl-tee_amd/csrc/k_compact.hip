@@ -32,10 +32,11 @@
 
 namespace fltee {
 
-// FLTEE_CP_PICK: 1 = compares + selects; 2 = the staying value as bit operations; 3
-// (default) = bit operations only, no compare (see cp_pick)
+// FLTEE_CP_PICK: 1 = compares + selects; 2 = the staying value as bit operations; 3 = bit
+// operations only, no compare; 4 (default, round 5) = form 3 with a dummy's val left as it
+// was (see cp_pick, cp_out)
 #ifndef FLTEE_CP_PICK
-#define FLTEE_CP_PICK 3
+#define FLTEE_CP_PICK 4
 #endif
 // an unselected slot in flight: c = 2^31 (bit j clear at every level j <= 28, so it never
 // moves; form 1's u32::MAX carried the same meaning through its top-bit test), +0.0
@@ -59,7 +60,9 @@ __device__ __forceinline__ uint64_t cp_pick(uint64_t self, uint64_t right, uint3
     const uint32_t cs = (uint32_t)self, cr = (uint32_t)right;
     if constexpr (FLTEE_CP_PICK == 4) {
         // form 4: a dummy's val is left as it was (the final pass writes +0.0 for any dummy
-        // it outputs, cp_out), so the staying val needs no select: five VALU per pick
+        // it outputs, cp_out), so the staying val needs no select: five VALU per pick.
+        // Round 5 A/B (`profiles/r05/ab/ab15_*`, bit-identical): compact_pass 431 -> 420 us
+        // at C5 (12.27 -> 12.23 ms), C3 0.1365 -> 0.1355 ms.
         uint32_t lo, hi, e, em;
         const uint32_t dmy = 0x80000000u;
         asm("v_bfe_i32 %2, %4, %8, 1\n\t"        // e = ~0 iff self leaves
@@ -293,9 +296,14 @@ void set_compact_variant(int v) { g_compact_variant = v; }
 #ifndef FLTEE_COMPACT_V2
 #define FLTEE_COMPACT_V2 1
 #endif
-// the last levels as one pass over the output prefix (compact_levels)
+// the last levels as one pass over the output prefix (compact_levels) on arrays of at most
+// 2^FLTEE_CP_TAIL_MERGE records (0: never).  Round 5 A/B (`profiles/r05/ab/ab15_*`,
+// bit-identical): C3 0.1365 -> 0.1319 ms, MLP-MNIST n = 30 advanced 0.088 -> 0.082 ms (a
+// launch less on arrays that stay in the caches); C5 12.27 -> 12.55 ms (the merged pass
+// computes 8 levels over 14x the slots it outputs, 1.07 ms against 0.75 for the two passes
+// it replaces), so large arrays keep the separate passes.
 #ifndef FLTEE_CP_TAIL_MERGE
-#define FLTEE_CP_TAIL_MERGE 0
+#define FLTEE_CP_TAIL_MERGE 21
 #endif
 template <int NT, int PER, int MINB = 1>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
@@ -350,11 +358,12 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         // pass writes out[p] for p < d only, i.e. rows < ceil(d / 2^j0) of each residue
         // class, and a record reaches row r from rows < r + 2^G.  So one band of those rows +
         // 2^G - 1 halo rows per residue group covers every level left (G up to 10) when it
-        // fits a tile: e.g. C5's levels 19-26 (2 passes: 1.7 GB read + 0.9 GB written) as
-        // one pass reading the array once.
+        // fits a tile: e.g. C3's levels 9-18 (after the fused fold's 0-8) as one pass of 256
+        // tiles, 100 output + 1,023 halo rows of 2 residues each, instead of two.
         bool tail = false;
         uint32_t tcap = CAP;
-        if (FLTEE_CP_TAIL_MERGE && j0 > 0 && nlev - j0 > G && nlev - j0 <= 10) {
+        if (FLTEE_CP_TAIL_MERGE && L <= ((size_t)1 << FLTEE_CP_TAIL_MERGE) && j0 > 0 && nlev - j0 > G &&
+            nlev - j0 <= 10) {
             const uint32_t Gt = nlev - j0, Ht = (1u << Gt) - 1;
             const uint64_t so = (d + ((uint64_t)1 << j0) - 1) >> j0;  // output rows
             // the widest rows (<= 16 residues, <= 2^j0) that fit 4,096 slots, or 8,192 (1,024
@@ -365,7 +374,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
                 return ((so + Ht) << lw) <= cap ? (int)lw : -1;
             };
             int lw = widest(4096);
-            if (lw >= 0 && lw < 4 && L > ((size_t)1 << 21) && widest(8192) >= 4) {
+            if (lw >= 0 && lw < 4 && L > ((size_t)1 << 21) && widest(8192) >= 4) {  // (large arrays)
                 lw = widest(8192);
                 tcap = 8192;
             }
@@ -499,6 +508,10 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_FIXED_WALK
 #define FLTEE_FC_FIXED_WALK 2
 #endif
+// (Round 5, measured and not kept: the walk's dependent chain as rounds of carries between
+// lanes — each lane folds its own slots onto the last sum of the lane before, ceil(lim /
+// chunk) rounds through LDS — C3 0.136-0.139 vs 0.136 ms, bit-identical,
+// `profiles/r05/ab/ab15_*`.)
 // The fixed walk's bound: lim <= 128 at any size, <= 320 on arrays of <= 2^20 records,
 // where the streaming fold's launch and latency cost more than the longer walk (MLP-MNIST
 // n = 300, lim 301: 0.101 vs 0.138 ms, `profiles/r05/ab/ab12_*`); 320 keeps three windows
@@ -558,73 +571,8 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             if (t + i * NT < Wn) win[t + i * NT] = pf[i];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        // form 3 keeps its chunk in registers through the fold: the prefetch goes after it
-        constexpr bool kLatePf = FLTEE_FC_FIXED_WALK == 3;
-        if (FLTEE_FC_PF && !kLatePf) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
-        if constexpr (FLTEE_FC_FIXED_WALK == 3) {
-            // Form 3: form 2's sums without its lim-step walk.  Each lane owns window slots
-            // [x0, x0 + chunk) (in registers: values and "continues the run of the slot
-            // before" flags, read once) and folds them onto a carry — the sum of the run up
-            // to slot x0 - 1 — as acc = cont ? acc + v : v, the enclave's order.  The carry
-            // is the last sum of the lane before, exchanged through sums[] in rounds: after j
-            // rounds a lane's carry is exact when the run crossing into its chunk starts at
-            // most j lanes back, and a legal run (<= lim entries) starts at most
-            // ceil(lim / chunk) lanes back, so that many rounds (public) give every owned
-            // slot form 2's sum, bit for bit.  Per lane: (rounds + 1) x chunk selects and
-            // adds in registers instead of lim + chunk dependent LDS steps.
-            float *sums = reinterpret_cast<float *>(win + Wn);
-            constexpr uint32_t CH = PER + XMAX;  // >= chunk
-            const int x0 = (int)(t * chunk);
-            const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
-            auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
-            // the values are re-read from the window each round (LDS, independent of the
-            // chain): held in registers they push the PER = 6 kernels past 80 VGPRs
-            const float *wv = reinterpret_cast<const float *>(win) + 1;  // win[y]'s val: wv[2y]
-            auto val = [&](int y) { return wv[2 * min((uint32_t)max(y, 0), Wn - 1)]; };
-            bool cont[CH];
-            {
-                const int yb = x0 - 1;  // the slot before the chunk (y < 0: not a slot)
-                uint32_t prevk = (uint32_t)rd(yb);
-                bool have = (yb >= 0) & ((uint32_t)yb < Wn) & ((uint32_t)(pw + yb) < L);
-#pragma unroll
-                for (uint32_t i = 0; i < CH; ++i) {
-                    const int y = x0 + (int)i;
-                    const uint64_t r = rd(y);
-                    const uint32_t p = (uint32_t)(pw + y);  // a position < 0 wraps past L
-                    const bool valid = (i < chunk) & ((uint32_t)y < Wn) & (p < L);
-                    const uint32_t ky = (uint32_t)r;
-                    cont[i] = have & valid & (p != 0u) & (ky == prevk);
-                    prevk = ky;
-                    have = valid;
-                }
-            }
-            const uint32_t rounds = (lim + chunk - 1) / chunk;
-            const int ylast = x0 + (int)chunk - 1;
-            float carry = 0.0f;
-            for (uint32_t q = 0;; ++q) {
-                float acc = carry;
-                float vv[CH];
-#pragma unroll
-                for (uint32_t i = 0; i < CH; ++i) vv[i] = val(x0 + (int)i);
-                if (q == rounds) {
-#pragma unroll
-                    for (uint32_t i = 0; i < CH; ++i) {
-                        acc = cont[i] ? __fadd_rn(acc, vv[i]) : vv[i];
-                        const int y = x0 + (int)i;
-                        if (i < chunk && y < (int)Wn) sums[y] = acc;
-                    }
-                    break;
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < CH; ++i)
-                    if (i < chunk) acc = cont[i] ? __fadd_rn(acc, vv[i]) : vv[i];
-                if (q) __syncthreads();  // the previous round's carry reads are done
-                if (ylast < (int)Wn) sums[ylast] = acc;
-                __syncthreads();
-                carry = x0 >= 1 && x0 - 1 < (int)Wn ? sums[x0 - 1] : 0.0f;
-            }
-            if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile compacts
-        } else if constexpr (FLTEE_FC_FIXED_WALK == 2) {
+        if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        if constexpr (FLTEE_FC_FIXED_WALK == 2) {
             // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
             // in-order sum of its run up to that slot: a walk from x0 - lim (every legal run
             // of an owned slot starts after it), lim + chunk steps whatever the data, no
@@ -757,7 +705,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             const uint32_t idx = (uint32_t)r;
             over |= f < S && p < (long long)L && p >= (long long)lim && (uint32_t)win[x - lim] == idx;
             const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-            const uint64_t hi = FLTEE_FC_FIXED_WALK >= 2
+            const uint64_t hi = FLTEE_FC_FIXED_WALK == 2
                                     ? (uint64_t)__float_as_uint(reinterpret_cast<const float *>(win + Wn)[x]) << 32
                                     : (r & 0xFFFFFFFF00000000ull);
             v[i] = (p < (long long)L && idx < d && end) ? (hi | (uint32_t)((uint32_t)p - idx)) : CP_DUMMY;
@@ -902,7 +850,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const bool last = G == nlev;
     const unsigned grid = (unsigned)(ntiles < 256u * bpc ? ntiles : 256u * bpc);
     // the window, and (fixed walk, form 2) the run sums beside it
-    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK >= 2 ? (Hr + CAP + 1) * 4 : 0);
+    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK == 2 ? (Hr + CAP + 1) * 4 : 0);
     // the resident blocks per CU must fit the 160 KiB LDS at the largest window
     static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
     static_assert((1023 + 8 * 1024 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU (8,192 records)");
