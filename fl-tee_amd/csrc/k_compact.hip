@@ -35,6 +35,13 @@ namespace fltee {
 // FLTEE_CP_PICK: 1 = compares + selects; 2 = the staying value as bit operations; 3 = bit
 // operations only, no compare; 4 (default, round 5) = form 3 with a dummy's val left as it
 // was (see cp_pick, cp_out)
+// FLTEE_CP_TWO: two levels per LDS round (3 picks, 4 reads and 1 write per slot) or one
+// (1 pick, 2 reads, 1 write and one more barrier per level).  Round 5 A/B, bit-identical:
+// one level per round is slower though it issues a third fewer picks — C5 12.22 -> 12.26
+// ms, C3 0.1317 -> 0.1350 ms (`profiles/r05/ab/ab16_compact_one_level_rounds_rejected.jsonl`)
+#ifndef FLTEE_CP_TWO
+#define FLTEE_CP_TWO 1
+#endif
 #ifndef FLTEE_CP_PICK
 #define FLTEE_CP_PICK 4
 #endif
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         for (uint32_t g = 0; g < G;) {
             const uint32_t stepf = W << g;
             const uint32_t j = j0 + g;
-            const bool two = g + 1 < G;
+            const bool two = FLTEE_CP_TWO && g + 1 < G;
             const uint32_t gl = two ? g + 1 : g;
             const uint32_t lim = (S + H - ((2u << gl) - 1)) << logW;
             if (two) {
@@ -720,7 +727,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         uint64_t nv[PER];
         for (uint32_t g = 0; g < G;) {
             const uint32_t stepf = 1u << g;
-            const bool two = g + 1 < G;
+            const bool two = FLTEE_CP_TWO && g + 1 < G;
             const uint32_t gl = two ? g + 1 : g;
             const uint32_t lim = S + H - ((2u << gl) - 1);
             if (two) {
