@@ -408,6 +408,25 @@ def test_advanced_compaction_equals_second_sort(dev, oracle, n, d, k):
         assert st == 0 and bits_equal(a, ref)
 
 
+# the compaction's last levels as one pass over the output prefix (arrays <= 2^21
+# records, k_compact.hip compact_levels): remaining levels 6-10 after the first pass, output
+# rows of 1..196 per residue class, rows of 2..16 residues, d below one row (the live-group
+# trim), and the streaming fold's converted first pass (n + 1 > 320) in front of it
+@pytest.mark.parametrize("n,d,k", [(16, 777, 1500), (64, 100_000, 4000), (3, 5, 70_000),
+                                   (400, 5000, 1000), (31, 50_890, 8191)])
+def test_advanced_output_prefix_tail_pass(dev, oracle, n, d, k):
+    rng = np.random.default_rng(n * 7 + k)
+    idx = np.concatenate([np.sort(rng.choice(d, min(k, d), replace=False))
+                          if k <= d else rng.integers(0, d, k) for _ in range(n)]).astype(np.uint32)
+    val = rng.normal(0, 0.01, n * k).astype(np.float32)
+    rec = cuda_records(dev, idx, val)
+    # (k > d repeats indices inside a client: runs beyond n + 1, the exact halo)
+    out = dev.aggregate(1, rec, n, k, d, fold_halo=n * k + d if k > d else 0).cpu().numpy()
+    assert dev.status() == 0
+    ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
+    assert st == 0 and bits_equal(out, ref)
+
+
 def test_advanced_compaction_out_of_range_and_repeated_indices(dev, oracle):
     # indices >= d fold into their own runs and never reach [0, d); a client's
     # repeated index makes runs longer than n+1 (halo re-run by the ECALL layer,
