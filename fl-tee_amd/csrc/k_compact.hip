@@ -42,6 +42,14 @@ namespace fltee {
 #ifndef FLTEE_CP_TWO
 #define FLTEE_CP_TWO 1
 #endif
+// FLTEE_CP_CT: the compaction passes of the common tile shapes (C5's first and middle passes,
+// the fused kernel's nine levels) with their levels at compile time (cp_levels_ct).  Round 5
+// A/B, bit-identical (`profiles/r05/ab/ab17_*`): C5 12.25 -> 12.15 ms (compact_pass 423 ->
+// 403 us on average); the fused kernel 12.3 -> 11.7 us at MLP-MNIST n = 30, 10.2 -> 9.5 us
+// at n = 3, 19.8 -> 19.7 us at C3.
+#ifndef FLTEE_CP_CT
+#define FLTEE_CP_CT 1
+#endif
 #ifndef FLTEE_CP_PICK
 #define FLTEE_CP_PICK 4
 #endif
@@ -119,6 +127,46 @@ __device__ __forceinline__ float cp_out(uint64_t r) {
 typedef unsigned int cp_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int cp_u32x4 __attribute__((ext_vector_type(4)));
 
+// The levels of one tile with its shape known at compile time (FLTEE_CP_CT): G levels on rows
+// of 2^LW residues, SH = S + H rows in the tile.  The level loop unrolls, so every LDS slot
+// of a round is an immediate offset off one per-lane address, and the range test (f < lim)
+// is decided at compile time for every slot but those of the last rows: only the picks'
+// five VALU per slot remain (the runtime loop adds ~8 address / range VALU per slot and
+// round, `make asm`).  The same levels and picks: bit-identical.
+template <int NT, int PER, int G, int LW, int SH, int G0 = 0>
+__device__ __forceinline__ void cp_levels_ct(uint64_t *sm, uint32_t j0, uint32_t t) {
+    if constexpr (G0 < G) {
+        constexpr bool two = FLTEE_CP_TWO && G0 + 1 < G;
+        constexpr uint32_t stepf = (1u << LW) << G0;
+        constexpr uint32_t gl = two ? G0 + 1 : G0;
+        constexpr uint32_t lim = ((uint32_t)SH - ((2u << gl) - 1)) << LW;
+        const uint32_t j = j0 + (uint32_t)G0;
+        uint64_t *const base = sm + t;
+        uint64_t nv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const uint32_t o = (uint32_t)i * NT;
+            if (o + NT <= lim || t + o < lim) {  // the first test is decided at compile time
+                if constexpr (two) {
+                    const uint64_t y0 = cp_pick(base[o], base[o + stepf], j);
+                    const uint64_t y2 = cp_pick(base[o + 2 * stepf], base[o + 3 * stepf], j);
+                    nv[i] = cp_pick(y0, y2, j + 1);
+                } else {
+                    nv[i] = cp_pick(base[o], base[o + stepf], j);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const uint32_t o = (uint32_t)i * NT;
+            if (o + NT <= lim || t + o < lim) base[o] = nv[i];
+        }
+        __syncthreads();
+        cp_levels_ct<NT, PER, G, LW, SH, G0 + (two ? 2 : 1)>(sm, j0, t);
+    }
+}
+
 // FIRST: src holds folded records (idx, val); else (c, val).
 // FINAL: 0 = write (c, val) records, 1 = out[i] = val*coef, 2 = out[i] += val.
 // Persistent: block b walks tiles b, b + grid, ...; the next tile's records are
@@ -127,7 +175,8 @@ typedef unsigned int cp_u32x4 __attribute__((ext_vector_type(4)));
 // V2 (rows of W >= 2 residues, L even): a lane loads and stores two adjacent slots of a
 // row (16 B; 8-B accesses run at about half the 16-B rate, MI355X_MICROARCH.md); the
 // levels keep the one-slot-per-lane assignment.
-template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1, bool V2 = false>
+template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1, bool V2 = false, int CG = 0, int CLW = 0,
+          int CSH = 0>
 __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restrict__ src,
                                                    uint64_t *__restrict__ dst, uint32_t L,
                                                    uint32_t d, uint32_t j0, uint32_t G,
@@ -205,6 +254,11 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         // pick_g(x[f+2s], x[f+3s])) — 4 reads + 1 write per record per two levels
         // instead of 2 + 1 per level (ds_write_b64 costs ~3x a ds_read_b64), half the
         // barriers.  After level g the rows still needed are S + H - (2^(g+1) - 1).
+        // CG: the tile shape at compile time (launch_pass checked G == CG, logW == CLW and
+        // S + H == CSH)
+        if constexpr (CG != 0) {
+            cp_levels_ct<NT, PER, CG, CLW, CSH>(sm, j0, tid());
+        } else {
         uint64_t nv[PER];
         for (uint32_t g = 0; g < G;) {
             const uint32_t stepf = W << g;
@@ -237,6 +291,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             }
             __syncthreads();
             g += two ? 2 : 1;
+        }
         }
         const uint32_t nout = S << logW;
         if constexpr (V2 && FINAL == 0) {
@@ -320,10 +375,23 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
 #define CP_GO(F, X, V)                                                                           \
     hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
                        d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
+#define CP_GO_CT(V, G_, LW_, SH_)                                                                \
+    hipLaunchKernelGGL((compact_pass<NT, PER, false, 0, MINB, V, G_, LW_, SH_>), dim3(grid), dim3(NT), 0, s, \
+                       src, dst, L, d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
     // 16-B slot pairs: rows of >= 2 residues (or a contiguous tile of an even S: the
     // converted first pass), L even, both buffers 16-B aligned
     const bool v2 = FLTEE_COMPACT_V2 && !first && (logW >= 1 || S % 2 == 0) && L % 2 == 0 &&
                     (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0;
+    // the tile shapes of C5's passes with compile-time levels (FLTEE_CP_CT): the converted
+    // first pass (9 levels, contiguous, S + H = 4,095) and the strided middle ones (5 levels
+    // on rows of 16, one 256-row band)
+    const uint32_t sh = S + (1u << G) - 1;
+    if constexpr (FLTEE_CP_CT && NT * PER == 4096) {
+        if (!first && v2 && fin == 0) {
+            if (G == 9 && logW == 0 && sh == 4095) { CP_GO_CT(true, 9, 0, 4095); return hipGetLastError(); }
+            if (G == 5 && logW == 4 && sh == 256) { CP_GO_CT(true, 5, 4, 256); return hipGetLastError(); }
+        }
+    }
     if (first) {
         if (fin == 0) CP_GO(true, 0, false); else if (fin == 1) CP_GO(true, 1, false); else CP_GO(true, 2, false);
     } else if (v2) {
@@ -332,6 +400,7 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
         if (fin == 0) CP_GO(false, 0, false); else if (fin == 1) CP_GO(false, 1, false); else CP_GO(false, 2, false);
     }
 #undef CP_GO
+#undef CP_GO_CT
     return hipGetLastError();
 }
 
@@ -723,9 +792,17 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) sm[t + i * NT] = v[i];
         __syncthreads();
-        // the first G levels, exactly compact_pass's (contiguous: W = 1, j0 = 0)
+        // the first G levels, exactly compact_pass's (contiguous: W = 1, j0 = 0); all nine at
+        // compile time when the array has that many (FLTEE_CP_CT, cp_levels_ct)
+        bool lv_done = false;
+        if constexpr (FLTEE_CP_CT) {
+            if (G == 9 && S + H == CAP) {
+                cp_levels_ct<NT, PER, 9, 0, (int)CAP>(sm, 0u, t);
+                lv_done = true;
+            }
+        }
         uint64_t nv[PER];
-        for (uint32_t g = 0; g < G;) {
+        for (uint32_t g = 0; g < (lv_done ? 0u : G);) {
             const uint32_t stepf = 1u << g;
             const bool two = FLTEE_CP_TWO && g + 1 < G;
             const uint32_t gl = two ? g + 1 : g;
