@@ -42,6 +42,13 @@ namespace fltee {
 #ifndef FLTEE_CP_TWO
 #define FLTEE_CP_TWO 1
 #endif
+// FLTEE_CP_NOHALO: a residue group's only band loads and keeps no halo rows (they lie past
+// L), so its rows may be twice as wide (compact_pass NH).  Round 5 A/B, bit-identical
+// (`profiles/r05/ab/ab18_*`): C5's last two passes (one band each) ~65 us faster, C5 12.11
+// -> 12.06 ms; C3 unchanged (its last pass is the output-prefix tail).
+#ifndef FLTEE_CP_NOHALO
+#define FLTEE_CP_NOHALO 1
+#endif
 // FLTEE_CP_CT: the compaction passes of the common tile shapes (C5's first and middle passes,
 // the fused kernel's nine levels) with their levels at compile time (cp_levels_ct).  Round 5
 // A/B, bit-identical (`profiles/r05/ab/ab17_*`): C5 12.25 -> 12.15 ms (compact_pass 423 ->
@@ -175,8 +182,11 @@ __device__ __forceinline__ void cp_levels_ct(uint64_t *sm, uint32_t j0, uint32_t
 // V2 (rows of W >= 2 residues, L even): a lane loads and stores two adjacent slots of a
 // row (16 B; 8-B accesses run at about half the 16-B rate, MI355X_MICROARCH.md); the
 // levels keep the one-slot-per-lane assignment.
+// NH (no halo): the tile is its residue group's only band (S = every row), so the rows a
+// halo would hold lie past L — dummies that never move: they are neither loaded nor kept in
+// LDS, a level reading one gets the dummy (compact_levels; FLTEE_CP_NOHALO).
 template <int NT, int PER, bool FIRST, int FINAL, int MINB = 1, bool V2 = false, int CG = 0, int CLW = 0,
-          int CSH = 0>
+          int CSH = 0, bool NH = false>
 __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restrict__ src,
                                                    uint64_t *__restrict__ dst, uint32_t L,
                                                    uint32_t d, uint32_t j0, uint32_t G,
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
     // the tile's rows in use: S + H (a pass over the output prefix only may use fewer than CAP
     // slots); the other slots, and positions past L, load out of the buffer's range — no
     // memory access, the dummy is selected when the tile lands
-    const uint32_t used = (S + H) << logW;
+    const uint32_t used = (NH ? S : S + H) << logW;
     const uint32_t oob = L * 8u;
     // the loads only: the dummy for slots past L is selected when the tile lands (a use of
     // the loaded value here would make the compiler wait for the prefetch right away)
@@ -260,19 +270,22 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
             cp_levels_ct<NT, PER, CG, CLW, CSH>(sm, j0, tid());
         } else {
         uint64_t nv[PER];
+        // NH: slots at or past `used` are rows past L (dummies); only rows < S are kept
+        auto rdl = [&](uint32_t x) -> uint64_t { return (!NH || x < used) ? sm[x] : CP_DUMMY; };
         for (uint32_t g = 0; g < G;) {
             const uint32_t stepf = W << g;
             const uint32_t j = j0 + g;
             const bool two = FLTEE_CP_TWO && g + 1 < G;
             const uint32_t gl = two ? g + 1 : g;
-            const uint32_t lim = (S + H - ((2u << gl) - 1)) << logW;
+            const uint32_t lim0 = (S + H - ((2u << gl) - 1)) << logW;
+            const uint32_t lim = NH && used < lim0 ? used : lim0;
             if (two) {
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
                     const uint32_t f = tid() + i * NT;
                     if (f < lim) {
-                        const uint64_t y0 = cp_pick(sm[f], sm[f + stepf], j);
-                        const uint64_t y2 = cp_pick(sm[f + 2 * stepf], sm[f + 3 * stepf], j);
+                        const uint64_t y0 = cp_pick(rdl(f), rdl(f + stepf), j);
+                        const uint64_t y2 = cp_pick(rdl(f + 2 * stepf), rdl(f + 3 * stepf), j);
                         nv[i] = cp_pick(y0, y2, j + 1);
                     }
                 }
@@ -280,7 +293,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
                     const uint32_t f = tid() + i * NT;
-                    if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], j);
+                    if (f < lim) nv[i] = cp_pick(rdl(f), rdl(f + stepf), j);
                 }
             }
             __syncthreads();
@@ -371,7 +384,7 @@ template <int NT, int PER, int MINB = 1>
 static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s, const uint64_t *src,
                               uint64_t *dst, uint32_t L, uint32_t d, uint32_t j0, uint32_t G,
                               uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
-                              float coef, float *out, uint32_t ntiles) {
+                              float coef, float *out, uint32_t ntiles, bool nh = false) {
 #define CP_GO(F, X, V)                                                                           \
     hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
                        d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
@@ -392,6 +405,18 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
             if (G == 5 && logW == 4 && sh == 256) { CP_GO_CT(true, 5, 4, 256); return hipGetLastError(); }
         }
     }
+#define CP_GO_NH(X, V)                                                                           \
+    hipLaunchKernelGGL((compact_pass<NT, PER, false, X, MINB, V, 0, 0, 0, true>), dim3(grid), dim3(NT), 0, s, \
+                       src, dst, L, d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
+    if (FLTEE_CP_NOHALO && nh && !first) {  // one band: no halo rows (compact_pass NH)
+        if (v2) {
+            if (fin == 0) CP_GO_NH(0, true); else if (fin == 1) CP_GO_NH(1, true); else CP_GO_NH(2, true);
+        } else {
+            if (fin == 0) CP_GO_NH(0, false); else if (fin == 1) CP_GO_NH(1, false); else CP_GO_NH(2, false);
+        }
+        return hipGetLastError();
+    }
+#undef CP_GO_NH
     if (first) {
         if (fin == 0) CP_GO(true, 0, false); else if (fin == 1) CP_GO(true, 1, false); else CP_GO(true, 2, false);
     } else if (v2) {
@@ -430,6 +455,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
         const uint64_t rows64 = (L + ((uint64_t)1 << j0) - 1) >> j0;
         const uint32_t rows = (uint32_t)rows64;
         uint32_t logW, S;
+        bool nohalo = false;
         // The last levels in one pass over the output prefix (FLTEE_CP_TAIL_MERGE): the final
         // pass writes out[p] for p < d only, i.e. rows < ceil(d / 2^j0) of each residue
         // class, and a record reaches row r from rows < r + 2^G.  So one band of those rows +
@@ -469,9 +495,13 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
             if (converted) S &= ~1u;  // even: 16-B slot pairs
         } else {
             logW = 4;  // 16 residues = 128-B row segments
-            if (rows + H <= CAP >> logW) {  // one band: widen the rows instead
-                S = rows;                        // (halo rows past L are dummies in LDS)
-                while (logW < j0 && ((rows + H) << (logW + 1)) <= CAP) ++logW;
+            // one band: widen the rows instead.  Its halo rows lie past L (dummies): with
+            // FLTEE_CP_NOHALO the tile holds the band's rows only
+            const uint32_t hh = FLTEE_CP_NOHALO && kCompactBlocks >= 4 ? 0u : H;
+            if (rows + hh <= CAP >> logW) {
+                S = rows;
+                nohalo = hh == 0;
+                while (logW < j0 && ((rows + hh) << (logW + 1)) <= CAP) ++logW;
             } else {
                 S = (CAP >> logW) - H;
             }
@@ -504,7 +534,7 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
             !wide ? (blk >= 4
                          ? launch_pass<512, 8, 8>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
-                                                  out, (uint32_t)ntiles)
+                                                  out, (uint32_t)ntiles, nohalo)
                      : blk == 3
                          ? launch_pass<512, 8, 6>(j0 == 0 && !converted, fin, grid, s, cur, oth, (uint32_t)L,
                                                   (uint32_t)d, j0, G, logW, S, rows, ngroups, coef,
