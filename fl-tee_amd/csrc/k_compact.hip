@@ -49,6 +49,14 @@ namespace fltee {
 #ifndef FLTEE_CP_NOHALO
 #define FLTEE_CP_NOHALO 1
 #endif
+// FLTEE_CP_PAD_BAND: a one-band pass on rows of 16 padded to the full tile (compact_levels).
+// Round 5 A/B, bit-identical (`profiles/r05/ab/ab19_*`): C5 12.03 -> 12.00 ms (its levels
+// 19-23 on the compile-time levels); dropping that band's halo instead (compact_pass NH)
+// was slower there (488 vs 459 us: a select per level read in a VALU-bound pass), so NH is
+// kept for the bands whose rows it widens (C5's last pass: 293 -> 197 us).
+#ifndef FLTEE_CP_PAD_BAND
+#define FLTEE_CP_PAD_BAND 1
+#endif
 // FLTEE_CP_CT: the compaction passes of the common tile shapes (C5's first and middle passes,
 // the fused kernel's nine levels) with their levels at compile time (cp_levels_ct).  Round 5
 // A/B, bit-identical (`profiles/r05/ab/ab17_*`): C5 12.25 -> 12.15 ms (compact_pass 423 ->
@@ -495,13 +503,25 @@ static hipError_t compact_levels(uint64_t *src, uint64_t *tmp, size_t L, size_t 
             if (converted) S &= ~1u;  // even: 16-B slot pairs
         } else {
             logW = 4;  // 16 residues = 128-B row segments
-            // one band: widen the rows instead.  Its halo rows lie past L (dummies): with
-            // FLTEE_CP_NOHALO the tile holds the band's rows only
-            const uint32_t hh = FLTEE_CP_NOHALO && kCompactBlocks >= 4 ? 0u : H;
-            if (rows + hh <= CAP >> logW) {
-                S = rows;
-                nohalo = hh == 0;
-                while (logW < j0 && ((rows + hh) << (logW + 1)) <= CAP) ++logW;
+            // One band: widen the rows instead.  Its halo rows lie past L (dummies).  With
+            // FLTEE_CP_NOHALO the tile drops them (compact_pass NH: a select per level read)
+            // where that widens the rows; else they stay (they load nothing), and a band of
+            // 16-residue rows is padded to the full 256-row tile — rows past L again — so
+            // the compile-time levels run it (FLTEE_CP_CT; C5's levels 19-23: 488 -> ~400 us).
+            const bool nh_ok = FLTEE_CP_NOHALO && kCompactBlocks >= 4;
+            const bool fits = rows + H <= CAP >> logW;
+            if (fits || (nh_ok && rows <= CAP >> logW)) {
+                uint32_t lw = logW, lwn = logW;
+                while (lw < j0 && ((rows + H) << (lw + 1)) <= CAP) ++lw;
+                while (lwn < j0 && (rows << (lwn + 1)) <= CAP) ++lwn;
+                if (nh_ok && (!fits || lwn > lw)) {
+                    logW = lwn;
+                    S = rows;
+                    nohalo = true;
+                } else {
+                    logW = lw;
+                    S = lw == 4 && FLTEE_CP_CT && FLTEE_CP_PAD_BAND ? (CAP >> 4) - H : rows;
+                }
             } else {
                 S = (CAP >> logW) - H;
             }
