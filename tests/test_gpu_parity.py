@@ -394,9 +394,12 @@ def _advanced_both_ways(dev, rec, n, k, d):
     return a, b
 
 
-# (n, d, k): compaction levels log2(L - d) = 3 / 14 / 19 / 23 -> 1 / 2 / 3 / 4 passes
+# (n, d, k): compaction levels log2(L - d) = 3 / 14 / 19 / 23 -> 1 / 2 / 3 / 4 passes; the
+# last two: a one-band pass padded to the full tile (levels 14-18 of 3.05M records) before a
+# final pass without halo rows, and exp5's MLP-MNIST n = 3000 (a final pass without halo)
 @pytest.mark.parametrize("n,d,k", [(2, 1_000_000, 3), (1000, 16, 16), (100, 50890, 5089),
-                                   (300, 2_000_000, 20_000)])
+                                   (300, 2_000_000, 20_000), (300, 50890, 10_000),
+                                   (3000, 50890, 5089)])
 def test_advanced_compaction_equals_second_sort(dev, oracle, n, d, k):
     rng = np.random.default_rng(n + d + k)
     idx, val = rand_sparse(rng, n, d, k)
