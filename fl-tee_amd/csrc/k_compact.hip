@@ -49,6 +49,12 @@ namespace fltee {
 #ifndef FLTEE_CP_NOHALO
 #define FLTEE_CP_NOHALO 1
 #endif
+// FLTEE_CP_SKIP_SELF: a block on its last tile prefetches nothing (else it re-reads its own
+// tile, a load with no branch around it).  Round 5 A/B, bit-identical (`ab20_*`): C3 0.1315
+// -> 0.1297 ms (its tail pass, one tile per block, 16.6 -> 14.5 us), C5 unchanged.
+#ifndef FLTEE_CP_SKIP_SELF
+#define FLTEE_CP_SKIP_SELF 1
+#endif
 // FLTEE_CP_PAD_BAND: a one-band pass on rows of 16 padded to the full tile (compact_levels).
 // Round 5 A/B, bit-identical (`profiles/r05/ab/ab19_*`): C5 12.03 -> 12.00 ms (its levels
 // 19-23 on the compile-time levels); dropping that band's halo instead (compact_pass NH)
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(NT, MINB) void compact_pass(const uint64_t *__restr
         }
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        prefetch(next < ntiles ? next : tile);
+        if (!FLTEE_CP_SKIP_SELF || next < ntiles) prefetch(next < ntiles ? next : tile);
         // Levels two per LDS round: z[f] = pick_{g+1}(pick_g(x[f], x[f+s]),
         // pick_g(x[f+2s], x[f+3s])) — 4 reads + 1 write per record per two levels
         // instead of 2 + 1 per level (ds_write_b64 costs ~3x a ds_read_b64), half the
@@ -697,7 +703,8 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             if (t + i * NT < Wn) win[t + i * NT] = pf[i];
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
-        if (FLTEE_FC_PF) prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
+        if (FLTEE_FC_PF && (!FLTEE_CP_SKIP_SELF || next < ntiles))
+            prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
         if constexpr (FLTEE_FC_FIXED_WALK == 2) {
             // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
             // in-order sum of its run up to that slot: a walk from x0 - lim (every legal run
