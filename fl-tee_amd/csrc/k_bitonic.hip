@@ -131,6 +131,9 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 //   but the passes on 64-B rows run far slower (round 5, bit-identical: C5 12.29 -> 13.65
 //   ms, C4 7.85 -> 8.45 ms; tile passes 367 -> 447 us on average,
 //   `profiles/r05/ab/ab14_tile_rows_of_8_rejected.jsonl`), so 4 stays.
+#ifndef FLTEE_TILE_SKIP_SELF
+#define FLTEE_TILE_SKIP_SELF 0
+#endif
 #ifndef FLTEE_TILE_MINW14
 #define FLTEE_TILE_MINW14 4
 #endif
@@ -737,8 +740,11 @@ __global__ __launch_bounds__(NT) void bitonic_tiles(uint64_t *__restrict__ data,
         __syncthreads();
         const uint32_t next = tile + gridDim.x;
         // always prefetch (the last round re-reads its own tile) so no branch wraps the loads
+        // FLTEE_TILE_SKIP_SELF: a block on its last tile prefetches nothing (one uniform
+        // branch around the whole prefetch; else it re-reads its own tile)
         auto prefetch = [&]() {
-            load_tile(tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog, wlog, dtile));
+            if (!FLTEE_TILE_SKIP_SELF || next < ntiles)
+                load_tile(tile_base(past_hole(next < ntiles ? next : tile, hole_at, hole_len), tlog, wlog, dtile));
         };
         // compile-time strided tiles: the prefetch after the fused tail's rounds (its
         // registers are then not live through the tail)
