@@ -131,8 +131,10 @@ constexpr int kLdsBatch = (FLTEE_LDS_BATCH == 0 || FLTEE_LDS_BATCH > G) ? G : FL
 //   but the passes on 64-B rows run far slower (round 5, bit-identical: C5 12.29 -> 13.65
 //   ms, C4 7.85 -> 8.45 ms; tile passes 367 -> 447 us on average,
 //   `profiles/r05/ab/ab14_tile_rows_of_8_rejected.jsonl`), so 4 stays.
+//   FLTEE_TILE_SKIP_SELF  a tile pass's block on its last tile prefetches nothing (round 5,
+//   bit-identical: C3 0.1295 -> 0.1285 ms, C4 / C5 unchanged, `profiles/r05/ab/ab21_*`)
 #ifndef FLTEE_TILE_SKIP_SELF
-#define FLTEE_TILE_SKIP_SELF 0
+#define FLTEE_TILE_SKIP_SELF 1
 #endif
 #ifndef FLTEE_TILE_MINW14
 #define FLTEE_TILE_MINW14 4
