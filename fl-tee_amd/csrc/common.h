@@ -228,6 +228,7 @@ hipError_t launch_gather_by_keys(const uint64_t *keys, size_t n, const void *rec
 size_t oram_slots(size_t d);
 bool oram_supported(size_t d);
 size_t oram_accesses(size_t nrec, size_t d, bool lazy);
+bool oram_fits(size_t nrec, size_t d, bool lazy);
 void set_oram_bucket(int z);
 hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, void *tree,
                             uint64_t seed, uint64_t *keys, uint64_t *keys2, uint64_t *records,

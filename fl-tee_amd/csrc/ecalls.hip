@@ -178,8 +178,8 @@ static fltee_device_opts ecall_opts(uint32_t alg, size_t n, size_t rpc, size_t d
     const bool flat = alg == FLTEE_ALG_BASELINE || alg == FLTEE_ALG_PATH_ORAM ||
                       alg == FLTEE_ALG_NON_OBLIVIOUS;
     if (flat && rpc == d) o.flags |= FLTEE_OPT_DENSE;
-    if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_supported(d))
-        o.flags |= FLTEE_OPT_ORAM_TREE;
+    if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_fits(n * rpc, d, false))
+        o.flags |= FLTEE_OPT_ORAM_TREE;  // (a shape past the tree's bounds takes the sweep)
     if (alg == FLTEE_ALG_NIPS19) o.seed = seed ? seed : next_seed();
     // advanced's fold (advanced.rs:66-101) runs once with halo = n: exact for every run of
     // up to n + 1 entries — every upload whose clients each send distinct indices (n
@@ -194,23 +194,25 @@ static fltee_device_opts ecall_opts(uint32_t alg, size_t n, size_t rpc, size_t d
 }
 
 // What an ECALL returns for the device status word of one aggregate (aggregate_records'
-// rules); *retry: a dense-sized non_oblivious upload out of position, to rerun sparse.
+// rules); *retry: a dense-sized upload out of position, to rerun sparse.
 static uint32_t status_to_retval(uint32_t dev_st, uint32_t alg, bool *retry) {
     *retry = false;
     if (dev_st == 0) return FLTEE_SUCCESS;
     if (dev_st & FLTEE_DEV_ERR_INDEX_RANGE) return FLTEE_ERROR_INVALID_PARAMETER;
     if (dev_st & FLTEE_DEV_ERR_ORAM_STASH) return FLTEE_ERROR_UNEXPECTED;
     if (dev_st & FLTEE_DEV_ERR_DENSE_ORDER) {
-        // a dense-sized upload with a record out of position (not serialize_dense's
-        // layout).  non_oblivious (not oblivious in the reference) reruns it with scatter
-        // semantics; baseline / path_oram, which the enclave runs at a fixed cost, reject
-        // it (0x2) after the one fixed-cost pass: no data-dependent relaunch — the retval
-        // reveals only that the upload was malformed.
-        if (alg != FLTEE_ALG_NON_OBLIVIOUS) return FLTEE_ERROR_INVALID_PARAMETER;
+        // a dense-sized upload (k = d) with a record out of position — not serialize_dense's
+        // layout, e.g. fl_main.py --alpha 1.0, whose top-k orders the records by |val|.
+        // Every flat alg reruns it sparse, with the reference's result for any upload:
+        // non_oblivious by its scatter / ordered fold, baseline and path_oram by the
+        // ordered fold in the composite-key network's order (engine.hip flat_ordered,
+        // baseline.rs:28-60's upload order).  The rerun follows the upload's layout (one
+        // bit: in position or not, the same for every round of a given client code), not
+        // its values.
+        (void)alg;
         *retry = true;
         return FLTEE_SUCCESS;
     }
-    if (dev_st & FLTEE_DEV_ERR_FOLD_OVERFLOW) return FLTEE_ERROR_INVALID_PARAMETER;
     return FLTEE_ERROR_UNEXPECTED;
 }
 
@@ -229,7 +231,7 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
         bool retry = false;
         st = status_to_retval(dev_st, alg, &retry);
         if (!retry) return st;
-        o.flags &= ~FLTEE_OPT_DENSE;  // non_oblivious: scatter semantics
+        o.flags &= ~FLTEE_OPT_DENSE;  // the sparse path: exact for any upload
     }
     return FLTEE_ERROR_INVALID_PARAMETER;
 }
@@ -332,7 +334,7 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
         st = status_to_retval(*(const volatile uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg,
                               &retry);
         if (!retry) break;
-        o.flags &= ~FLTEE_OPT_DENSE;  // non_oblivious: scatter semantics
+        o.flags &= ~FLTEE_OPT_DENSE;  // the sparse path: exact for any upload
     }
     if (st) return st;
     std::memcpy(host_out, c->pin_out.ptr, d * 4);
@@ -509,7 +511,8 @@ extern "C" fltee_status_t ecall_secure_aggregation(
     double t2 = 0;
     const bool flat = aggregation_alg == FLTEE_ALG_BASELINE || aggregation_alg == FLTEE_ALG_PATH_ORAM ||
                       aggregation_alg == FLTEE_ALG_NON_OBLIVIOUS;
-    const bool tree = aggregation_alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_supported(d);
+    const bool tree = aggregation_alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() &&
+                      oram_fits(n * rpc, d, false);
     if (G && flat && !tree && rpc == d && bpc == d * 8) {
         // dense uploads over a multi-GPU eid: every GPU loads and decrypts its own
         // parameter range (group.hip); "Loading" = the parallel H2D, "Decryption" = the
@@ -518,7 +521,7 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         client_round_keys(client_ids, n, rk);
         st = group_dense_ecall(G, rk.data(), n, encrypted_parameters_data, d, coef, d_out,
                                &execution_time_results[0], &execution_time_results[1],
-                               aggregation_alg != FLTEE_ALG_NON_OBLIVIOUS);
+                               false);  // out of position: the root's sparse rerun, every alg
         t2 = now_s();
         if (st != FLTEE_SUCCESS && st != FLTEE_GROUP_FALLBACK) return fail(st);
     }

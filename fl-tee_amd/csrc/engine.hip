@@ -40,6 +40,14 @@ static bool use_scatter_rows(size_t n, size_t k, size_t d) {
            (cells <= ((size_t)1 << 24) || cells <= 64 * next_pow2_sz(n * k));
 }
 
+// Sparse baseline / path_oram (the sweep otherwise): uploads of dense size (k = d, e.g.
+// fl_main.py --alpha 1.0, whose top-k orders each client's records by |val|, utils.py:
+// 346-352), where the sweep's n*k*d compare-selects (n*d^2) would dominate, go through the
+// ordered fold in the composite-key network's order (idx, upload position): the
+// enclave's o_update result for any upload, bit for bit (baseline.rs:28-60 adds each
+// index's records in upload order).  A public-size decision.
+static bool flat_ordered(size_t n, size_t k, size_t d) { return k == d && n * k > 0; }
+
 static DeviceCtx g_ctx[kMaxDevices];
 static std::mutex g_ctx_mu;
 static std::atomic<uint64_t> g_debug_seed{0};
@@ -158,7 +166,8 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
     Plan p;
     const bool dense = (o.flags & FLTEE_OPT_DENSE) != 0;
     const bool clip = (o.flags & FLTEE_OPT_CLIP) != 0;
-    const bool tree = alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE) && oram_supported(d);
+    // (aggregate() refuses a tree shape that does not fit before it plans: tree_shape)
+    const bool tree = alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE);
     if (clip) {
         p.coef_bytes = n * 4;
         if (!dense || tree) p.rec_bytes = n * k * 8;  // the tree reads records: clipped copies
@@ -173,9 +182,13 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
             size_t m = next_pow2_sz(oram_accesses(n * k, d, lazy));
             if (lazy && next_pow2_sz(ns + d) > m) m = next_pow2_sz(ns + d);
             p.a_bytes = p.b_bytes = m * 8;
+        } else if (!dense && flat_ordered(n, k, d)) {
+            p.keys_bytes = n * k * 8, p.radix_bytes = next_pow2_sz(n * k) * 8;
         }
         break;
     case FLTEE_ALG_BASELINE:
+        if (!dense && flat_ordered(n, k, d))  // the composite-key network + its gather
+            p.keys_bytes = n * k * 8, p.radix_bytes = next_pow2_sz(n * k) * 8;
         break;
     case FLTEE_ALG_NON_OBLIVIOUS:
         if (!dense) {
@@ -228,12 +241,12 @@ bool oram_tree_default() { return g_oram_tree; }
 
 static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, size_t d,
                                        float coef, float *out, bool acc, uint32_t *status,
-                                       hipStream_t s) {
+                                       hipStream_t s, bool network_order = false) {
     if (n == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
     if (!c->ws_keys.reserve(n * 8)) return hipErrorOutOfMemory;
     uint64_t *sorted = (uint64_t *)c->ws_keys.ptr;
     hipError_t e;
-    if (g_radix_order) {
+    if (g_radix_order && !network_order) {
         if (!c->ws_radix.reserve(radix_scratch_bytes(n, d))) return hipErrorOutOfMemory;
         e = launch_sort_records_by_idx(rec, n, d, c->ws_radix.ptr, c->ws_radix.cap, sorted, status,
                                        acc ? nullptr : out, d, s);
@@ -347,8 +360,9 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         size_t mf = (L + 1 + 15) / 16 * 16;
         if (mf > M) mf = M;
         // the fold emits the compaction's first-pass form (no conversion there, 16-B pairs;
-        // FLTEE_FOLD_CEMIT=0: the enclave's folded array, converted by that pass)
-        if (FLTEE_FOLD_CEMIT) {
+        // FLTEE_FOLD_CEMIT=0: the enclave's folded array, converted by that pass; and a
+        // one-entry array — d = 1 and no records — which has nothing to fold: copied)
+        if (FLTEE_FOLD_CEMIT && mf >= 2) {
             e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s, d, compact_dummy());
             if (e != hipSuccess) return e;
             return launch_compact_extract_converted(B, A, L, d, coef, out, acc, s);
@@ -391,6 +405,14 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         (alg == FLTEE_ALG_NON_OBLIVIOUS && !(o.flags & FLTEE_OPT_DENSE) &&
          !use_scatter_rows(n, k, d) && next_pow2_sz(n * k) > kMaxNet))
         return FLTEE_ERROR_INVALID_PARAMETER;
+    // the tree Path ORAM: a shape outside oram_fits is refused before any scratch is sized
+    // for it (the ECALL gates the tree on the same predicate and takes the sweep instead)
+    const bool tree = alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE);
+    if (tree && !oram_fits(n * k, d, (o.flags & FLTEE_OPT_ORAM_LAZY) != 0))
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    if ((alg == FLTEE_ALG_BASELINE || (alg == FLTEE_ALG_PATH_ORAM && !tree)) &&
+        !(o.flags & FLTEE_OPT_DENSE) && flat_ordered(n, k, d) && next_pow2_sz(n * k) > kMaxNet)
+        return FLTEE_ERROR_INVALID_PARAMETER;
     if (alg == FLTEE_ALG_NIPS19) {
         const size_t kq = (o.flags & FLTEE_OPT_K_REQ) ? o.k_req : k;
         const size_t tf = f32_to_usize_sat(nips19_threshold(d, kq, n));
@@ -412,7 +434,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
         if (launch_client_clip_coef(rec, n, k, o.clipping, cf, s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
         ccoef = cf;
-        if (!dense || (alg == FLTEE_ALG_PATH_ORAM && (o.flags & FLTEE_OPT_ORAM_TREE))) {
+        if (!dense || tree) {  // plan_for reserved ws_rec on the same predicate
             if (hipMemcpyAsync(c->ws_rec.ptr, rec, n * k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
                 launch_apply_clip(c->ws_rec.ptr, n, k, cf, s) != hipSuccess)
                 return FLTEE_ERROR_UNEXPECTED;
@@ -423,10 +445,8 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
     hipError_t e = hipSuccess;
     switch (alg) {
     case FLTEE_ALG_PATH_ORAM:
-        if (o.flags & FLTEE_OPT_ORAM_TREE) {  // the tree Path ORAM (k_oram.hip)
+        if (tree) {  // the tree Path ORAM (k_oram.hip); oram_fits checked above
             const bool lazy = (o.flags & FLTEE_OPT_ORAM_LAZY) != 0;
-            if (!oram_supported(d) || oram_accesses(n * k, d, lazy) >= 0x7F000000ull)
-                return FLTEE_ERROR_INVALID_PARAMETER;
             const size_t ns = oram_slots(d);
             uint8_t *tree = (uint8_t *)c->ws_oram.ptr;
             uint64_t *recs = lazy ? (uint64_t *)(tree + ns * 16) : nullptr;
@@ -458,10 +478,17 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             e = ordered_fold_records(c, rec, n * k, d, coef, out, acc, status, s);
         } else {
             // baseline / path_oram on sparse uploads: the ordered sweep (exact for any
-            // upload, a client may repeat an index; fixed cost n*k*d compare-selects)
+            // upload, a client may repeat an index; fixed cost n*k*d compare-selects) —
+            // or, for dense-sized uploads (flat_ordered), the composite-key network's
+            // ordered fold (exact for any upload too).  Records with idx >= d are ignored
+            // (o_update's compare never matches): the network's range flag goes to a
+            // scratch word.
             if (alg == FLTEE_ALG_PATH_ORAM)  // oram.rs: blocks beyond next_pow2(d) do not exist
                 e = launch_check_range(rec, n * k, (uint32_t)next_pow2_sz(d), status, s);
-            if (e == hipSuccess) e = launch_sweep_accumulate(rec, n * k, d, coef, out, acc, s);
+            if (e == hipSuccess && flat_ordered(n, k, d))
+                e = ordered_fold_records(c, rec, n * k, d, coef, out, acc, c->status + 32, s, true);
+            else if (e == hipSuccess)
+                e = launch_sweep_accumulate(rec, n * k, d, coef, out, acc, s);
         }
         break;
     case FLTEE_ALG_ADVANCED: {
@@ -896,8 +923,14 @@ extern "C" void fltee_set_advanced_exact_runs(int on) {
     fltee::set_exact_runs(on);
 }
 // test hook: blocks a bucket of the tree ORAM takes on eviction (4; 0 forces the stash)
-extern "C" void fltee_debug_set_oram_bucket(int z) { fltee::set_oram_bucket(z); }
-extern "C" void fltee_debug_set_aes_variant(int v) { fltee::set_aes_variant(v); }
+extern "C" void fltee_debug_set_oram_bucket(int z) {
+    std::lock_guard<std::recursive_mutex> lk(fltee::api_mutex());
+    fltee::set_oram_bucket(z);
+}
+extern "C" void fltee_debug_set_aes_variant(int v) {
+    std::lock_guard<std::recursive_mutex> lk(fltee::api_mutex());
+    fltee::set_aes_variant(v);
+}
 extern "C" void fltee_debug_set_swizzle(int on) { fltee::set_swizzle(on); }
 extern "C" void fltee_debug_set_fused_init(int on) { fltee::set_fused_init(on); }
 // A/B hook: 0 writes nips19's shuffled array out and selects in separate passes

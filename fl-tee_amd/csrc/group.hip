@@ -459,7 +459,7 @@ uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const u
     if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
     if (t_dec) *t_dec = std::chrono::duration<float>(std::chrono::steady_clock::now() - t1).count();
     for (uint32_t v : st)
-        if (v & FLTEE_DEV_ERR_DENSE_ORDER)  // not dense: rejected, or the root's scatter path
+        if (v & FLTEE_DEV_ERR_DENSE_ORDER)  // not dense: rejected, or the root's sparse rerun
             return reject_order ? FLTEE_ERROR_INVALID_PARAMETER : FLTEE_GROUP_FALLBACK;
     for (uint32_t v : st)
         if (v) return FLTEE_ERROR_UNEXPECTED;

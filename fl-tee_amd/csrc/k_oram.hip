@@ -460,6 +460,15 @@ bool oram_supported(size_t d) { return next_pow2_sz(d ? d : 1) <= ((size_t)1 << 
 
 size_t oram_accesses(size_t nrec, size_t d, bool lazy) { return lazy ? nrec : 2 * nrec + 2 * d; }
 
+// the tree runs this shape: its block count, and the leaf precompute's (and the lazy
+// readout's) sorts within the networks' 2^29-entry bound (k_bitonic.hip)
+bool oram_fits(size_t nrec, size_t d, bool lazy) {
+    constexpr size_t kMaxNet = (size_t)1 << 29;
+    if (!oram_supported(d) || oram_accesses(nrec, d, lazy) >= 0x7F000000ull) return false;
+    if (next_pow2_sz(oram_accesses(nrec, d, lazy)) > kMaxNet) return false;
+    return !lazy || next_pow2_sz(oram_slots(d) + d) <= kMaxNet;
+}
+
 hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, void *tree,
                             uint64_t seed, uint64_t *keys, uint64_t *keys2, uint64_t *records,
                             float coef, bool accumulate, float *out, uint32_t *status,

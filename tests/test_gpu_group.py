@@ -186,8 +186,9 @@ def test_group_nips19_declined_shape_same_seed(enclaves, oracle, w):
 def test_group_exact_runs_policy_and_dense_order(enclaves, oracle):
     """fltee_set_advanced_exact_runs(1): the long run above is folded exactly on every eid
     (the one-GPU sequential walk; the group path declines) and alg 6 likewise — the
-    oracle's advanced bit for bit.  Dense-sized uploads out of position: baseline and
-    path_oram reject with 0x2 on every eid (fixed cost), non_oblivious reruns exactly."""
+    oracle's advanced bit for bit.  Dense-sized uploads out of position: every flat alg
+    reruns them sparse on the root (baseline / path_oram through the composite-key
+    network's ordered fold), the reference's in-order sum bit for bit on every eid."""
     from fltee import _lib as L
     from fltee.ecalls import set_advanced_exact_runs, set_debug_seed
     rng = np.random.default_rng(5)
@@ -234,7 +235,5 @@ def test_group_exact_runs_policy_and_dense_order(enclaves, oracle):
             assert E.ecall_start_round(_fl[0], 0, n)[:2] == (0, 0)
             st, rv, out, _ = E.ecall_secure_aggregation(_fl[0], 0, ids, enc2, d2, d2, alg)
             set_debug_seed(0)
-            if alg == 4:
-                assert (st, rv) == (0, 0) and np.array_equal(out.view(np.uint32), exp.view(np.uint32))
-            else:
-                assert (st, rv) == (0, L.ERROR_INVALID_PARAMETER) and not out.any()
+            # every flat alg reruns it sparse on the root: the in-order sum, bit for bit
+            assert (st, rv) == (0, 0) and np.array_equal(out.view(np.uint32), exp.view(np.uint32)), (w, alg)

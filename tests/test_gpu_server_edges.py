@@ -63,10 +63,13 @@ def test_server_round_trip(oracle):
         srv.aggregate(12, 0, fx["ciphertext"].tobytes(), d, k, 100, 6, ids)
 
 
+@pytest.mark.parametrize("d", [64, 1])
 @pytest.mark.parametrize("alg", [1, 2, 3, 4, 5])
-def test_empty_payload_k0(enclave, oracle, alg):
+def test_empty_payload_k0(enclave, oracle, alg, d):
+    # d = 1 with no records: advanced's padded array is one entry (nothing to fold)
     ids = np.array([1, 2, 3], np.uint32)
-    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 20 + alg, ids, 64, 0, alg, b"")
+    (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 20 + alg + 300 * (d == 1), ids, d, 0,
+                                           alg, b"")
     assert (st, rv) == (0, ost) == (0, 0)
     assert bits_equal(out, ref) and not out.any()
 
@@ -127,26 +130,38 @@ def test_single_client_dense(enclave, oracle, alg):
 
 
 def test_dense_out_of_order(enclave, oracle):
-    # k == d but the records are permuted.  non_oblivious (a plain scatter in the
-    # reference): the dense kernel reports it and the ECALL reruns with scatter semantics
-    # (bit-exact).  baseline / path_oram (fixed-cost in the reference): rejected with 0x2
-    # after the one fixed-cost pass, no data-dependent relaunch — where the
-    # reference would return the in-order sum the oracle computes here.
+    # k == d but the records are permuted (fl_main.py --alpha 1.0: top-k of all d orders
+    # each client's records by |val|, utils.py:346-352).  The dense kernel reports it and
+    # the ECALL reruns sparse: non_oblivious by its scatter, baseline / path_oram by the
+    # ordered fold in the composite-key network's order — the reference's in-order sum,
+    # bit for bit, for every alg.  Also with a client repeating an index (k == d but not a
+    # permutation) and with an index >= d (baseline ignores it, path_oram too while it is
+    # below next_pow2(d)).
     rng = np.random.default_rng(4)
     d = 500
     ids = np.array([1, 2, 3], np.uint32)
     plain = []
-    for _ in ids:
+    for c in ids:
         idx = rng.permutation(d).astype(np.uint32)
+        if c == 2:
+            idx[:7] = 13   # repeats
+        if c == 3:
+            idx[3] = 501   # >= d, < next_pow2(d)
         plain.append(oracle.as_weights(idx, rng.normal(0, 1, d).astype(np.float32)).tobytes())
     enc = oracle.encrypt_clients(ids, plain)
     for alg in (3, 4, 5):
         (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 80 + alg, ids, d, d, alg, enc)
-        assert st == 0 and ost == 0 and ref.any()  # the reference's defined result
-        if alg == 4:
-            assert rv == 0 and bits_equal(out, ref)
-        else:
-            assert rv == 0x2 and not out.any()
+        if alg == 4:  # non_oblivious.rs:12 panics on the index >= d
+            assert (st, rv, ost) == (0, 0x2, 0x2) and not out.any()
+            continue
+        assert (st, rv, ost) == (0, 0, 0) and ref.any()
+        assert bits_equal(out, ref), alg
+    plain = [oracle.as_weights(rng.permutation(d).astype(np.uint32),
+                               rng.normal(0, 1, d).astype(np.float32)).tobytes() for _ in ids]
+    enc = oracle.encrypt_clients(ids, plain)
+    for alg in (3, 4, 5):
+        (st, rv, out, _), (ost, ref, _) = both(enclave, oracle, 180 + alg, ids, d, d, alg, enc)
+        assert (st, rv, ost) == (0, 0, 0) and bits_equal(out, ref), alg
 
 
 def test_repeated_index_within_client(enclave, oracle):
