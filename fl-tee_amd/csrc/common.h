@@ -154,26 +154,87 @@ hipError_t launch_advanced_init(const void *rec, size_t nrec, size_t d, size_t m
 hipError_t launch_advanced_init_range(const void *rec, size_t nrec, size_t d, size_t pbase,
                                       size_t m, uint64_t *dst, hipStream_t s);
 size_t fold_context(size_t halo);  // records of context the fold re-reads: halo rounded to 16
-// The fold reports FLTEE_DEV_ERR_FOLD_OVERFLOW iff a run inside [0, fold_len) has more than
-// fold_run_limit(halo) = halo + 1 entries (halo = n: some client repeated an index): a
-// property of the data alone, checked in the same single pass (no rerun: the caller
-// rejects the call); below it the sums are exact.
-uint32_t fold_run_limit(size_t halo);
+// The streaming fold's side record per lane (k_fold.hip header: runs of any length) and the
+// segmented aggregate of consecutive pieces the patch scans.
+constexpr uint32_t kFsPiece = 1u, kFsFull = 2u, kFsCorr = 4u;
+struct FoldSide {
+    uint32_t F, K;  // keys of the piece's first and last positions
+    float Q;        // in-order partial of the run ending the piece, over the piece
+    uint32_t fl;    // kFsPiece: the piece holds positions; kFsFull: one key; kFsCorr: below
+    uint32_t ck;    // kFsCorr: the key of a run begun before the walk and ended in the chunk
+    float S;        // kFsCorr: that run's in-order sum from the walk start to its end
+    uint32_t pad[2];
+};
+struct FoldAgg {
+    uint32_t F, K;
+    float Q;
+    uint32_t fl;
+};
+// FoldAgg: the segmented aggregate of consecutive pieces — first key, last key, one key
+// throughout, and the in-order (within a piece; re-associated across pieces) partial of
+// the run ending the range.  combine is associative.
+__device__ __forceinline__ FoldAgg fa_combine(const FoldAgg &x, const FoldAgg &y) {
+    if (!(x.fl & kFsPiece)) return y;
+    if (!(y.fl & kFsPiece)) return x;
+    const bool yfull = (y.fl & kFsFull) != 0;
+    FoldAgg r;
+    r.F = x.F;
+    r.K = y.K;
+    r.fl = kFsPiece | (((x.fl & kFsFull) && yfull && x.K == y.F) ? kFsFull : 0u);
+    r.Q = (yfull && y.F == x.K) ? __fadd_rn(x.Q, y.Q) : y.Q;
+    return r;
+}
+
+__device__ __forceinline__ FoldAgg fa_of(const FoldSide &sd) {
+    FoldAgg a;
+    a.F = sd.F;
+    a.K = sd.K;
+    a.Q = sd.Q;
+    a.fl = sd.fl & (kFsPiece | kFsFull);
+    return a;
+}
+
+__device__ __forceinline__ FoldAgg fa_empty() {
+    FoldAgg a;
+    a.F = a.K = 0;
+    a.Q = 0.0f;
+    a.fl = 0;
+    return a;
+}
+
+// lanes of a streaming fold over span positions (0: the one-lane walk: no side records)
+size_t fold_lanes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase);
+size_t fold_side_bytes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase);
 // cemit_d != 0: emit the compaction's first-pass form instead (run ends with idx < cemit_d
-// as (c = p - idx, sum), the rest as cdummy; whole arrays only: origin = pbase = 0)
+// as (c = p - idx, sum), the rest as cdummy; whole arrays only: origin = pbase = 0).
+// side: fold_lanes() records (required unless the one-lane walk); then
+// launch_fold_range_patch writes the long runs' records (after the totals of the ranges
+// before, prev[0, nprev), for a position-sharded array)
 hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
                              size_t end, long long pbase, size_t fold_len, size_t halo,
-                             uint32_t *status, hipStream_t s, size_t cemit_d = 0,
+                             FoldSide *side, hipStream_t s, size_t cemit_d = 0,
                              uint64_t cdummy = 0);
+hipError_t launch_fold_range_total(const FoldSide *side, size_t lanes, FoldAgg *total,
+                                   hipStream_t s);
+hipError_t launch_fold_range_patch(uint64_t *dst, size_t span, size_t origin, long long pbase,
+                                   size_t fold_len, size_t halo, const FoldSide *side,
+                                   const FoldAgg *prev, size_t nprev, hipStream_t s,
+                                   size_t cemit_d = 0, uint64_t cdummy = 0);
+// the whole array: fold + patch (side_ws: >= fold_side_bytes(m, fold_len, halo, 0, 0))
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
-                       uint32_t *status, hipStream_t s, size_t cemit_d = 0, uint64_t cdummy = 0);
+                       void *side_ws, size_t side_cap, hipStream_t s, size_t cemit_d = 0,
+                       uint64_t cdummy = 0);
 hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out, bool accumulate,
                           hipStream_t s);
 // k_compact.hip
 // fold (fold_len == L) + compaction from the SORTED array; hipErrorNotSupported: fold apart
+// lb: fc_lookback_bytes() of zeroed look-back slots (the tiles' carries), *epoch: the
+// device's launch counter for them (at 2^30 - 1 the caller zeroes the slots and resets it)
+size_t fc_lookback_bytes(size_t M, size_t L, size_t d, size_t halo);
 hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
                                        size_t halo, float coef, float *out, bool accumulate,
-                                       uint32_t *status, hipStream_t s);
+                                       uint32_t *status, hipStream_t s, void *lb, size_t lb_cap,
+                                       uint32_t *epoch);
 hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t d, float coef,
                                   float *out, bool accumulate, hipStream_t s);
 // the same from launch_fold(..., cemit_d = d, compact_dummy())'s output

@@ -40,6 +40,9 @@ struct DeviceCtx {
     Buffer ws_cnt, ws_sel;                               // nips19's selected list
     Buffer ws_keys, ws_radix;  // ordered folds: records sorted by idx, the counting sort's scratch
     Buffer ws_oram;            // path_oram tree mode: the tree + stash slots, then their records
+    Buffer ws_side;            // advanced's streaming fold: its side records (k_fold.hip)
+    Buffer ws_lb;              // the fused fold's look-back slots (k_compact.hip), zeroed
+    uint32_t fc_epoch = 0;     // their launch counter
     uint32_t *host_word = nullptr;                       // pinned readback word
     hipStream_t stream = nullptr;                        // ECALL stream
     hipStream_t copy_stream = nullptr;                   // ECALL H2D (pipelined load)
@@ -60,8 +63,9 @@ float nips19_threshold(size_t d, size_t k, size_t n);
 // API selects it per call with FLTEE_OPT_ORAM_TREE
 void set_oram_tree(int on);
 bool oram_tree_default();
-// advanced / alg 6 in the ECALLs: the exact fold for any run length at the public
-// worst-case cost (fltee_set_advanced_exact_runs), else runs > n + 1 are rejected
+// advanced / alg 6 in the ECALLs: the one-lane sequential fold at the public worst-case
+// cost (fltee_set_advanced_exact_runs: the enclave's sums bit for bit for any run length),
+// else the halo fold (bit for bit up to n + 1 entries a run, re-associated beyond)
 void set_exact_runs(int on);
 bool exact_runs_default();
 

@@ -159,8 +159,20 @@ static size_t f32_to_usize_sat(float x) {
 struct Plan {
     size_t a_bytes = 0, b_bytes = 0, mat_bytes = 0, r_bytes = 0, coef_bytes = 0, rec_bytes = 0;
     size_t keys_bytes = 0, radix_bytes = 0;  // ordered fold: sorted records, sort scratch
+    size_t side_bytes = 0;                   // advanced's streaming fold: side records
+    size_t lb_bytes = 0;                     // advanced's fused fold: look-back slots
     size_t oram_bytes = 0;                   // path_oram tree: slots (16 B) + their records (8 B)
 };
+
+// the side records of advanced's streaming fold over its array (M) or its compaction
+// prefix (run_advanced's mf), whichever has more lanes
+static size_t advanced_side_bytes(size_t n, size_t k, size_t d, size_t halo) {
+    const size_t L = n * k + d, M = next_pow2_sz(L);
+    size_t mf = (L + 1 + 15) / 16 * 16;
+    if (mf > M) mf = M;
+    const size_t a = fold_side_bytes(M, M, halo, 0, 0), b = mf >= 2 ? fold_side_bytes(mf, L, halo, 0, 0) : 0;
+    return a > b ? a : b;
+}
 
 static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
     Plan p;
@@ -198,10 +210,14 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
         break;
     case FLTEE_ALG_ADVANCED:
         p.a_bytes = p.b_bytes = next_pow2_sz(n * k + d) * 8;
+        p.side_bytes = advanced_side_bytes(n, k, d, o.fold_halo ? o.fold_halo : n);
+        p.lb_bytes = fc_lookback_bytes(next_pow2_sz(n * k + d), n * k + d, d, o.fold_halo ? o.fold_halo : n);
         break;
     case FLTEE_ALG_OPTIMIZED: {
         size_t b = o.batch ? (o.batch < n ? o.batch : n) : n;
         p.a_bytes = p.b_bytes = next_pow2_sz(b * k + d) * 8;
+        p.side_bytes = advanced_side_bytes(b, k, d, o.fold_halo ? o.fold_halo : b);
+        p.lb_bytes = fc_lookback_bytes(next_pow2_sz(b * k + d), b * k + d, d, o.fold_halo ? o.fold_halo : b);
         break;
     }
     case FLTEE_ALG_NIPS19: {
@@ -216,12 +232,22 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
     return p;
 }
 
+// the fused fold's look-back slots: grown zeroed (a stale slot must never carry a live
+// epoch), the epochs starting over
+static bool reserve_lb(DeviceCtx *c, size_t bytes) {
+    if (bytes <= c->ws_lb.cap) return true;
+    if (!c->ws_lb.reserve(bytes) || hipMemset(c->ws_lb.ptr, 0, c->ws_lb.cap) != hipSuccess) return false;
+    c->fc_epoch = 0;
+    return true;
+}
+
 static bool reserve_plan(DeviceCtx *c, const Plan &p) {
     return c->ws_a.reserve(p.a_bytes) && c->ws_b.reserve(p.b_bytes) &&
            c->ws_mat.reserve(p.mat_bytes) && c->ws_r.reserve(p.r_bytes) &&
            c->ws_coef.reserve(p.coef_bytes) && c->ws_rec.reserve(p.rec_bytes) &&
            c->ws_keys.reserve(p.keys_bytes) && c->ws_radix.reserve(p.radix_bytes) &&
-           c->ws_oram.reserve(p.oram_bytes);
+           c->ws_oram.reserve(p.oram_bytes) && c->ws_side.reserve(p.side_bytes) &&
+           reserve_lb(c, p.lb_bytes);
 }
 
 // The ordered fold of n records (common.rs:25-35, non_oblivious.rs:11-13): the records in
@@ -351,7 +377,15 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
     // the fold runs inside the compaction's first pass; the k_req != k quirk leaves
     // unfolded records competing for that prefix and keeps the full network.
     if (fold_len == L && g_advanced_compaction) {
-        e = launch_fold_compact_extract(A, B, M, L, d, halo ? halo : n, coef, out, acc, status, s);
+        const size_t lbb = fc_lookback_bytes(M, L, d, halo ? halo : n);
+        if (lbb && (lbb > c->ws_lb.cap || c->fc_epoch >= (1u << 30) - 1)) {
+            // new slots hold whatever was there: zero them (the epochs start over)
+            if (!c->ws_lb.reserve(lbb) || hipMemsetAsync(c->ws_lb.ptr, 0, c->ws_lb.cap, s) != hipSuccess)
+                return hipErrorOutOfMemory;
+            c->fc_epoch = 0;
+        }
+        e = launch_fold_compact_extract(A, B, M, L, d, halo ? halo : n, coef, out, acc, status, s,
+                                        c->ws_lb.ptr, c->ws_lb.cap, &c->fc_epoch);
         if (e != hipErrorNotSupported) return e;
     }
     if (fold_len == L && g_advanced_compaction) {
@@ -362,16 +396,21 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         // the fold emits the compaction's first-pass form (no conversion there, 16-B pairs;
         // FLTEE_FOLD_CEMIT=0: the enclave's folded array, converted by that pass; and a
         // one-entry array — d = 1 and no records — which has nothing to fold: copied)
+        if (!c->ws_side.reserve(fold_side_bytes(mf, fold_len, halo ? halo : n, 0, 0)))
+            return hipErrorOutOfMemory;
         if (FLTEE_FOLD_CEMIT && mf >= 2) {
-            e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s, d, compact_dummy());
+            e = launch_fold(A, B, mf, fold_len, halo ? halo : n, c->ws_side.ptr, c->ws_side.cap, s,
+                            d, compact_dummy());
             if (e != hipSuccess) return e;
             return launch_compact_extract_converted(B, A, L, d, coef, out, acc, s);
         }
-        e = launch_fold(A, B, mf, fold_len, halo ? halo : n, status, s);
+        e = launch_fold(A, B, mf, fold_len, halo ? halo : n, c->ws_side.ptr, c->ws_side.cap, s);
         if (e != hipSuccess) return e;
         return launch_compact_extract(B, A, L, d, coef, out, acc, s);
     }
-    e = launch_fold(A, B, M, fold_len, halo ? halo : n, status, s);
+    if (!c->ws_side.reserve(fold_side_bytes(M, fold_len, halo ? halo : n, 0, 0)))
+        return hipErrorOutOfMemory;
+    e = launch_fold(A, B, M, fold_len, halo ? halo : n, c->ws_side.ptr, c->ws_side.cap, s);
     if (e != hipSuccess) return e;
     e = bitonic_sort(B, M, 0, 0, s, L);  // the fold copies the pads past fold_len
     if (e == hipSuccess) e = launch_extract(B, d, coef, out, acc, s);
@@ -555,7 +594,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
 size_t workspace_bytes(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
     const Plan p = plan_for(alg, n, k, d, o);
     return p.a_bytes + p.b_bytes + p.mat_bytes + p.r_bytes + p.coef_bytes + p.rec_bytes +
-           p.keys_bytes + p.radix_bytes + p.oram_bytes;
+           p.keys_bytes + p.radix_bytes + p.oram_bytes + p.side_bytes + p.lb_bytes;
 }
 
 bool reserve(uint32_t alg, size_t n, size_t k, size_t d, const fltee_device_opts &o) {
@@ -625,8 +664,12 @@ extern "C" fltee_status_t fltee_fold_device(const void *d_src, void *d_dst, size
                                             size_t fold_len, size_t halo, uint32_t *d_status,
                                             void *stream) {
     if (fold_len == 0 || fold_len > m || !d_status) return FLTEE_ERROR_INVALID_PARAMETER;
-    return launch_fold((const uint64_t *)d_src, (uint64_t *)d_dst, m, fold_len, halo, d_status,
-                       (hipStream_t)stream) == hipSuccess
+    std::lock_guard<std::recursive_mutex> lk(api_mutex());
+    DeviceCtx *c = current_ctx();
+    if (!c || !c->ws_side.reserve(fold_side_bytes(m, fold_len, halo, 0, 0)))
+        return FLTEE_ERROR_OUT_OF_MEMORY;
+    return launch_fold((const uint64_t *)d_src, (uint64_t *)d_dst, m, fold_len, halo,
+                       c->ws_side.ptr, c->ws_side.cap, (hipStream_t)stream) == hipSuccess
                ? FLTEE_SUCCESS
                : FLTEE_ERROR_INVALID_PARAMETER;
 }
@@ -722,18 +765,48 @@ extern "C" fltee_status_t fltee_bitonic_range_steps_device(void *d_records, size
 
 extern "C" size_t fltee_fold_context(size_t halo) { return fold_context(halo); }
 
+extern "C" size_t fltee_fold_side_bytes(size_t span, size_t halo) {
+    return sizeof(FoldSide) * fold_lanes(span, (size_t)1 << 62, halo, 1, 1);
+}
+
 extern "C" fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m,
                                                   size_t origin, size_t end, int64_t pos_base,
-                                                  size_t fold_len, size_t halo,
-                                                  uint32_t *d_status, void *stream) {
-    if (!d_status || origin < fold_context(halo) || end > m || origin >= end || (origin & 1) ||
+                                                  size_t fold_len, size_t halo, void *d_side,
+                                                  void *stream) {
+    // range mode: [0, origin) holds >= fold_context(halo) + 1 records of context
+    if (!d_side || origin < fold_context(halo) + 1 || end > m || origin >= end || (origin & 1) ||
         (end & 1) || (m & 1))
         return FLTEE_ERROR_INVALID_PARAMETER;
     if (end < m ? false : (int64_t)end + pos_base < (int64_t)fold_len)
         return FLTEE_ERROR_INVALID_PARAMETER;  // needs the next range's first record
     return launch_fold_range((const uint64_t *)d_src, (uint64_t *)d_dst, m, origin, end,
-                             (long long)pos_base, fold_len, halo, d_status,
+                             (long long)pos_base, fold_len, halo, (FoldSide *)d_side,
                              (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_fold_range_total_device(const void *d_side, size_t span,
+                                                        size_t halo, void *d_total, void *stream) {
+    if (!d_side || !d_total) return FLTEE_ERROR_INVALID_PARAMETER;
+    const size_t lanes = fold_lanes(span, (size_t)1 << 62, halo, 1, 1);
+    return launch_fold_range_total((const FoldSide *)d_side, lanes, (FoldAgg *)d_total,
+                                   (hipStream_t)stream) == hipSuccess
+               ? FLTEE_SUCCESS
+               : FLTEE_ERROR_UNEXPECTED;
+}
+
+extern "C" fltee_status_t fltee_fold_range_patch_device(void *d_dst, size_t origin, size_t end,
+                                                        int64_t pos_base, size_t fold_len,
+                                                        size_t halo, const void *d_side,
+                                                        const void *d_prev_totals, size_t n_prev,
+                                                        void *stream) {
+    if (!d_dst || !d_side || origin >= end || (n_prev && !d_prev_totals))
+        return FLTEE_ERROR_INVALID_PARAMETER;
+    return launch_fold_range_patch((uint64_t *)d_dst, end - origin, origin, (long long)pos_base,
+                                   fold_len, halo, (const FoldSide *)d_side,
+                                   (const FoldAgg *)d_prev_totals, n_prev, (hipStream_t)stream) ==
+                   hipSuccess
                ? FLTEE_SUCCESS
                : FLTEE_ERROR_UNEXPECTED;
 }

@@ -59,6 +59,7 @@ struct Rank {
     hipStream_t s = nullptr;
     ncclComm_t comm = nullptr;
     Buffer cipher, rec, rk, out, chunk, spare, fold, fold_dst, cbuf, ctmp, lap, list, cnt, st;
+    Buffer side, tot;  // advanced's fold: side records; its total, then the totals before it
 };
 
 struct Group {
@@ -578,46 +579,58 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
             return FLTEE_ERROR_UNEXPECTED;
     }
     if (network(G, chunk, spare, M, 0, 0, W > 1, n * k + d) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-    // fold (advanced.rs:66-101) with the previous range's tail in front and the next
-    // range's head behind, halo n: a run of more than n + 1 entries rejects the call (as
-    // the ECALL does: fold_run_limit), no rerun
+    // fold (advanced.rs:66-101) with the previous range's tail in front (the halo and the
+    // record before it) and the next range's head behind, halo n; then the long-run patch
+    // (k_fold.hip): every range's segmented total goes to the ranges after it (device to
+    // device), which finish the runs begun before them.  Fixed cost: no status readback.
     const size_t fold_len = L;
     const size_t h = n;
+    const size_t X = fold_context(h) + 16;  // context records in front of each range
     std::vector<float *> outs(W);
     {
-        const size_t H = fold_context(h);
-        if (H > C) return FLTEE_GROUP_FALLBACK;
-        const size_t m = H + C + 16;
+        if (X > C) return FLTEE_GROUP_FALLBACK;
+        const size_t m = X + C + 16;
+        const size_t lanes = fold_lanes(C, fold_len, h, X, 1);
         std::vector<P2P> ops;
         for (int i = 0; i < W; ++i) {
             Rank &R = G.r[i];
-            if (!reserve_on(R, R.fold, m * 8) || !reserve_on(R, R.fold_dst, m * 8) || !reserve_on(R, R.st, 64))
+            if (!reserve_on(R, R.fold, m * 8) || !reserve_on(R, R.fold_dst, m * 8) ||
+                !reserve_on(R, R.side, lanes * sizeof(FoldSide) + 64) ||
+                !reserve_on(R, R.tot, (size_t)(W + 1) * sizeof(FoldAgg)))
                 return FLTEE_ERROR_OUT_OF_MEMORY;
             uint64_t *f = (uint64_t *)R.fold.ptr;
-            ops.push_back({i, i, chunk[i], f + H, C * 8});
-            if (i > 0) ops.push_back({i - 1, i, chunk[i - 1] + C - H, f, H * 8});
-            if (i < W - 1) ops.push_back({i + 1, i, chunk[i + 1], f + H + C, 16 * 8});
-            if (hipMemsetAsync(R.st.ptr, 0, 4, R.s) != hipSuccess ||
-                (i == 0 && fill_pads(f, H, R.s) != hipSuccess) ||
-                (i == W - 1 && fill_pads(f + H + C, 16, R.s) != hipSuccess))
+            ops.push_back({i, i, chunk[i], f + X, C * 8});
+            if (i > 0) ops.push_back({i - 1, i, chunk[i - 1] + C - X, f, X * 8});
+            if (i < W - 1) ops.push_back({i + 1, i, chunk[i + 1], f + X + C, 16 * 8});
+            if ((i == 0 && fill_pads(f, X, R.s) != hipSuccess) ||
+                (i == W - 1 && fill_pads(f + X + C, 16, R.s) != hipSuccess))
                 return FLTEE_ERROR_UNEXPECTED;
         }
         if (p2p(G, ops) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-        std::vector<const uint32_t *> sw;
+        // tot[0] = this range's total, tot[1 + j] = range j's (j < i)
         for (int i = 0; i < W; ++i) {
             Rank &R = G.r[i];
             if (hipSetDevice(R.dev) != hipSuccess ||
-                launch_fold_range((const uint64_t *)R.fold.ptr, (uint64_t *)R.fold_dst.ptr, m, H, H + C,
-                                  (long long)(i * C) - (long long)H, fold_len, h,
-                                  (uint32_t *)R.st.ptr, R.s) != hipSuccess)
+                launch_fold_range((const uint64_t *)R.fold.ptr, (uint64_t *)R.fold_dst.ptr, m, X, X + C,
+                                  (long long)(i * C) - (long long)X, fold_len, h, (FoldSide *)R.side.ptr,
+                                  R.s) != hipSuccess ||
+                launch_fold_range_total((const FoldSide *)R.side.ptr, lanes, (FoldAgg *)R.tot.ptr,
+                                        R.s) != hipSuccess)
                 return FLTEE_ERROR_UNEXPECTED;
-            sw.push_back((const uint32_t *)R.st.ptr);
         }
-        std::vector<uint32_t> st;
-        if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
-        bool over = false;
-        for (uint32_t v : st) over |= (v & FLTEE_DEV_ERR_FOLD_OVERFLOW) != 0;
-        if (over) return FLTEE_ERROR_INVALID_PARAMETER;
+        std::vector<P2P> tops;
+        for (int i = 0; i < W; ++i)
+            for (int j = 0; j < i; ++j)
+                tops.push_back({j, i, G.r[j].tot.ptr, (FoldAgg *)G.r[i].tot.ptr + 1 + j, sizeof(FoldAgg)});
+        if (p2p(G, tops) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        for (int i = 0; i < W; ++i) {
+            Rank &R = G.r[i];
+            if (hipSetDevice(R.dev) != hipSuccess ||
+                launch_fold_range_patch((uint64_t *)R.fold_dst.ptr, C, X, (long long)(i * C) - (long long)X,
+                                        fold_len, h, (const FoldSide *)R.side.ptr,
+                                        (const FoldAgg *)R.tot.ptr + 1, (size_t)i, R.s) != hipSuccess)
+                return FLTEE_ERROR_UNEXPECTED;
+        }
     }
     for (int i = 0; i < W; ++i) {  // advanced.rs:106-111 + :32-34: each range's representatives
         Rank &R = G.r[i];
@@ -625,7 +638,7 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
         if (!o || !reserve_on(R, R.cbuf, (d + C) * 8) || !reserve_on(R, R.ctmp, (d + C) * 8))
             return FLTEE_ERROR_OUT_OF_MEMORY;
         outs[i] = o;
-        if (launch_compact_offset((const uint64_t *)R.fold_dst.ptr + fold_context(h), C, d,
+        if (launch_compact_offset((const uint64_t *)R.fold_dst.ptr + X, C, d,
                                   (uint64_t *)R.cbuf.ptr, (uint64_t *)R.ctmp.ptr, 1.0f, o, R.s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
     }
@@ -718,7 +731,7 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
     }
     std::vector<const uint64_t *> rec;
     if (uint32_t st = group_records(G, in, n, k, lo, hi, rec)) return st;
-    const size_t h = halo;  // halo n: a run of more than n + 1 entries rejects the call (no rerun)
+    const size_t h = halo;  // halo n: bit for bit up to n + 1 entries a run, re-associated beyond
     {
         std::vector<P2P> ops;
         std::vector<const uint32_t *> sw;
@@ -741,11 +754,7 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
             }
             sw.push_back((const uint32_t *)R.st.ptr);
         }
-        std::vector<uint32_t> st;
-        if (read_words(G, sw, st)) return FLTEE_ERROR_UNEXPECTED;
-        bool over = false;
-        for (uint32_t v : st) over |= (v & FLTEE_DEV_ERR_FOLD_OVERFLOW) != 0;
-        if (over) return FLTEE_ERROR_INVALID_PARAMETER;
+        (void)sw;  // (the folds finish runs of any length: no status to read back)
         if (p2p(G, ops) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     }
     // lib.rs:564-573: global[i] += batch_sum[i] in batch order, then x 1f32/n

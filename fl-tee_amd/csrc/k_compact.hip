@@ -596,13 +596,24 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 // with the first G compaction levels.  The fold needs, per position p < L, only what
 // the compaction reads: whether p is its run's representative (the run's last
 // position: idx[p+1] != idx[p], or p = L-1) with idx < d, and then the run's sum —
-// v_head, (v_head + v_next), ... left to right, the enclave's order.  Every run head
-// in the window walks its run in LDS and leaves the sum in the val of the run's last
-// record; a run of more than halo + 1 entries (positions p and p - halo - 1 in one run,
-// the window reaching that far back) is reported as FLTEE_DEV_ERR_FOLD_OVERFLOW like
-// the fold kernel (fold_run_limit), and the caller rejects the call.  The folded array (1 GB at C5) is
-// never written and read back.  Dummies and non-representatives are never selected by
-// the compaction, so their contents do not matter.
+// v_head, (v_head + v_next), ... left to right, the enclave's order.  Each lane walks
+// back lim = halo + 1 slots from its own and forward through them (FLTEE_FC_FIXED_WALK
+// below), so every run of <= lim entries gets the enclave's sum bit for bit.  The folded
+// array (1 GB at C5) is never written and read back.  Dummies and non-representatives are
+// never selected by the compaction, so their contents do not matter.
+//
+// Runs of any length (round 6; a client repeated an index).  A run that began before a
+// lane's walk start is finished with a re-associated sum: every lane folds its own slots
+// again (the run partials from its first slot), the block scans the lanes' segmented
+// aggregates (FoldAgg: first key, last key, one key throughout, the partial of the run
+// ending the range), and the carry from in front of the window comes from the tiles
+// before by a decoupled look-back: each tile publishes the aggregate of its piece (window
+// slots [0, S) — the pieces of consecutive tiles tile the array) as soon as its walk is
+// done, then its inclusive prefix; wave 0 reads 64 predecessors at a time back to the
+// nearest inclusive one.  Every tile runs the same steps whatever the data (the waits
+// depend on the other tiles' progress only), and the grid never exceeds the blocks that
+// fit on the chip at once (a tile only waits for tiles of lower index, already running),
+// with a bounded wait that reports FLTEE_DEV_ERR_LAUNCH instead of hanging.
 // Resident blocks per CU of the fused first pass, and whether a block prefetches its next
 // window during the fold.  Round 3 (A/B in one process, `profiles/r03/ab/ab18_fold_blocks_*`):
 // three blocks (6 waves per SIMD, <= 85 VGPRs) without the prefetch — the other resident
@@ -615,35 +626,19 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #ifndef FLTEE_FC_PF
 #define FLTEE_FC_PF 0
 #endif
-// Round 5, measured and not kept (FLTEE_FC_PER16=1): 8,192-record windows (1,024 lanes x
-// 8, one block per CU: 16 waves, <= 128 VGPRs) for the wide-halo arrays (C5: Hr = 1,008
-// against 4,096 records per tile — the window re-read 1.42x the records it compacts, 2.14
-// GB of PMC traffic against 1.76 GB launch-side), the halo and the H = 511 overlap rows
-// then costing 1.2x: 1,356-1,358 vs 1,097-1,098 us per pass (A/B in one process,
-// `profiles/r05/ab/ab3_fold_window8192_c5_rejected.jsonl`) — one 1,024-lane block per CU
-// has too few waves to hide the window load that three 512-lane blocks hide.  (512 lanes
-// x 16 at two blocks per CU spills: 112 B of scratch.)
-#ifndef FLTEE_FC_PER16
-#define FLTEE_FC_PER16 0
-#endif
-// FLTEE_FC_FIXED_WALK (round 5): the fold's lane walks have a trip count fixed by the
-// public sizes, instead of stopping at the end of the lane's last run, whose position
-// follows the data (the run lengths: how many clients sent each index).  1: every lane
-// walks its slots plus lim (the longest legal run, n + 1) forward from its heads with
-// selects and conditional stores; 2 (default): every lane walks back lim slots and forward
-// through its own, branch-free, and stores its own slots' sums after a barrier.  That walk grows with n, so
-// the fused kernel takes it only up to kFixedWalkMax; longer runs go to the streaming
-// fold (fixed Hr + C + 16 steps per lane) + the compaction.  A/B (`profiles/r05/ab/ab9_*`,
-// `ab10_*`, with cp_pick form 3): C3 (lim 101) 0.147 vs 0.135 ms with the data-dependent
-// walk; C5 (lim 1,001) through the streaming fold 12.33 vs 12.07 ms — the fused fixed
-// walk there took 11.4 ms alone.
-#ifndef FLTEE_FC_FIXED_WALK
-#define FLTEE_FC_FIXED_WALK 2
-#endif
-// (Round 5, measured and not kept: the walk's dependent chain as rounds of carries between
-// lanes — each lane folds its own slots onto the last sum of the lane before, ceil(lim /
-// chunk) rounds through LDS — C3 0.136-0.139 vs 0.136 ms, bit-identical,
-// `profiles/r05/ab/ab15_*`.)
+// Round 5, measured and not kept: 8,192-record windows (1,024 lanes x 8, one block per CU)
+// for the wide-halo arrays — one 1,024-lane block per CU has too few waves to hide the
+// window load that three 512-lane blocks hide (`profiles/r05/ab/ab3_fold_window8192_c5_
+// rejected.jsonl`: 1,356-1,358 vs 1,097-1,098 us per pass at C5).
+// The fold's lane walks have a trip count fixed by the public sizes (round 5): every lane
+// walks back lim slots and forward through its own, branch-free, and stores its own slots'
+// sums after a barrier.  That walk grows with n, so the fused kernel takes it only up to
+// kFixedWalkMax; longer runs go to the streaming fold (fixed Hr + C + 16 steps per lane) +
+// the compaction.  (Round 5 A/B, `profiles/r05/ab/ab9_*`, `ab10_*`: C3 (lim 101) 0.147 vs
+// 0.135 ms against a data-dependent walk; C5 (lim 1,001) through the streaming fold 12.33
+// vs 12.07 ms — the fused fixed walk there took 11.4 ms alone.  Also measured and not kept:
+// the walk's dependent chain as rounds of carries between lanes, C3 0.136-0.139 vs 0.136
+// ms, `profiles/r05/ab/ab15_*`.)
 // The fixed walk's bound: lim <= 128 at any size, <= 320 on arrays of <= 2^20 records,
 // where the streaming fold's launch and latency cost more than the longer walk (MLP-MNIST
 // n = 300, lim 301: 0.101 vs 0.138 ms, `profiles/r05/ab/ab12_*`); 320 keeps three windows
@@ -656,10 +651,82 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #endif
 constexpr uint32_t kFixedWalkMax = FLTEE_FC_WALK_MAX;
 constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
-// form 2's LDS read-ahead depth (1: the next slot only)
-#ifndef FLTEE_FC_RA
-#define FLTEE_FC_RA 1
-#endif
+// the bounded look-back wait: polls of ~0.25 us (about a quarter second in all)
+constexpr uint32_t kFcSpinMax = 1u << 20;
+
+// one tile's look-back slot: its piece aggregate, its inclusive prefix, and the flag
+// (epoch << 2 | 1: aggregate published, | 2: inclusive published)
+struct FcLb {
+    FoldAgg agg, inc;
+    uint32_t flag, pad[3];
+};
+
+__device__ __forceinline__ FoldAgg fa_shfl_up(const FoldAgg &x, int o) {
+    FoldAgg r;
+    r.F = (uint32_t)__shfl_up((int)x.F, o);
+    r.K = (uint32_t)__shfl_up((int)x.K, o);
+    r.Q = __shfl_up(x.Q, o);
+    r.fl = (uint32_t)__shfl_up((int)x.fl, o);
+    return r;
+}
+__device__ __forceinline__ FoldAgg fa_shfl_down(const FoldAgg &x, int o) {
+    FoldAgg r;
+    r.F = (uint32_t)__shfl_down((int)x.F, o);
+    r.K = (uint32_t)__shfl_down((int)x.K, o);
+    r.Q = __shfl_down(x.Q, o);
+    r.fl = (uint32_t)__shfl_down((int)x.fl, o);
+    return r;
+}
+
+// wave 0 of tile `tile`: the aggregate of every piece before it (decoupled look-back)
+__device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t lane,
+                               uint32_t *status) {
+    FoldAgg run = fa_empty();
+    long long base = (long long)tile - 1;
+    bool done = tile == 0;
+    while (!done) {
+        const long long p = base - (long long)lane;
+        uint32_t st = 2;  // before position 0: nothing (an empty inclusive prefix)
+        bool got = false;
+        if (p >= 0) {
+            uint32_t f = __hip_atomic_load(&lb[p].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t it = 0;
+            while ((f >> 2) != epoch && it < kFcSpinMax) {
+                __builtin_amdgcn_s_sleep(8);
+                f = __hip_atomic_load(&lb[p].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                ++it;
+            }
+            if ((f >> 2) != epoch) {
+                atomicOr(status, FLTEE_DEV_ERR_LAUNCH);
+                st = 2;
+            } else {
+                st = f & 3;
+                got = true;
+            }
+        }
+        const uint64_t incl = __ballot(st == 2);
+        const uint32_t first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+        FoldAgg v = fa_empty();
+        if (got && lane < first) v = lb[p].agg;
+        else if (got && lane == first) v = lb[p].inc;
+        // the window's lanes in position order: a higher lane is an older piece
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const FoldAgg older = fa_shfl_down(v, o);
+            if ((lane & (2 * o - 1)) == 0) v = fa_combine(older, v);
+        }
+        FoldAgg w;  // lane 0's: the window in order
+        w.F = (uint32_t)__shfl((int)v.F, 0);
+        w.K = (uint32_t)__shfl((int)v.K, 0);
+        w.Q = __shfl(v.Q, 0);
+        w.fl = (uint32_t)__shfl((int)v.fl, 0);
+        run = fa_combine(w, run);
+        done = first < 64;
+        base -= 64;
+    }
+    return run;
+}
+
 template <int NT, int PER, int FINAL, int XMAX, int BPC = FLTEE_FC_BLOCKS>
 __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fold_compact_first(const uint64_t *__restrict__ A,
                                                             uint64_t *__restrict__ dst, uint32_t L,
@@ -667,12 +734,18 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                                                             uint32_t S, uint32_t Hr,
                                                             uint32_t ntiles, float coef,
                                                             float *__restrict__ out,
-                                                            uint32_t lim, uint32_t *status) {
+                                                            uint32_t lim, FcLb *lb, uint32_t epoch,
+                                                            uint32_t *status) {
     constexpr uint32_t CAP = (uint32_t)NT * PER;
+    constexpr int CH = PER + XMAX;  // the most window slots one lane owns
+    constexpr int NW = NT / 64;
     // XMAX: window slots beyond CAP per lane, ceil((Hr + 1) / NT)
-    extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1
+    extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1, then the sums
+    __shared__ FoldAgg wtot[NW];
+    __shared__ float red[NW];
+    __shared__ FoldAgg wc_s;
     const uint32_t H = (1u << G) - 1;
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t Wn = Hr + CAP + 1;
     const uint32_t chunk = (Wn + NT - 1) / NT;
     const __amdgpu_buffer_rsrc_t rs =
@@ -705,15 +778,32 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         const uint32_t next = tile + gridDim.x;
         if (FLTEE_FC_PF && (!FLTEE_CP_SKIP_SELF || next < ntiles))
             prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
-        if constexpr (FLTEE_FC_FIXED_WALK == 2) {
-            // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
-            // in-order sum of its run up to that slot: a walk from x0 - lim (every legal run
-            // of an owned slot starts after it), lim + chunk steps whatever the data, no
-            // branch, the next slot's LDS read issued a step ahead.  The sums go to their own
-            // LDS array (sums[], after the window), so no lane overwrites what another still
-            // reads; a run's last slot then holds the run's sum — all the compaction reads.
-            float *sums = reinterpret_cast<float *>(win + Wn);
-            const int x0 = (int)(t * chunk), ys = x0 - (int)lim;
+        // the tile's piece (window slots [0, S)): the run ending it, its values summed in
+        // any order (a carry is re-associated anyway)
+        {
+            const uint32_t kS = (uint32_t)win[S - 1];
+            float qp = 0.0f;
+#pragma unroll
+            for (uint32_t i = 0; i < PER; ++i) {
+                const uint32_t y = t + i * NT;
+                if (y < S) {
+                    const uint64_t r = win[y];
+                    qp = (uint32_t)r == kS ? __fadd_rn(qp, rec_val(r)) : qp;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) qp = __fadd_rn(qp, __shfl_down(qp, o));
+            if (lane == 0) red[wave] = qp;
+        }
+        // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
+        // in-order sum of its run up to that slot: a walk from x0 - lim (every run of <= lim
+        // entries of an owned slot starts after it), lim + chunk steps whatever the data, no
+        // branch, the next slot's LDS read issued a step ahead.  The sums go to their own
+        // LDS array (sums[], after the window), so no lane overwrites what another still
+        // reads; a run's last slot then holds the run's sum — all the compaction reads.
+        float *sums = reinterpret_cast<float *>(win + Wn);
+        const int x0 = (int)(t * chunk), ys = x0 - (int)lim;
+        {
             const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
             auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
             uint32_t prevk = 0xFFFFFFFFu;
@@ -730,120 +820,127 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 prevk = ky;
                 have = valid;
             };
-            if constexpr (FLTEE_FC_RA > 1) {
-                // one loop of lim + chunk steps (the same count in every lane), FLTEE_FC_RA
-                // LDS reads in flight ahead of the step that uses them
-                const uint32_t T = lim + chunk;
-                uint64_t ring[FLTEE_FC_RA];
-#pragma unroll
-                for (int k = 0; k < FLTEE_FC_RA; ++k) ring[k] = rd(ys + k);
-                for (uint32_t s0 = 0; s0 < T; s0 += FLTEE_FC_RA) {
-#pragma unroll
-                    for (int k = 0; k < FLTEE_FC_RA; ++k) {
-                        const uint32_t q = s0 + (uint32_t)k;
-                        const uint64_t r = ring[k];
-                        ring[k] = rd(ys + (int)q + FLTEE_FC_RA);
-                        if (q < T) {
-                            const int y = ys + (int)q;
-                            step(r, y);
-                            if (q >= lim && y < (int)Wn) sums[y] = acc;
-                        }
-                    }
-                }
-            } else {
-                uint64_t rn = rd(ys);
-                for (uint32_t q = 0; q < lim; ++q) {  // the same trip count in every lane
-                    const uint64_t r = rn;
-                    rn = rd(ys + (int)q + 1);
-                    step(r, ys + (int)q);
-                }
-                for (uint32_t i = 0; i < chunk; ++i) {
-                    const int y = x0 + (int)i;
-                    const uint64_t r = rn;
-                    rn = rd(y + 1);
-                    step(r, y);
-                    if (y < (int)Wn) sums[y] = acc;
-                }
-            }
-        } else
-        // Each lane owns window slots [x0, x1) and folds the runs whose heads lie there,
-        // left to right: one loop that goes past x1 only to finish its last run, so a
-        // wave's trip count is about chunk + the longest run (a loop per head nested in
-        // a loop over the slots cost chunk x the longest run).  The sum lands in the
-        // val of the run's last slot; idx words are never rewritten, so the head tests
-        // of the neighbouring lanes read the same keys whatever the order of the writes.
-        {
-            const uint32_t x0 = t * chunk, x1 = min(x0 + chunk, Wn);
-            const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
-            uint32_t prevk = x0 > 0 ? (uint32_t)win[x0 - 1] : 0u;
-            bool run = false;
-            float acc = 0.0f;
-            uint32_t k = 0;
-            uint64_t rn = win[x0 < Wn ? x0 : Wn - 1];
-            // FLTEE_FC_FIXED_WALK: every lane walks exactly to x1 + lim (lim = the longest
-            // legal run, public), so the loop's trip count no longer follows the data
-            const uint32_t yend = FLTEE_FC_FIXED_WALK ? min(x1 + lim, Wn) : Wn;
-            for (uint32_t y = x0; y < yend; ++y) {
-                const int p = pw + (int)y;
-                const bool valid = p >= 0 && p < (int)L;
+            uint64_t rn = rd(ys);
+            for (uint32_t q = 0; q < lim; ++q) {  // the same trip count in every lane
                 const uint64_t r = rn;
-                rn = win[y + 1 < Wn ? y + 1 : y];  // read ahead: the LDS latency overlaps this slot
-                const uint32_t ky = (uint32_t)r;
-                const bool head = y == 0 || p == 0 || ky != prevk;
-                prevk = ky;
-                if (FLTEE_FC_FIXED_WALK) {
-                    const bool ext = valid && !head;
-                    const float sum = __fadd_rn(acc, rec_val(r));
-                    if (run && !ext) win[y - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;
-                    acc = run && ext ? sum : acc;
-                    run = run && ext;
-                    const bool start = y < x1 && valid && head;
-                    acc = start ? rec_val(r) : acc;
-                    k = start ? ky : k;
-                    run = run || start;
-                    continue;
-                }
-                if (run) {
-                    if (valid && !head) {
-                        acc = __fadd_rn(acc, rec_val(r));
-                        continue;
-                    }
-                    win[y - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;  // ended at y - 1
-                    run = false;
-                }
-                if (y >= x1) break;
-                if (valid && head) {
-                    run = true;
-                    acc = rec_val(r);
-                    k = ky;
-                }
+                rn = rd(ys + (int)q + 1);
+                step(r, ys + (int)q);
             }
-            // a run still open at the window's end ends there only if position L follows
-            if (run && pw + (long long)Wn >= (long long)L)
-                win[Wn - 1] = ((uint64_t)__float_as_uint(acc) << 32) | k;
+            for (uint32_t i = 0; i < chunk; ++i) {
+                const int y = x0 + (int)i;
+                const uint64_t r = rn;
+                rn = rd(y + 1);
+                step(r, y);
+                if (y < (int)Wn) sums[y] = acc;
+            }
         }
         __syncthreads();
-        // representatives with idx < d -> (c = p - idx, sum); the rest never move.  And the
-        // run-length test (fold_run_limit): positions p and p - lim in one run (runs are
-        // contiguous) = a run of more than lim entries; the window holds p - lim (Hr >= lim).
-        // (Measured against the test in the fold loop — a run's length at its end, plus the
-        // tile-start test for heads before the window: C5 1,150 vs 1,099 us per pass.)
-        uint64_t v[PER];
-        bool over = false;
+        if (t == 0) {  // publish the piece's aggregate
+            float q = 0.0f;
 #pragma unroll
-        for (uint32_t i = 0; i < PER; ++i) {
-            const uint32_t f = t + i * NT, x = f + Hr;
-            const long long p = a + f;
-            const uint64_t r = win[x];
-            const uint32_t idx = (uint32_t)r;
-            over |= f < S && p < (long long)L && p >= (long long)lim && (uint32_t)win[x - lim] == idx;
-            const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-            const uint64_t hi = FLTEE_FC_FIXED_WALK == 2
-                                    ? (uint64_t)__float_as_uint(reinterpret_cast<const float *>(win + Wn)[x]) << 32
-                                    : (r & 0xFFFFFFFF00000000ull);
-            v[i] = (p < (long long)L && idx < d && end) ? (hi | (uint32_t)((uint32_t)p - idx)) : CP_DUMMY;
+            for (int w = 0; w < NW; ++w) q = __fadd_rn(q, red[w]);
+            FoldAgg g;
+            g.F = (uint32_t)win[0];
+            g.K = (uint32_t)win[S - 1];
+            g.Q = q;
+            g.fl = kFsPiece | (g.F == g.K ? kFsFull : 0u);
+            lb[tile].agg = g;
+            __hip_atomic_store(&lb[tile].flag, (epoch << 2) | 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (over) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+        // the lane's own slots again: the aggregate of their run partials from x0
+        FoldAgg ca = fa_empty();
+        const uint32_t k0 = x0 < (int)Wn ? (uint32_t)win[x0] : 0u;
+        {
+            uint32_t pk = k0;
+            float acc = 0.0f;
+            bool unb = true;
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int y = x0 + i;
+                if ((uint32_t)i < chunk && y < (int)Wn) {
+                    const uint64_t r = win[y];
+                    const uint32_t ky = (uint32_t)r;
+                    const bool cont = i > 0 && ky == pk;
+                    acc = cont ? __fadd_rn(acc, rec_val(r)) : rec_val(r);
+                    unb = unb && (i == 0 || cont);
+                    pk = ky;
+                }
+            }
+            if (x0 < (int)Wn) {
+                ca.F = k0;
+                ca.K = pk;
+                ca.Q = acc;
+                ca.fl = kFsPiece | (unb ? kFsFull : 0u);
+            }
+        }
+        FoldAgg inc = ca;  // the wave's inclusive scan (lane order = position order)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const FoldAgg y = fa_shfl_up(inc, o);
+            if (lane >= (uint32_t)o) inc = fa_combine(y, inc);
+        }
+        FoldAgg wex = fa_shfl_up(inc, 1);
+        if (lane == 0) wex = fa_empty();
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        if (wave == 0) {  // the carry from in front of the window
+            const FoldAgg wc = fc_lookback(lb, tile, epoch, lane, status);
+            if (lane == 0) {
+                wc_s = wc;
+                lb[tile].inc = fa_combine(wc, lb[tile].agg);
+                __hip_atomic_store(&lb[tile].flag, (epoch << 2) | 2u, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        {  // the window-local run prefix of every owned slot, into the slot's val
+            FoldAgg ex = fa_empty();
+            for (uint32_t w = 0; w < wave; ++w) ex = fa_combine(ex, wtot[w]);
+            ex = fa_combine(ex, wex);
+            const bool ec = (ex.fl & kFsPiece) && ex.K == k0;
+            // the key in front of this lane's walk: a run holding it began before the walk
+            // (more than lim entries) and takes the window-local prefix, else the walk's sum
+            const uint32_t kys = ys > 0 ? (uint32_t)win[ys - 1] : 0u;
+            uint32_t pk = k0;
+            float acc = 0.0f;
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const int y = x0 + i;
+                if ((uint32_t)i < chunk && y < (int)Wn) {
+                    const uint64_t r = win[y];
+                    const uint32_t ky = (uint32_t)r;
+                    acc = (i > 0 && ky == pk) ? __fadd_rn(acc, rec_val(r)) : rec_val(r);
+                    pk = ky;
+                    const float wl = (ec && ky == k0) ? __fadd_rn(ex.Q, acc) : acc;
+                    const float v = (ys > 0 && kys == ky) ? wl : sums[y];
+                    win[y] = ((uint64_t)__float_as_uint(v) << 32) | ky;
+                }
+            }
+        }
+        __syncthreads();
+        // representatives with idx < d -> (c = p - idx, sum); the rest never move.  A slot
+        // holds its run's sum from the window's start on (the walk's, bit for bit, or the
+        // re-associated window-local prefix for a run longer than its walk); a run begun
+        // before the window adds the carry.
+        uint64_t v[PER];
+        {
+            const FoldAgg wc = wc_s;
+            const uint32_t kw0 = (uint32_t)win[0];
+            const bool wok = (wc.fl & kFsPiece) && wc.K == kw0;
+#pragma unroll
+            for (uint32_t i = 0; i < PER; ++i) {
+                const uint32_t f = t + i * NT, x = f + Hr;
+                const long long p = a + f;
+                const uint64_t r = win[x];
+                const uint32_t idx = (uint32_t)r;
+                const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
+                const float wv = rec_val(r);
+                const float hv = (wok && idx == kw0) ? __fadd_rn(wc.Q, wv) : wv;
+                v[i] = (p < (long long)L && idx < d && end)
+                           ? (((uint64_t)__float_as_uint(hv) << 32) | (uint32_t)((uint32_t)p - idx))
+                           : CP_DUMMY;
+            }
+        }
         __syncthreads();
         uint64_t *sm = win;
 #pragma unroll
@@ -863,12 +960,12 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             const uint32_t stepf = 1u << g;
             const bool two = FLTEE_CP_TWO && g + 1 < G;
             const uint32_t gl = two ? g + 1 : g;
-            const uint32_t lim = S + H - ((2u << gl) - 1);
+            const uint32_t lmt = S + H - ((2u << gl) - 1);
             if (two) {
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
                     const uint32_t f = t + i * NT;
-                    if (f < lim) {
+                    if (f < lmt) {
                         const uint64_t y0 = cp_pick(sm[f], sm[f + stepf], g);
                         const uint64_t y2 = cp_pick(sm[f + 2 * stepf], sm[f + 3 * stepf], g);
                         nv[i] = cp_pick(y0, y2, g + 1);
@@ -878,14 +975,14 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
 #pragma unroll
                 for (uint32_t i = 0; i < PER; ++i) {
                     const uint32_t f = t + i * NT;
-                    if (f < lim) nv[i] = cp_pick(sm[f], sm[f + stepf], g);
+                    if (f < lmt) nv[i] = cp_pick(sm[f], sm[f + stepf], g);
                 }
             }
             __syncthreads();
 #pragma unroll
             for (uint32_t i = 0; i < PER; ++i) {
                 const uint32_t f = t + i * NT;
-                if (f < lim) sm[f] = nv[i];
+                if (f < lmt) sm[f] = nv[i];
             }
             __syncthreads();
             g += two ? 2 : 1;
@@ -915,45 +1012,63 @@ void set_fold_compact(int on) { g_fold_compact = on != 0; }
 // The fold (fold_len == L) + the compaction of `advanced`: sorted array A (M records,
 // [0, L) meaningful) -> out.  A and B are clobbered.  hipErrorNotSupported: not fused
 // here (halo wide against the 4096-record tile, or no levels): the caller folds separately.
+// lb: fc_lookback_bytes() of look-back slots, zeroed when allocated; *epoch: this
+// device's launch counter (the slots of earlier launches never match a later epoch).
 template <int PER, int F, int X>
-static hipError_t fc_launch(unsigned grid, size_t lds, hipStream_t s, const uint64_t *A, uint64_t *B,
+static hipError_t fc_launch(uint64_t ntiles, size_t lds, hipStream_t s, const uint64_t *A, uint64_t *B,
                             size_t L, size_t M, size_t d, uint32_t G, uint32_t S, size_t Hr,
-                            uint64_t ntiles, float coef, float *out, uint32_t lim, uint32_t *status) {
-    // PER 16 stands for the 8,192-record window: 1,024 lanes x 8, one block per CU
-    constexpr int NT = PER > 8 ? 1024 : 512;
-    constexpr int BPC = PER > 8 ? 1 : FLTEE_FC_BLOCKS;
-    constexpr int PL = PER > 8 ? 8 : PER;
-    static bool attr = false;  // 26-74 KB of window
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)fold_compact_first<NT, PL, F, X, BPC>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        attr = true;
+                            float coef, float *out, uint32_t lim, FcLb *lb, uint32_t epoch,
+                            uint32_t *status) {
+    constexpr int NT = 512;
+    constexpr int BPC = FLTEE_FC_BLOCKS;
+    auto kern = fold_compact_first<NT, PER, F, X, BPC>;
+    // the grid never exceeds the blocks resident at once (the look-back waits for tiles of
+    // lower index only: they are running), whatever the occupancy turns out to be
+    static int resident = 0;
+    static size_t res_lds = 0;
+    if (!resident || res_lds != lds) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  80 * 1024);
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kern, NT, lds) !=
+                hipSuccess)
+            return hipErrorLaunchFailure;
+        if (per_cu > BPC) per_cu = BPC;
+        resident = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+        res_lds = lds;
     }
-    hipLaunchKernelGGL((fold_compact_first<NT, PL, F, X, BPC>), dim3(grid), dim3(NT), lds, s, A, B,
-                       (uint32_t)L, (uint32_t)M, (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles,
-                       coef, out, lim, status);
+    const unsigned grid = (unsigned)(ntiles < (uint64_t)resident ? ntiles : (uint64_t)resident);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, s, A, B, (uint32_t)L, (uint32_t)M,
+                       (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles, coef, out, lim, lb, epoch,
+                       status);
     return hipGetLastError();
 }
 
 template <int PER>
-static hipError_t fc_dispatch(int F, bool x1, unsigned grid, size_t lds, hipStream_t s,
+static hipError_t fc_dispatch(int F, bool x1, uint64_t ntiles, size_t lds, hipStream_t s,
                               const uint64_t *A, uint64_t *B, size_t L, size_t M, size_t d,
-                              uint32_t G, uint32_t S, size_t Hr, uint64_t ntiles, float coef,
-                              float *out, uint32_t lim, uint32_t *status) {
-#define FC_ARGS grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status
+                              uint32_t G, uint32_t S, size_t Hr, float coef, float *out,
+                              uint32_t lim, FcLb *lb, uint32_t epoch, uint32_t *status) {
+#define FC_ARGS ntiles, lds, s, A, B, L, M, d, G, S, Hr, coef, out, lim, lb, epoch, status
     if (F == 0) return x1 ? fc_launch<PER, 0, 1>(FC_ARGS) : fc_launch<PER, 0, 2>(FC_ARGS);
     if (F == 2) return x1 ? fc_launch<PER, 2, 1>(FC_ARGS) : fc_launch<PER, 2, 2>(FC_ARGS);
     return x1 ? fc_launch<PER, 1, 1>(FC_ARGS) : fc_launch<PER, 1, 2>(FC_ARGS);
 #undef FC_ARGS
 }
 
-hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
-                                       size_t halo, float coef, float *out, bool accumulate,
-                                       uint32_t *status, hipStream_t s) {
+// the fused pass's tile geometry for this shape (false: not fused)
+struct FcShape {
+    uint32_t per, G, S, lim;
+    size_t Hr, ntiles;
+};
+static bool fc_shape(size_t M, size_t L, size_t d, size_t halo, FcShape &o) {
     constexpr uint32_t NT = 512;
-    // the window reaches lim = halo + 1 records back for the run-length test
-    const size_t Hr = fold_context(halo + 1);
-    const uint32_t lim = fold_run_limit(halo);
+    // the window reaches lim = halo + 1 records back: every run of <= halo + 1 entries
+    // (each client's indices distinct) folds bit for bit
+    o.Hr = fold_context(halo + 1);
+    o.lim = halo + 1 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(halo + 1);
     // A/B in one process (scripts/ab_fold_compact.py, profiles/r02/ab/fold_compact.jsonl):
     // C3 (Hr = 112): 0.211 vs 0.214 ms with the separate fold; C5 (Hr = 1008, windows 25 %
     // wider than the tile): 17.66 vs 17.48 ms in round 2, when it stayed separate; round 3
@@ -964,48 +1079,64 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     // and again in round 4 with the 16-B slot pairs: 414-418 us either way,
     // `profiles/r04/ab/ab15_compact_swizzle_v2_rejected.jsonl`; 64 KiB tiles, 3 passes of 6
     // levels, as slow as 4 of 5, `ab11_*`.)
-    if (!g_fold_compact || d == 0 || L <= d || Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
-        return hipErrorNotSupported;
-    if (FLTEE_FC_FIXED_WALK && lim > kFixedWalkMax &&
-        !(lim <= kFixedWalkMaxSmall && M <= ((size_t)1 << 20)))
-        return hipErrorNotSupported;  // the streaming fold
+    if (!g_fold_compact || d == 0 || L <= d || o.Hr + 1 > 2 * 512 || M >= ((size_t)1 << 29) || L > M)
+        return false;
+    if (o.lim > kFixedWalkMax && !(o.lim <= kFixedWalkMaxSmall && M <= ((size_t)1 << 20)))
+        return false;  // the streaming fold
     const uint32_t nlev = bitlen(L - d);
-    const uint32_t G = nlev < 9 ? nlev : 9, H = (1u << G) - 1;
+    o.G = nlev < 9 ? nlev : 9;
+    const uint32_t H = (1u << o.G) - 1;
     // records per lane: the fewest (4, 6 or 8) that still leave at most one tile per CU —
     // each lane's walk and levels are the critical path, the window re-read is cheap
-    uint32_t per = 8;
+    o.per = 8;
     for (uint32_t p : {4u, 6u}) {
         if (NT * p <= 2 * H) continue;  // the halo rows would swamp the tile
         if ((L + NT * p - H - 1) / (NT * p - H) <= 256) {
-            per = p;
+            o.per = p;
             break;
         }
     }
-    // a wide halo (two window slots per lane) on an array of >= 2 tiles per block slot:
-    // 8,192-record windows, two blocks per CU (see fold_compact_first)
-    if (FLTEE_FC_PER16 && per == 8 && Hr + 1 > NT && (L + NT * 16 - H - 1) / (NT * 16 - H) >= 2 * 512)
-        per = 16;
-    const uint32_t bpc = per > 8 ? 1u : (uint32_t)FLTEE_FC_BLOCKS;
-    const uint32_t CAP = NT * per, S = CAP - H;  // (per 16: 1,024 lanes x 8)
-    const uint64_t ntiles = (L + S - 1) / S;
-    const bool last = G == nlev;
-    const unsigned grid = (unsigned)(ntiles < 256u * bpc ? ntiles : 256u * bpc);
-    // the window, and (fixed walk, form 2) the run sums beside it
-    const size_t lds = (Hr + CAP + 1) * 8 + (FLTEE_FC_FIXED_WALK == 2 ? (Hr + CAP + 1) * 4 : 0);
-    // the resident blocks per CU must fit the 160 KiB LDS at the largest window
+    const uint32_t CAP = NT * o.per;
+    o.S = CAP - H;
+    o.ntiles = (L + o.S - 1) / o.S;
+    // the window and the run sums beside it; the resident blocks per CU must fit the
+    // 160 KiB LDS at the largest window
+    const size_t lds = (o.Hr + CAP + 1) * 12;
     static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
-    static_assert((1023 + 8 * 1024 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU (8,192 records)");
-    if (lds * bpc > 160 * 1024) return hipErrorNotSupported;
+    return lds * FLTEE_FC_BLOCKS <= 160 * 1024;
+}
+
+size_t fc_lookback_bytes(size_t M, size_t L, size_t d, size_t halo) {
+    FcShape o;
+    return fc_shape(M, L, d, halo, o) ? o.ntiles * sizeof(FcLb) : 0;
+}
+
+hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_t L, size_t d,
+                                       size_t halo, float coef, float *out, bool accumulate,
+                                       uint32_t *status, hipStream_t s, void *lb, size_t lb_cap,
+                                       uint32_t *epoch) {
+    constexpr uint32_t NT = 512;
+    FcShape o;
+    if (!fc_shape(M, L, d, halo, o)) return hipErrorNotSupported;
+    if (!lb || lb_cap < o.ntiles * sizeof(FcLb) || !epoch) return hipErrorInvalidValue;
+    if (++*epoch >= (1u << 30)) return hipErrorInvalidValue;  // the caller re-zeroes the slots
+    const uint32_t nlev = bitlen(L - d);
+    const uint32_t CAP = NT * o.per;
+    const bool last = o.G == nlev;
+    const size_t lds = (o.Hr + CAP + 1) * 12;
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
-    const bool x1 = Hr + 1 <= (per > 8 ? 1024u : NT);  // one window slot past CAP per lane, else two
+    const bool x1 = o.Hr + 1 <= NT;  // one window slot past CAP per lane, else two
     const int F = !last ? 0 : (accumulate ? 2 : 1);
+    FcLb *l = (FcLb *)lb;
     hipError_t e;
-    if (per == 4) e = fc_dispatch<4>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
-    else if (per == 6) e = fc_dispatch<6>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
-    else if (per == 8) e = fc_dispatch<8>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
-    else e = fc_dispatch<16>(F, x1, grid, lds, s, A, B, L, M, d, G, S, Hr, ntiles, coef, out, lim, status);
+#define FC_GO(P_) fc_dispatch<P_>(F, x1, o.ntiles, lds, s, A, B, L, M, d, o.G, o.S, o.Hr, coef, out, \
+                                  o.lim, l, *epoch, status)
+    if (o.per == 4) e = FC_GO(4);
+    else if (o.per == 6) e = FC_GO(6);
+    else e = FC_GO(8);
+#undef FC_GO
     if (e != hipSuccess || last) return e;
-    return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, G);
+    return compact_levels(B, A, L, d, L - d, coef, out, accumulate, s, o.G);
 }
 
 // ------------------------------------------------ one range of the array ---

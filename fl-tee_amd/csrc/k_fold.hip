@@ -16,10 +16,22 @@
 // it (the halo): whenever the run crossing the chunk start began inside the
 // halo, the carry entering the chunk is bit-identical to the enclave's.  With
 // each client's indices distinct (top-k, utils.py:327-354) a run holds at most
-// n+1 records, so H = n.  A lane whose carry could be wrong (key[a-Hr-1] ==
-// key[a-1] == key[a]) reports FLTEE_DEV_ERR_FOLD_OVERFLOW and the host re-runs
-// with a larger halo.  Every lane performs the same Hr+C+16 steps whatever the
+// n+1 records, so H = n.  Every lane performs the same Hr+C+16 steps whatever the
 // data (oblivious).
+//
+// Runs of any length (round 6).  A run that began before a lane's walk start b (a
+// client repeated an index: more than Hr + 1 entries) ends in that lane's chunk with a
+// sum missing its part before b.  The lane emits a dummy at that run end instead and
+// leaves a side record (FoldSide): the run's key and its sum over [b, end], and — for
+// every lane — the aggregate of its piece [b, b + C) (first key, last key, one key or
+// not, and the in-order partial of the run ending the piece).  The walk starts are C
+// apart, so the pieces tile the array.  fold_patch_kernel then scans the pieces
+// (segmented: a run's partials add up only while the key goes on) and writes, at every
+// lane's first position a (a fixed address, whatever the data), either what the fold
+// left there or — for a lane with such a run — (key, carry + sum): a inside that run,
+// the one record of its key.  Exact (bit for bit) for every run inside one lane's walk,
+// the enclave's sum re-associated at the walk boundaries otherwise (north_star's 1e-6
+// relative tolerance for the aggregate).  No run-length limit, no rerun.
 //
 // Layout: C >= Hr on large arrays (halo work <= 2x; small arrays take shorter
 // chunks, down to 16, to keep ~1024 waves in flight), so a lane walks a long chunk; the 64
@@ -75,33 +87,35 @@ __device__ __forceinline__ void wave_sync_lds() {
 // up to `end`.  Positions are local to src/dst (length m); pbase + position is the
 // global position, which decides fold_len and the dummies' idx.  Range mode (one
 // GPU's part of a position-sharded array, SURVEY §8e Option B): [0, origin) holds
-// >= Hr records of context from the previous range, and src[end] is the next
+// >= Hr + 1 records of context from the previous range, and src[end] is the next
 // range's first record (or end + pbase >= fold_len).
 // CEMIT (round 5): emit what the compaction's first pass would make of the folded array
 // — a run's last record as (sum, c = p - idx) when idx < dsel, every other position as the
 // compaction's unselected slot `cdummy` — so that pass needs no conversion (and may move
 // 16-B slot pairs); positions past fold_len are copied as before.
+// side (nullptr: the one-lane walk, which has no boundary): the lane's FoldSide record.
 template <int DEPTH, bool CEMIT = false>
 __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restrict__ src,
                                                          uint64_t *__restrict__ dst, long long m,
                                                          long long origin, long long end,
                                                          long long pbase, long long fold_len,
-                                                         uint32_t Hr, uint32_t C, uint32_t lim,
-                                                         uint32_t *status, uint32_t dsel = 0,
-                                                         uint64_t cdummy = 0) {
+                                                         uint32_t Hr, uint32_t C,
+                                                         FoldSide *__restrict__ side,
+                                                         uint32_t dsel = 0, uint64_t cdummy = 0) {
     __shared__ uint64_t win[2][64 * FS_ROW];
     const uint32_t l = threadIdx.x;
     const long long wave0 = origin + (long long)blockIdx.x * 64 * C;  // first position of lane 0
     const long long a = wave0 + (long long)l * C;
+    const long long b = a - (long long)Hr;  // the walk's first position (the piece start)
     const uint32_t nstage = (Hr + C + FS_W) / FS_W;
     const uint32_t hw = Hr / FS_W;  // stage s holds window u = s - hw of the chunk
 
-    // carry check (see header): only the first owned position consumes the carry
-    if (a < end && a + pbase < fold_len && a - (long long)Hr - 1 >= 0 &&
-        a + pbase - (long long)Hr - 1 >= 0) {
-        const uint32_t k1 = rec_idx(src[a - 1]);
-        if (rec_idx(src[a - Hr - 1]) == k1 && rec_idx(src[a]) == k1)
-            atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+    // the key in front of the walk: does the run at b begin before it?
+    bool hasprev = false;
+    uint32_t kprev = 0;
+    if (side && a < end && b - 1 >= 0 && b - 1 + pbase >= 0) {
+        kprev = rec_idx(src[b - 1]);
+        hasprev = true;
     }
 
     // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
@@ -130,8 +144,10 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     float pre_val = 0.0f;
     bool started = false;
     uint64_t prev = 0;
-    uint32_t cnt = 0;   // entries of the current run seen so far (a lower bound in the halo)
-    bool over = false;  // a run of more than lim entries inside [0, fold_len)
+    // the side record: the piece [b, b + C) and the head run (the one holding b)
+    bool in_head = false, unbroken = true, corr = false, piece = false;
+    uint32_t pf_key = 0, pk = 0, ck = 0;
+    float pq = 0.0f, cs = 0.0f;
     auto stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
         uint64_t *cur = win[s & 1], *old = win[(s + 1) & 1];
 #pragma unroll
@@ -152,26 +168,46 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             const long long qg = q + pbase;
             const uint32_t ci = rec_idx(r[t]);
             const bool eq = started && ci == pre_idx;
+            const bool copy = qg - 1 >= fold_len, dmy = qg < fold_len && eq;
+            // the head run ends at q - 1: inside the chunk it is the one the side record
+            // carries (emitted as a dummy here, its record written by fold_patch_kernel)
+            const bool hend = in_head && !copy && !dmy;
+            const bool sup = hend && q - 1 >= a && q - 1 < a + (long long)C;
             uint64_t emit;
             if constexpr (CEMIT) {
-                emit = (qg - 1 >= fold_len) ? prev
-                       : (qg < fold_len && eq) || pre_idx >= dsel
+                emit = copy ? prev
+                       : dmy || sup || pre_idx >= dsel
                            ? cdummy
                            : make_rec((uint32_t)(qg - 1) - pre_idx, pre_val);  // (c, sum)
             } else {
-                emit = (qg - 1 >= fold_len) ? prev
-                       : (qg < fold_len && eq) ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
-                                               : make_rec(pre_idx, pre_val);
+                emit = copy ? prev
+                       : dmy || sup ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
+                                    : make_rec(pre_idx, pre_val);
             }
+            if (sup) {
+                corr = true;
+                ck = pre_idx;
+                cs = pre_val;
+            }
+            in_head = in_head && !hend && !copy;
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
             if (q >= 0 && qg >= 0) {
+                if (!started) {  // the walk's first position (b, or 0 at the array's start)
+                    pf_key = ci;
+                    in_head = hasprev && ci == kprev;
+                } else {
+                    unbroken = unbroken && eq;
+                }
                 pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
                 pre_idx = ci;
                 started = true;
-                cnt = eq ? cnt + 1 : 1;
-                // (q < end: a lane past the range streams zero-filled windows it never stores)
-                over |= q < end && qg < fold_len && cnt > lim;
+            }
+            // the piece's last position b + C - 1: its run partial
+            if (t == FS_W - 1 && s == C / FS_W - 1 && started && q >= 0 && qg >= 0) {
+                piece = true;
+                pk = pre_idx;
+                pq = pre_val;
             }
             prev = r[t];
         }
@@ -198,47 +234,27 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         for (int q = 0; q < DEPTH; ++q)
             if (s + (uint32_t)q < nstage) stage(pf[q], s + (uint32_t)q);
     }
-    if (over) atomicOr(status, FLTEE_DEV_ERR_FOLD_OVERFLOW);
+    if (side && a < end) {
+        const uint32_t fl = (piece ? kFsPiece : 0u) | (piece && unbroken ? kFsFull : 0u) |
+                            (corr ? kFsCorr : 0u);
+        FoldSide *o = side + (size_t)blockIdx.x * 64 + l;
+        o->F = pf_key;
+        o->K = pk;
+        o->Q = pq;
+        o->fl = fl;
+        o->ck = ck;
+        o->S = cs;
+    }
 }
 
 size_t fold_context(size_t halo) { return (halo + FS_W - 1) / FS_W * FS_W; }
-uint32_t fold_run_limit(size_t halo) {
-    return halo + 1 >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(halo + 1);
-}
 
 #ifndef FLTEE_FS_DOUBLE_WAVES
 #define FLTEE_FS_DOUBLE_WAVES 1024
 #endif
-hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
-                             size_t end, long long pbase, size_t fold_len, size_t halo,
-                             uint32_t *status, hipStream_t s, size_t cemit_d,
-                             uint64_t cdummy) {
-    const bool cemit = cemit_d != 0;
-    if (cemit && (origin != 0 || pbase != 0 || cemit_d > 0xFFFFFFFFull)) return hipErrorInvalidValue;
-    // runs of more than halo + 1 entries are reported, wherever they lie (fold_run_limit)
-    const uint32_t lim = fold_run_limit(halo);
-    if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
-    const size_t span = end - origin;
-    if ((halo + 1 >= span || halo + 1 >= fold_len) && origin == 0 && pbase == 0) {
-        // a halo as long as the array (the exact-runs policy: the public worst case n*k + 1
-        // entries per run): ONE lane folds the whole array from position 0, the enclave's
-        // own sequential walk (advanced.rs:66-101) — exact for any run, span/16 stages
-        // whatever the data.  No halo to re-read, no run-length limit.
-        const size_t C1 = (span + FS_W - 1) / FS_W * FS_W;
-        if (C1 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-        net_account((uint64_t)16 * span, "fold_stream_kernel", s);
-        if (cemit)
-            hipLaunchKernelGGL((fold_stream_kernel<2, true>), dim3(1), dim3(64), 0, s, src, dst,
-                               (long long)m, 0ll, (long long)end, 0ll, (long long)fold_len, 0u,
-                               (uint32_t)C1, 0xFFFFFFFFu, status, (uint32_t)cemit_d, cdummy);
-        else
-            hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
-                               0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
-                               0xFFFFFFFFu, status, 0u, 0ull);
-        return hipGetLastError();
-    }
-    const size_t Hr = fold_context(halo);
-    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
+// The chunk length of a fold over span positions with this halo (0: the one-lane walk
+// over the whole array, origin = pbase = 0 only).
+static size_t fold_chunk(size_t span, size_t Hr) {
     size_t C = 64;
     while (C < Hr) C <<= 1;
     // keep >= ~1024 waves: shorter chunks re-read more halo but put more loads in flight
@@ -247,6 +263,50 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     // one doubling more while >= 1024 waves remain: less halo re-read (C5: 2048 instead
     // of 1024, 620 vs 643 us; 4096: 700 us, 8192: 1220 us — too few waves in flight)
     if (C >= Hr && span / (64 * 2 * C) >= FLTEE_FS_DOUBLE_WAVES) C <<= 1;
+    return C;
+}
+
+static bool one_lane(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase) {
+    return (halo + 1 >= span || halo + 1 >= fold_len) && origin == 0 && pbase == 0;
+}
+
+size_t fold_lanes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase) {
+    if (one_lane(span, fold_len, halo, origin, pbase)) return 0;
+    const size_t C = fold_chunk(span, fold_context(halo));
+    return (span + C - 1) / C;
+}
+
+hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_t origin,
+                             size_t end, long long pbase, size_t fold_len, size_t halo,
+                             FoldSide *side, hipStream_t s, size_t cemit_d, uint64_t cdummy) {
+    const bool cemit = cemit_d != 0;
+    if (cemit && (origin != 0 || pbase != 0 || cemit_d > 0xFFFFFFFFull)) return hipErrorInvalidValue;
+    if (end > m || origin >= end || (m & 1) || (origin & 1) || (end & 1)) return hipErrorInvalidValue;
+    const size_t span = end - origin;
+    if (one_lane(span, fold_len, halo, origin, pbase)) {
+        // a halo as long as the array (the exact-runs policy: the public worst case n*k + 1
+        // entries per run): ONE lane folds the whole array from position 0, the enclave's
+        // own sequential walk (advanced.rs:66-101) — exact for any run, span/16 stages
+        // whatever the data.  No halo to re-read, no boundary, no side record.
+        const size_t C1 = (span + FS_W - 1) / FS_W * FS_W;
+        if (C1 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        net_account((uint64_t)16 * span, "fold_stream_kernel", s);
+        if (cemit)
+            hipLaunchKernelGGL((fold_stream_kernel<2, true>), dim3(1), dim3(64), 0, s, src, dst,
+                               (long long)m, 0ll, (long long)end, 0ll, (long long)fold_len, 0u,
+                               (uint32_t)C1, (FoldSide *)nullptr, (uint32_t)cemit_d, cdummy);
+        else
+            hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
+                               0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
+                               (FoldSide *)nullptr, 0u, 0ull);
+        return hipGetLastError();
+    }
+    if (!side) return hipErrorInvalidValue;
+    const size_t Hr = fold_context(halo);
+    if (Hr > ((size_t)1 << 30)) return hipErrorInvalidValue;
+    // range mode reads the record in front of the first walk (the context holds Hr + 1)
+    if (origin != 0 && origin < Hr + 1) return hipErrorInvalidValue;
+    const size_t C = fold_chunk(span, Hr);
     const size_t lanes = (span + C - 1) / C;
     const size_t blocks = (lanes + 63) / 64;
     net_account((uint64_t)16 * span, "fold_stream_kernel", s);
@@ -257,8 +317,8 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
 #define FS_GO(D_, E_)                                                                              \
     hipLaunchKernelGGL((fold_stream_kernel<D_, E_>), dim3((unsigned)blocks), dim3(64), 0, s, src,  \
                        dst, (long long)m, (long long)origin, (long long)end, pbase,                \
-                       (long long)fold_len, (uint32_t)Hr, (uint32_t)C, lim, status,                \
-                       (uint32_t)cemit_d, cdummy)
+                       (long long)fold_len, (uint32_t)Hr, (uint32_t)C, side, (uint32_t)cemit_d,    \
+                       cdummy)
     if (depth == 2) {
         if (cemit) FS_GO(2, true);
         else FS_GO(2, false);
@@ -270,12 +330,108 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     return hipGetLastError();
 }
 
+// ---- the long-run patch (see the header) ----------------------------------------
+// One block of 1024 threads over the G lanes' side records: thread t takes lanes
+// [t * per, (t + 1) * per); an exclusive block scan of the threads' aggregates, the
+// carry from the ranges before (prev[0, nprev): their totals, in order) in front.
+// PATCH: dst[a_j] for every lane j (read, then written back or replaced: fixed
+// addresses); else: *total = the aggregate of all G pieces.
+constexpr int kFpNT = 1024;
+template <bool PATCH, bool CEMIT>
+__global__ __launch_bounds__(kFpNT) void fold_patch_kernel(const FoldSide *__restrict__ side,
+                                                           uint32_t G, uint64_t *__restrict__ dst,
+                                                           long long origin, uint32_t C,
+                                                           long long pbase,
+                                                           const FoldAgg *__restrict__ prev,
+                                                           uint32_t nprev, FoldAgg *total,
+                                                           uint32_t dsel, uint64_t cdummy) {
+    __shared__ FoldAgg part[kFpNT];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (G + kFpNT - 1) / kFpNT;
+    const uint32_t j0 = t * per, j1 = min(j0 + per, G);
+    FoldAgg acc = fa_empty();
+    for (uint32_t j = j0; j < j1; ++j) acc = fa_combine(acc, fa_of(side[j]));
+    part[t] = acc;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over the 1024 thread aggregates (order kept: x before y)
+    for (uint32_t o = 1; o < kFpNT; o <<= 1) {
+        const FoldAgg y = part[t];
+        const FoldAgg x = t >= o ? part[t - o] : fa_empty();
+        __syncthreads();
+        part[t] = fa_combine(x, y);
+        __syncthreads();
+    }
+    if constexpr (!PATCH) {
+        if (t == 0) *total = part[kFpNT - 1];
+        return;
+    } else {
+        FoldAgg run = fa_empty();
+        for (uint32_t i = 0; i < nprev; ++i) run = fa_combine(run, prev[i]);
+        if (t > 0) run = fa_combine(run, part[t - 1]);
+        for (uint32_t j = j0; j < j1; ++j) {
+            const FoldSide sd = side[j];
+            const long long aj = origin + (long long)j * C;
+            const uint64_t was = dst[aj];
+            // a lane with a run begun before its walk: the run's key is the one in front of
+            // the walk, the last key of the pieces before (run.K)
+            const bool c = (sd.fl & kFsCorr) && (run.fl & kFsPiece) && run.K == sd.ck;
+            const float tot = __fadd_rn(run.Q, sd.S);
+            uint64_t rec;
+            if constexpr (CEMIT)
+                rec = sd.ck < dsel ? make_rec((uint32_t)(aj + pbase) - sd.ck, tot) : cdummy;
+            else
+                rec = make_rec(sd.ck, tot);
+            dst[aj] = c ? rec : was;
+            run = fa_combine(run, fa_of(sd));
+        }
+    }
+}
+
+size_t fold_side_bytes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase) {
+    return fold_lanes(span, fold_len, halo, origin, pbase) * sizeof(FoldSide);
+}
+
+hipError_t launch_fold_range_total(const FoldSide *side, size_t lanes, FoldAgg *total,
+                                   hipStream_t s) {
+    if (lanes > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fold_patch_kernel<false, false>), dim3(1), dim3(kFpNT), 0, s, side,
+                       (uint32_t)lanes, (uint64_t *)nullptr, 0ll, 0u, 0ll, (const FoldAgg *)nullptr,
+                       0u, total, 0u, 0ull);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold_range_patch(uint64_t *dst, size_t span, size_t origin, long long pbase,
+                                   size_t fold_len, size_t halo, const FoldSide *side,
+                                   const FoldAgg *prev, size_t nprev, hipStream_t s,
+                                   size_t cemit_d, uint64_t cdummy) {
+    const size_t lanes = fold_lanes(span, fold_len, halo, origin, pbase);
+    if (lanes == 0) return hipSuccess;  // the one-lane walk: nothing to patch
+    if (lanes > 0xFFFFFFFFull || nprev > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const size_t C = fold_chunk(span, fold_context(halo));
+    net_account((uint64_t)sizeof(FoldSide) * lanes + 16 * lanes, "fold_patch_kernel", s);
+    if (cemit_d)
+        hipLaunchKernelGGL((fold_patch_kernel<true, true>), dim3(1), dim3(kFpNT), 0, s, side,
+                           (uint32_t)lanes, dst, (long long)origin, (uint32_t)C, pbase, prev,
+                           (uint32_t)nprev, (FoldAgg *)nullptr, (uint32_t)cemit_d, cdummy);
+    else
+        hipLaunchKernelGGL((fold_patch_kernel<true, false>), dim3(1), dim3(kFpNT), 0, s, side,
+                           (uint32_t)lanes, dst, (long long)origin, (uint32_t)C, pbase, prev,
+                           (uint32_t)nprev, (FoldAgg *)nullptr, 0u, 0ull);
+    return hipGetLastError();
+}
+
 hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold_len, size_t halo,
-                       uint32_t *status, hipStream_t s, size_t cemit_d, uint64_t cdummy) {
+                       void *side_ws, size_t side_cap, hipStream_t s, size_t cemit_d,
+                       uint64_t cdummy) {
     if (m == 1 && !cemit_d)  // nothing to fold: position 0 receives itself (:102-103)
         return hipMemcpyAsync(dst, src, 8, hipMemcpyDeviceToDevice, s);
     if (m == 0 || (m & 1)) return hipErrorInvalidValue;  // m = next_pow2: 16-B windows
-    return launch_fold_range(src, dst, m, 0, m, 0, fold_len, halo, status, s, cemit_d, cdummy);
+    if (side_cap < fold_side_bytes(m, fold_len, halo, 0, 0)) return hipErrorInvalidValue;
+    FoldSide *side = (FoldSide *)side_ws;
+    hipError_t e = launch_fold_range(src, dst, m, 0, m, 0, fold_len, halo, side, s, cemit_d, cdummy);
+    if (e == hipSuccess)
+        e = launch_fold_range_patch(dst, m, 0, 0, fold_len, halo, side, nullptr, 0, s, cemit_d, cdummy);
+    return e;
 }
 
 template <bool ACC>

@@ -26,7 +26,7 @@ ALG_CODES = {  # src/option.py:131-145
 
 DEV_ERR_DENSE_ORDER = 0x1
 DEV_ERR_INDEX_RANGE = 0x2
-DEV_ERR_FOLD_OVERFLOW = 0x4
+DEV_ERR_FOLD_OVERFLOW = 0x4  # retired in round 6: never set
 
 OPT_DENSE = 0x1
 OPT_DP = 0x2
@@ -85,7 +85,10 @@ SIGNATURES = {
     "fltee_bitonic_range_exchange_device": (_U32, [_P, _P, _S, _S, _S, _U32, _U32, _U32, _P]),
     "fltee_bitonic_range_steps_device": (_U32, [_P, _S, _S, _U32, _U32, _U32, _U32, _U32, _P]),
     "fltee_fold_context": (_S, [_S]),
+    "fltee_fold_side_bytes": (_S, [_S, _S]),
     "fltee_fold_range_device": (_U32, [_P, _P, _S, _S, _S, ctypes.c_int64, _S, _S, _P, _P]),
+    "fltee_fold_range_total_device": (_U32, [_P, _S, _S, _P, _P]),
+    "fltee_fold_range_patch_device": (_U32, [_P, _S, _S, ctypes.c_int64, _S, _S, _P, _P, _S, _P]),
     "fltee_compact_range_device": (_U32, [_P, _S, _S, _P, _P, _F, _P, _P]),
     "fltee_nips19_build_range_device": (_U32, [_P, _S, _P, _S, _S, _S, _S, _P, _P]),
     "fltee_safe_aggregate_device": (_U32, [_P, _S, _S, _P, _P]),

@@ -190,10 +190,36 @@ def fold_context(halo):
     return L.lib().fltee_fold_context(halo)
 
 
-def fold_range(src, dst, origin, end, pos_base, fold_len, halo, status_word, stream=None):
+def fold_side_bytes(span, halo):
+    return L.lib().fltee_fold_side_bytes(span, halo)
+
+
+def fold_range(src, dst, origin, end, pos_base, fold_len, halo, side, stream=None):
+    """fltee_fold_range_device: [0, origin) of src holds >= fold_context(halo) + 1 records
+    of context; side: a byte buffer of >= fold_side_bytes(end - origin, halo)."""
+    assert side.numel() * side.element_size() >= fold_side_bytes(end - origin, halo)
     _check(L.lib().fltee_fold_range_device(_ptr(src), _ptr(dst), src.numel(), origin, end, pos_base,
-                                           fold_len, halo, _ptr(status_word), _stream(stream)),
+                                           fold_len, halo, _ptr(side), _stream(stream)),
            "fltee_fold_range_device")
+    return dst
+
+
+def fold_range_total(side, span, halo, total, stream=None):
+    """the range's segmented total (16 bytes into `total`) for the ranges after it"""
+    assert total.numel() * total.element_size() >= 16
+    _check(L.lib().fltee_fold_range_total_device(_ptr(side), span, halo, _ptr(total), _stream(stream)),
+           "fltee_fold_range_total_device")
+    return total
+
+
+def fold_range_patch(dst, origin, end, pos_base, fold_len, halo, side, prev_totals, stream=None):
+    """the long-run patch of one range's fold output; prev_totals: the totals of the ranges
+    before it, in order (a contiguous tensor of n * 16 bytes, or None)"""
+    n_prev = 0 if prev_totals is None else prev_totals.numel() * prev_totals.element_size() // 16
+    _check(L.lib().fltee_fold_range_patch_device(_ptr(dst), origin, end, pos_base, fold_len, halo,
+                                                 _ptr(side), _ptr(prev_totals) if n_prev else None,
+                                                 n_prev, _stream(stream)),
+           "fltee_fold_range_patch_device")
     return dst
 
 

@@ -163,14 +163,24 @@ class DeviceRangeOps:
         self.D.bitonic_range_steps(x, pos, stage_log, step_top, step_bot)
 
     def fold(self, buf, origin, end, pos_base, fold_len, halo, key=0):
+        """The range's fold into a buffer like `buf` (positions [origin, end) written) and
+        its side records (fltee_fold_range_device)."""
         dst = self._buf(("fold", key), buf.numel(), torch.int64, buf.device)
-        st = self._buf(("st", key), 1, torch.int32, buf.device)
-        st.zero_()
-        self.D.fold_range(buf, dst, origin, end, pos_base, fold_len, halo, st)
-        return dst[origin:end], st
+        nb = max(16, self.D.fold_side_bytes(end - origin, halo))
+        side = self._buf(("side", key), (nb + 7) // 8, torch.int64, buf.device)
+        self.D.fold_range(buf, dst, origin, end, pos_base, fold_len, halo, side)
+        return dst, side
 
-    def ok(self, statuses):
-        return all(int(s.item()) == 0 for s in statuses)
+    def total(self, side, span, halo, key=0):
+        """16 bytes: the range's segmented total (int32 x 4)."""
+        t = torch.empty(4, dtype=torch.int32, device=side.device)
+        self.D.fold_range_total(side, span, halo, t)
+        return t
+
+    def patch(self, dst, origin, end, pos_base, fold_len, halo, side, prev):
+        """The long-run patch with the totals of the ranges before (list, in order)."""
+        pt = torch.cat(prev).contiguous() if prev else None
+        self.D.fold_range_patch(dst, origin, end, pos_base, fold_len, halo, side, pt)
 
     def compact(self, chunk, d, key=0):
         n = chunk.numel() + d
@@ -209,6 +219,11 @@ class VirtualRanks:
 
     def all_true(self, flag):
         return flag
+
+    def gather_totals(self, tots):
+        """Every range gets the totals of all ranges, in range order."""
+        every = [tots[q] for q in range(self.world)]
+        return {r: every for r in tots}
 
     def reduce(self, outs, root):
         out = outs[0].clone()
@@ -289,6 +304,17 @@ class DistRanks:
         t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
+
+    def gather_totals(self, tots):
+        """All ranks' 16-byte fold totals to every rank (one all_gather)."""
+        x = tots[self.rank]
+        staged = dist.get_backend() == "gloo" and x.is_cuda
+        h = x.cpu() if staged else x
+        parts = [torch.empty_like(h) for _ in range(self.world)]
+        dist.all_gather(parts, h)
+        if staged:
+            parts = [p.to(x.device) for p in parts]
+        return {self.rank: parts}
 
     def gather_lists(self, lists, root):
         """Variable-length lists to the root, concatenated in rank order: the counts go
@@ -410,10 +436,6 @@ def index_sharded_nips19(chunks, world, M, n_total, d, seed, ops=None, comm=None
     return out
 
 
-class FoldRunTooLong(ValueError):
-    """advanced's fold saw a run of more than halo + 1 entries: the ECALL's 0x2."""
-
-
 def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None, halo=None,
                            root=0, dp=None, exchange="transpose", spare=None):
     """Option B: `advanced` over the padded array of M = next_pow2(n_total*k + d)
@@ -425,10 +447,11 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
 
     advanced.rs:39-113 step by step: the network (:147-176) = per-range stages up to
     C, then per stage the exchange steps (j >= C, partner r ^ j/C) and the range's
-    own steps (j < C); the fold (:66-101) with fold_context(halo) records of the
-    previous range in front and the next range's first records behind (a run of more
-    than halo + 1 entries raises FoldRunTooLong: every rank raises, as the ECALL
-    returns 0x2); the second
+    own steps (j < C); the fold (:66-101) with fold_context(halo) + 16 records of the
+    previous range in front and the next range's first records behind, then the
+    long-run patch: every range's segmented total goes to the ranges after it, which
+    finish the runs begun before them (runs of any length: bit for bit up to halo + 1
+    entries, re-associated at the fold's walk boundaries beyond); the second
     sort's [0, d) prefix (:106-111, :32-34) = each range's compacted representatives,
     summed over the ranges by one reduce, then x 1f32/n (common.rs:14-19).
 
@@ -448,22 +471,22 @@ def index_sharded_advanced(chunks, world, M, n_total, k, d, ops=None, comm=None,
     chunks = distributed_network(chunks, world, M, ops, comm, exchange=exchange, spare=spare,
                                  valid=n_total * k + d)
     fold_len = n_total * k + d
-    # one fold with halo n (or the caller's): a run of more than halo + 1 entries (a client
-    # repeated an index) is reported by every range that sees it and rejects the call, as
-    # the ECALL does (0x2) — no data-dependent rerun
+    # one fold with halo n (or the caller's), fixed cost: a run of more than halo + 1
+    # entries (a client repeated an index) is finished by the patch, no rerun
     h = n_total if halo is None else halo
-    H = ops.fold_context(h)
-    if H > C:
-        raise ValueError(f"fold context {H} exceeds the range size {C}")
-    prev, nxt = comm.neighbours(chunks, H, 16, ops.pads)
-    folded, statuses = {}, []
+    X = ops.fold_context(h) + 16  # the halo and the record in front of the first walk
+    if X > C:
+        raise ValueError(f"fold context {X} exceeds the range size {C}")
+    prev, nxt = comm.neighbours(chunks, X, 16, ops.pads)
+    folded, sides, tots = {}, {}, {}
     for r, x in chunks.items():
         buf = torch.cat([prev[r], x, nxt[r]])
-        folded[r], st = ops.fold(buf, H, H + C, r * C - H, fold_len, h, key=r)
-        statuses.append(st)
-    if not comm.all_true(ops.ok(statuses)):
-        raise FoldRunTooLong(f"a run of more than {h + 1} entries (a client repeated an index)")
-    outs = {r: ops.compact(f, d, key=r) for r, f in folded.items()}
+        folded[r], sides[r] = ops.fold(buf, X, X + C, r * C - X, fold_len, h, key=r)
+        tots[r] = ops.total(sides[r], C, h, key=r)
+    every = comm.gather_totals(tots)
+    for r, f in folded.items():
+        ops.patch(f, X, X + C, r * C - X, fold_len, h, sides[r], every[r][:r])
+    outs = {r: ops.compact(f[X:X + C], d, key=r) for r, f in folded.items()}
     out = comm.reduce(outs, root)
     if out is None:
         return None

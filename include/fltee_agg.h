@@ -140,8 +140,8 @@ fltee_status_t ecall_client_size_optimized_secure_aggregation(
 /* device status bits */
 #define FLTEE_DEV_ERR_DENSE_ORDER 0x1u   /* dense input with idx != position */
 #define FLTEE_DEV_ERR_INDEX_RANGE 0x2u   /* idx >= d where the reference panics */
-#define FLTEE_DEV_ERR_FOLD_OVERFLOW 0x4u /* a run of more than halo + 1 entries (advanced's
-                                           fold; halo n: a client repeated an index) */
+#define FLTEE_DEV_ERR_FOLD_OVERFLOW 0x4u /* retired in round 6 (advanced's fold finishes runs
+                                           of any length); never set */
 #define FLTEE_DEV_ERR_ORAM_STASH 0x8u    /* path_oram tree mode: the stash (20) overflowed */
 #define FLTEE_DEV_ERR_LAUNCH 0x80000000u
 
@@ -172,7 +172,9 @@ typedef struct fltee_device_opts {
     size_t k_req;       /* advanced: request num_of_sparse_parameters (with FLTEE_OPT_K_REQ) */
     size_t batch;       /* alg 6: optimal_num_of_clients */
     size_t n_avg;       /* divisor for averaging (0 = n) */
-    size_t fold_halo;   /* advanced fold halo H (0 = n, exact when each client's indices are distinct) */
+    size_t fold_halo;   /* advanced fold halo H (0 = n): runs of <= H + 1 entries (each client's
+                           indices distinct) bit for bit, longer ones re-associated at the
+                           fold's walk boundaries */
     uint32_t *d_status; /* optional device status word (never cleared by the library) */
 } fltee_device_opts;
 
@@ -288,15 +290,33 @@ fltee_status_t fltee_bitonic_range_steps_device(void *d_records, size_t m, size_
                                                 uint32_t mode, uint32_t seed, uint32_t stage_log,
                                                 uint32_t step_top, uint32_t step_bot,
                                                 void *stream);
-/* records of context the fold needs in front of a range: halo rounded up to 16. */
+/* records of context the fold needs in front of a range: halo rounded up to 16 (the
+ * range fold reads one more record in front, see below). */
 size_t fltee_fold_context(size_t halo);
 /* advanced.rs:66-101 on [origin, end) of d_src (length m, global position =
- * pos_base + local): [0, origin) holds >= fltee_fold_context(halo) records of the
+ * pos_base + local): [0, origin) holds >= fltee_fold_context(halo) + 1 records of the
  * previous range, d_src[end] the next range's first record (unless end + pos_base
- * >= fold_len).  Writes d_dst[origin, end). */
+ * >= fold_len).  Writes d_dst[origin, end) and the fold's side records into d_side
+ * (fltee_fold_side_bytes(end - origin, halo) bytes).  Runs of any length (a client
+ * repeating an index): a run begun before a walk boundary is finished by the patch
+ * below — bit for bit for every run of <= halo + 1 entries, re-associated at the
+ * walk boundaries beyond. */
+size_t fltee_fold_side_bytes(size_t span, size_t halo);
 fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m, size_t origin,
                                        size_t end, int64_t pos_base, size_t fold_len, size_t halo,
-                                       uint32_t *d_status, void *stream);
+                                       void *d_side, void *stream);
+/* the range's segmented total (16 bytes into d_total) from its side records: the
+ * carry the ranges after it need */
+fltee_status_t fltee_fold_range_total_device(const void *d_side, size_t span, size_t halo,
+                                             void *d_total, void *stream);
+/* the long-run patch of one range's fold output d_dst (the same origin, end, pos_base,
+ * fold_len and halo as fltee_fold_range_device): d_prev_totals = the totals of the
+ * n_prev ranges before this one, in range order.  Writes every walk's first position
+ * (fixed addresses). */
+fltee_status_t fltee_fold_range_patch_device(void *d_dst, size_t origin, size_t end,
+                                             int64_t pos_base, size_t fold_len, size_t halo,
+                                             const void *d_side, const void *d_prev_totals,
+                                             size_t n_prev, void *stream);
 /* one folded range (c records) -> d_out[d]: val * coef at each run representative's
  * index i < d held by this range, +0.0 elsewhere (oblivious compaction; scratch
  * d_buf, d_tmp of d + c records each).  The sum of every range's d_out is the

@@ -109,31 +109,80 @@ class NumpyRangeOps:
             _step(a, pos, stage_log, jlog)
 
     def fold(self, buf, origin, end, pos_base, fold_len, halo, key=0):
-        """fo_fold (advanced.rs:66-101) over the buffer's global positions, started
-        fresh at its first position: the context in front makes the carry exact."""
+        """fo_fold (advanced.rs:66-101) over the buffer's global positions, one walk from
+        local position 1 (the record in front of it tells whether the run there began
+        before): the context in front makes the carry exact for every run of <= halo + 1
+        entries; a run begun before the walk and ended in [origin, end) is left as a dummy
+        and carried by the side record (the device's FoldSide, one walk per range here)."""
         s = _u(buf)
         out = s.copy()
-        pre_i = pre_v = None
-        for q in range(len(s)):
+        b, C = 1, end - origin
+        hasprev = pos_base + b - 1 >= 0
+        kprev = int(s[b - 1] & MASK) if hasprev else None
+        started, pre_i, pre_v = False, 0, np.float32(0)
+        in_head, unbroken, corr, piece = False, True, False, False
+        ck, cs, pf_key, pk, pq = 0, np.float32(0), 0, 0, np.float32(0)
+        for q in range(b, end + 1):
             g = pos_base + q
-            if g < 0 or g >= fold_len:
-                continue
-            ci, cv = int(s[q] & MASK), np.uint32(int(s[q] >> np.uint64(32))).view(np.float32)
-            if pre_i is None:
-                pre_i, pre_v = ci, cv
-            else:
-                if ci == pre_i:
+            ci = int(s[q] & MASK)
+            cv = np.uint32(int(s[q] >> np.uint64(32))).view(np.float32)
+            eq = started and ci == pre_i
+            copy = g - 1 >= fold_len
+            dmy = g < fold_len and eq
+            hend = in_head and not copy and not dmy
+            sup = hend and origin <= q - 1 < end
+            if origin <= q - 1 < end:
+                if copy:
+                    out[q - 1] = s[q - 1]
+                elif dmy or sup:
                     out[q - 1] = np.uint64(0xFFFFFFFF - (g - 1))
-                    pre_v = np.float32(pre_v + cv)
                 else:
-                    out[q - 1] = np.uint64(pre_i) | (np.uint64(pre_v.view(np.uint32)) << np.uint64(32))
-                    pre_i, pre_v = ci, cv
-            if g == fold_len - 1:
-                out[q] = np.uint64(pre_i) | (np.uint64(np.float32(pre_v).view(np.uint32)) << np.uint64(32))
-        return torch.from_numpy(out.view(np.int64)[origin:end].copy()), 0
+                    out[q - 1] = np.uint64(pre_i) | (np.uint64(np.float32(pre_v).view(np.uint32)) << np.uint64(32))
+            if sup:
+                corr, ck, cs = True, pre_i, pre_v
+            in_head = in_head and not hend and not copy
+            if g >= 0:
+                if not started:
+                    pf_key = ci
+                    in_head = hasprev and ci == kprev
+                else:
+                    unbroken = unbroken and eq
+                pre_v = np.float32(pre_v + cv) if eq else cv
+                pre_i = ci
+                started = True
+            if q == b + C - 1 and started and g >= 0:
+                piece, pk, pq = True, pre_i, pre_v
+        fl = (1 if piece else 0) | (2 if piece and unbroken else 0) | (4 if corr else 0)
+        side = np.array([pf_key, pk, np.float32(pq).view(np.uint32), fl, ck,
+                         np.float32(cs).view(np.uint32)], dtype=np.uint32)
+        return torch.from_numpy(out.view(np.int64).copy()), side
 
-    def ok(self, statuses):
-        return True
+    def total(self, side, span, halo, key=0):
+        return torch.from_numpy(np.array([side[0], side[1], side[2], side[3] & 3], np.uint32).view(np.int32))
+
+    @staticmethod
+    def _agg(t):
+        a = np.asarray(t).view(np.uint32)
+        return int(a[0]), int(a[1]), np.uint32(a[2]).view(np.float32), int(a[3]) & 3
+
+    @staticmethod
+    def _combine(x, y):
+        if not x[3] & 1:
+            return y
+        if not y[3] & 1:
+            return x
+        full = bool(x[3] & 2) and bool(y[3] & 2) and x[1] == y[0]
+        q = np.float32(x[2] + y[2]) if (y[3] & 2 and y[0] == x[1]) else y[2]
+        return x[0], y[1], q, 1 | (2 if full else 0)
+
+    def patch(self, dst, origin, end, pos_base, fold_len, halo, side, prev):
+        run = (0, 0, np.float32(0), 0)
+        for t in prev:
+            run = self._combine(run, self._agg(t.numpy() if hasattr(t, "numpy") else t))
+        if side[3] & 4 and run[3] & 1 and run[1] == int(side[4]):
+            tot = np.float32(run[2] + np.uint32(side[5]).view(np.float32))
+            v = np.uint64(int(side[4])) | (np.uint64(tot.view(np.uint32)) << np.uint64(32))
+            dst[origin] = torch.tensor(np.array([v], np.uint64).view(np.int64)[0])
 
     def compact(self, chunk, d, key=0):
         a = _u(chunk)

@@ -109,3 +109,29 @@ def test_advanced_c5_ecall_one_gpu_and_8_rank_eid(c5, device_out, oracle):
     finally:
         grp.destroy()
     assert np.array_equal(bits(out8), bits(device_out))
+
+
+@pytest.mark.parametrize("adv", ["one_client", "all_one_index"])
+def test_advanced_c5_adversarial_runs(c5, adv):
+    """configs[4] at full size with adversarial uploads: client 0 sending
+    one index k = 100,000 times, and all n*k = 10^8 records on one index (one run over
+    ~50,000 fold lanes).  One fixed-cost pass, no status; every index within the bound
+    any f32 left fold of its run obeys against the exact (float64) sum — the full-size
+    property check (the oracle's network at 2^27 per case would take minutes)."""
+    import torch
+
+    from longrun import assert_near_exact
+
+    from fltee import device as dev
+    idx, val = c5
+    idx = idx.copy()
+    if adv == "one_client":
+        idx[:K] = 7
+    else:
+        idx[:] = 7
+    rec = torch.from_numpy(dev.pack_records(idx, val)).cuda()
+    out = dev.aggregate(1, rec, N, K, D).cpu().numpy()
+    assert dev.status() == 0
+    del rec
+    torch.cuda.empty_cache()
+    assert_near_exact(out, idx, val, D, N)

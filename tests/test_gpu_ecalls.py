@@ -147,18 +147,19 @@ def _encrypt(oracle, ids, recs):
     return oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
 
 
-def test_advanced_long_run_is_rejected(enclave, oracle):
-    """advanced's fold runs once with halo n — fixed cost.  A client
-    repeating one index k times makes a run of ~k entries, more than the n + 1 that
-    distinct indices allow: the fold's own pass reports it and the ECALL returns 0x2 (like
-    an out-of-range index) instead of rerunning with a wider halo, for alg 1 and alg 6.
-    A repeated index that keeps every run within n + 1 entries is still folded exactly."""
+def test_advanced_long_run_is_folded(enclave, oracle):
+    """advanced's fold runs once with halo n — fixed cost.  A client repeating one index k
+    times makes a run of ~k entries, more than the n + 1 that distinct indices allow: the
+    ECALL returns the reference's aggregate (round 6: no 0x2), every run of <= n + 1
+    entries bit for bit and the long one within the re-association bound, for alg 1 and
+    alg 6.  A repeated index that keeps every run within n + 1 entries is exact."""
+    from longrun import assert_advanced
     from fltee import _lib as L
     from fltee.ecalls import set_debug_seed
     n = 30
     rng = np.random.default_rng(5)
     ids = np.arange(500, 500 + n, dtype=np.uint32)
-    for k, d, reps, want in ((4000, 4000, 4000, L.ERROR_INVALID_PARAMETER), (1000, 4000, 3, 0)):
+    for k, d, reps, want in ((4000, 4000, 4000, 0), (1000, 4000, 3, 0)):
         recs = []
         for c in range(n):
             w = np.zeros(k, dtype=oracle.WEIGHT)
@@ -182,10 +183,9 @@ def test_advanced_long_run_is_rejected(enclave, oracle):
                     fl, 0, 7, ids, enc, d, k, alg)
                 ost, ref, _ = O.client_size_optimized_secure_aggregation(fl, 0, 7, ids, enc, d, k, alg)
             assert (st, rv, ost) == (0, want, 0)
-            if want == 0:
-                assert bits_equal(out, ref)
-            else:
-                assert not out.any()  # a rejected call returns the zeroed [out] buffer
+            allw = np.concatenate(recs)
+            nlong = assert_advanced(out, ref, allw["idx"], allw["val"], d, n)
+            assert (nlong > 0) == (reps > n)
     set_debug_seed(0)
 
 
@@ -258,11 +258,13 @@ def test_repeated_small_calls_of_one_shape(enclave, oracle, alg):
         st, rv, out, ost, ref = call(fl + r, ids, kk, payload(ids, kk, dup))
         assert st == 0 and rv == ost == 0, (r, rv, ost)
         assert bits_equal(out, ref), r
-    # a run longer than n + 1 through the replayed graph: the status word still reaches
-    # the retval (0x2), and the next call of the shape is clean again
+    # a run longer than n + 1 (round 6: folded, no 0x2), and the next call of the shape is
+    # bit for bit again
     one = np.array([21], np.uint32)
     for r in range(3):
         st, rv, out, ost, ref = call(fl + 10 + r, one, k, payload(one, k, dup=(r == 1)))
-        assert st == 0 and rv == (2 if r == 1 else 0)
+        assert st == 0 and rv == ost == 0
         if r != 1:
-            assert ost == 0 and bits_equal(out, ref)
+            assert bits_equal(out, ref)
+        else:
+            assert np.allclose(out, ref, rtol=1e-5, atol=1e-9)

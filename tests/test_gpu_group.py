@@ -109,10 +109,13 @@ def test_group_alg6_bit_identical_to_one_gpu(enclaves, oracle, name, batch, w):
 
 
 def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
-    """A client repeating one index (a run of more than n + 1 entries): every eid rejects
-    the call with 0x2 after one fold (no halo widening, as the ECALL); the k=0 dense
-    quirk (advanced.rs:70, the root path) equals the single-GPU result."""
-    from fltee import _lib as L
+    """A client repeating one index (a run of more than n + 1 entries): every eid folds it
+    in one fixed-cost pass (round 6) — the long run crossing the position ranges finished
+    through the ranges' totals (group.hip) — every other index bit for bit against the
+    oracle, the long one within the re-association bound; the k=0 dense quirk
+    (advanced.rs:70, the root path) equals the single-GPU result."""
+    from longrun import assert_advanced
+
     from fltee.ecalls import set_debug_seed
     rng = np.random.default_rng(3)
     n, k, d = 16, 3000, 3000
@@ -127,6 +130,9 @@ def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
             w["idx"] = 11
         recs.append(w)
     enc = oracle.encrypt_clients(ids, [r.tobytes() for r in recs])
+    allw = np.concatenate(recs)
+    ref, rst = oracle.advanced(k, allw, d, n)
+    assert rst == 0
     for w in (1, 2, 8):
         E = enclaves[w]
         _fl[0] += 1
@@ -135,7 +141,8 @@ def test_group_advanced_long_run_and_k_quirk(enclaves, oracle):
         assert E.ecall_start_round(_fl[0], 0, n)[:2] == (0, 0)
         st, rv, out, _ = E.ecall_secure_aggregation(_fl[0], 0, ids, enc, d, k, 1)
         set_debug_seed(0)
-        assert (st, rv) == (0, L.ERROR_INVALID_PARAMETER) and not out.any()
+        assert (st, rv) == (0, 0)
+        assert assert_advanced(out, ref, allw["idx"], allw["val"], d, n) == 1, w
     enc0 = oracle.encrypt_clients(ids, [r.tobytes() for r in plain])
     c = dict(client_ids=ids, d=d, k=k, n=n, name="quirk")
     one0 = run(enclaves[1], c, 1, enc0, k=0)

@@ -355,16 +355,28 @@ def test_fold_bit_exact(dev, oracle, n, d, k):
         assert np.array_equal(gi, ref["idx"]) and bits_equal(gv, ref["val"])
 
 
-def test_fold_overflow_detected(dev):
+@pytest.mark.parametrize("m,halo,fold_len", [(4096, 8, 4096), (4096, 8, 3000), (1 << 20, 100, 1 << 20),
+                                             (1 << 16, 30, 60000)])
+def test_fold_long_run(dev, m, halo, fold_len):
+    """One run of fold_len records (idx 0, val 1.0) through fltee_fold_device with a halo
+    far shorter than the run: no status, exactly one representative of index 0 among
+    [0, fold_len) — somewhere inside the run (the patch writes it at a walk's first
+    position) — holding the whole run's sum (exact here: integers below 2^24); the rest
+    dummies (u32::MAX - p), the positions past fold_len copied."""
     import torch
-    m = 4096
-    idx = np.zeros(m, np.uint32)                     # one run of m records
+    idx = np.zeros(m, np.uint32)
     src = cuda_records(dev, idx, np.ones(m, np.float32))
     dst = torch.empty_like(src)
     st = torch.zeros(1, dtype=torch.int32, device="cuda")
-    dev.fold(src, dst, m, 8, st)
+    dev.fold(src, dst, fold_len, halo, st)
     torch.cuda.synchronize()
-    assert int(st.item()) & 0x4
+    assert int(st.item()) == 0
+    gi, gv = dev.unpack_records(dst.cpu().numpy())
+    reps = np.flatnonzero(gi[:fold_len] == 0)
+    assert reps.size == 1 and gv[reps[0]] == np.float32(fold_len)
+    others = np.setdiff1d(np.arange(fold_len), reps)
+    assert np.array_equal(gi[others], (0xFFFFFFFF - others).astype(np.uint32))
+    assert np.array_equal(gi[fold_len:], idx[fold_len:])
 
 
 # ---------------------------------------------------------- advanced -------
@@ -621,9 +633,9 @@ def test_swizzled_layout_bit_identical(dev, oracle, alg, n, d, k):
 def test_advanced_fold_fused_into_compaction(dev, oracle, n, d, k, repeat, fused):
     """The fold run inside the compaction's first pass (halo n up to 4096 records; wider
     halos fall back to the separate fold) == the oracle's advanced, bit for bit.  With a
-    repeated index (runs longer than the halo n) the default halo n reports
-    FLTEE_DEV_ERR_FOLD_OVERFLOW (a run of more than n + 1 entries, found by the one pass
-    whether fused or not: the ECALL rejects the call); the run-length halo is exact."""
+    repeated index (runs longer than the halo n) the default halo n finishes the long
+    runs re-associated (no status): bit for bit on every run of <= n + 1 entries, within
+    the re-association bound on the others; the run-length halo is exact."""
     from fltee import _lib as L
     rng = np.random.default_rng(n + d)
     idx, val = rand_sparse(rng, n, d, k)
@@ -637,10 +649,51 @@ def test_advanced_fold_fused_into_compaction(dev, oracle, n, d, k, repeat, fused
         out = dev.aggregate(1, rec, n, k, d, fold_halo=(k * n + d) if repeat else 0).cpu().numpy()
         assert dev.status() == 0 and bits_equal(out, ref)
         if repeat:
-            dev.aggregate(1, rec, n, k, d)
-            assert dev.status() == 0x4
+            from longrun import assert_advanced
+            out = dev.aggregate(1, rec, n, k, d).cpu().numpy()
+            assert dev.status() == 0
+            assert assert_advanced(out, ref, idx, val, d, n) >= 1
     finally:
         L.lib().fltee_debug_set_fold_compact(1)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("adv", ["one_client", "all_one_index", "two_clients_half"])
+@pytest.mark.parametrize("alg", [1, 6])
+def test_advanced_adversarial_runs_c3_shape(dev, oracle, adv, alg, fused):
+    """configs[2]'s shape (n = 100, d = 50890, k = 5089; M = 2^20) with adversarial
+    uploads: one client sending one index k times, every record on one
+    index (a run of n*k + 1 = 508,901 entries across every tile and lane), two clients
+    splitting theirs over two indices.  Fixed cost, no status: every run of <= n + 1
+    entries bit for bit against the oracle's advanced (alg 6: its batches of 30), the long
+    ones within the re-association bound — through the fused fold + compaction (the
+    tiles' look-back carries) and through the streaming fold + patch."""
+    from longrun import assert_advanced
+
+    from fltee import _lib as L
+    n, d, k = 100, 50890, 5089
+    rng = np.random.default_rng(77)
+    idx, val = rand_sparse(rng, n, d, k)
+    if adv == "one_client":
+        idx[:k] = 7
+    elif adv == "all_one_index":
+        idx[:] = 7
+    else:
+        idx[k:3 * k] = np.where(np.arange(2 * k) % 2 == 0, 11, 50000).astype(np.uint32)
+    rec = cuda_records(dev, idx, val)
+    w = oracle.as_weights(idx, val)
+    if alg == 1:
+        ref, rst = oracle.advanced(k, w, d, n)
+    else:
+        ref, rst = oracle.client_size_optimized(30, k, w, d, n)
+    assert rst == 0
+    L.lib().fltee_debug_set_fold_compact(1 if fused else 0)
+    try:
+        out = dev.aggregate(alg, rec, n, k, d, batch=30 if alg == 6 else 0).cpu().numpy()
+        assert dev.status() == 0
+    finally:
+        L.lib().fltee_debug_set_fold_compact(1)
+    assert assert_advanced(out, ref, idx, val, d, n) >= 1
 
 
 @pytest.mark.parametrize("n,d,k", [(10, 4000, 1000), (10, 8000, 1000), (10, 16000, 1000),

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+from longrun import assert_advanced
 from range_ops_np import NumpyRangeOps, init_range
 
 
@@ -21,7 +22,8 @@ def case(seed, n, d, k, idx_hi=None):
 @pytest.mark.parametrize("exchange", ["transpose", "pairwise"])
 @pytest.mark.parametrize("world,n,d,k,idx_hi", [(1, 5, 200, 30, None), (2, 5, 200, 30, None),
                                                 (4, 6, 300, 20, None), (8, 4, 100, 50, None),
-                                                (4, 10, 150, 40, 40), (2, 7, 333, 1, None)])
+                                                (4, 10, 150, 40, 40), (2, 7, 333, 1, None),
+                                                (4, 10, 150, 40, 1), (8, 30, 100, 60, 3)])
 def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi, exchange):
     from fltee.parallel import VirtualRanks, index_sharded_advanced
     idx, val = case(world * 100 + n, n, d, k, idx_hi)
@@ -32,7 +34,9 @@ def test_virtual_ranks_match_oracle(oracle, world, n, d, k, idx_hi, exchange):
                                  comm=VirtualRanks(world), exchange=exchange)
     ref, st = oracle.advanced(k, oracle.as_weights(idx, val), d, n)
     assert st == 0
-    assert np.array_equal(out.numpy().view(np.uint32), ref.view(np.uint32))
+    # bit for bit; idx_hi: runs of more than n + 1 entries re-associated (longrun.py)
+    nlong = assert_advanced(out.numpy(), ref, idx, val, d, n)
+    assert idx_hi is not None or nlong == 0
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
