@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     bool started = false;
     uint64_t prev = 0;
     // the side record: the piece [b, b + C) and the head run (the one holding b)
-    bool in_head = false, unbroken = true, corr = false, piece = false;
+    bool in_head = false, unbroken = true, corr = false, piece = false, pfull = false;
     uint32_t pf_key = 0, pk = 0, ck = 0;
     float pq = 0.0f, cs = 0.0f;
     auto stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
@@ -206,6 +206,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             // the piece's last position b + C - 1: its run partial
             if (t == FS_W - 1 && s == C / FS_W - 1 && started && q >= 0 && qg >= 0) {
                 piece = true;
+                pfull = unbroken;  // one key from the walk's start to here
                 pk = pre_idx;
                 pq = pre_val;
             }
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             if (s + (uint32_t)q < nstage) stage(pf[q], s + (uint32_t)q);
     }
     if (side && a < end) {
-        const uint32_t fl = (piece ? kFsPiece : 0u) | (piece && unbroken ? kFsFull : 0u) |
+        const uint32_t fl = (piece ? kFsPiece : 0u) | (pfull ? kFsFull : 0u) |
                             (corr ? kFsCorr : 0u);
         FoldSide *o = side + (size_t)blockIdx.x * 64 + l;
         o->F = pf_key;

@@ -38,7 +38,12 @@ def assert_advanced(out, ref, idx, val, d, n, lim=None):
     o64, r64 = o.astype(np.float64), r.astype(np.float64)
     bound = 2 * (cnt - 1) * U * absum / n + 2 * U * np.abs(r64) + 1e-45
     over = np.flatnonzero(~short & (np.abs(o64 - r64) > bound))
-    assert over.size == 0, f"{over.size} long runs over the bound (first idx {over[:5]})"
+    if over.size:
+        _, _, exact = run_stats(idx, val, d)
+        det = [(int(i), int(cnt[i]), float(o64[i]), float(r64[i]), float(exact[i] / n), float(bound[i]))
+               for i in over[:5]]
+        raise AssertionError(f"{over.size} long runs over the bound: (idx, entries, out, ref, "
+                             f"exact, bound) {det}")
     return int((~short).sum())
 
 

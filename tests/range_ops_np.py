@@ -120,7 +120,7 @@ class NumpyRangeOps:
         hasprev = pos_base + b - 1 >= 0
         kprev = int(s[b - 1] & MASK) if hasprev else None
         started, pre_i, pre_v = False, 0, np.float32(0)
-        in_head, unbroken, corr, piece = False, True, False, False
+        in_head, unbroken, corr, piece, pfull = False, True, False, False, False
         ck, cs, pf_key, pk, pq = 0, np.float32(0), 0, 0, np.float32(0)
         for q in range(b, end + 1):
             g = pos_base + q
@@ -151,8 +151,8 @@ class NumpyRangeOps:
                 pre_i = ci
                 started = True
             if q == b + C - 1 and started and g >= 0:
-                piece, pk, pq = True, pre_i, pre_v
-        fl = (1 if piece else 0) | (2 if piece and unbroken else 0) | (4 if corr else 0)
+                piece, pfull, pk, pq = True, unbroken, pre_i, pre_v
+        fl = (1 if piece else 0) | (2 if piece and pfull else 0) | (4 if corr else 0)
         side = np.array([pf_key, pk, np.float32(pq).view(np.uint32), fl, ck,
                          np.float32(cs).view(np.uint32)], dtype=np.uint32)
         return torch.from_numpy(out.view(np.int64).copy()), side
