@@ -202,6 +202,10 @@ __device__ __forceinline__ FoldAgg fa_empty() {
     return a;
 }
 
+// the fold's side buffer: FoldSide per lane (waves x 64 of them), then FoldAgg per wave
+__host__ __device__ inline FoldAgg *fold_wave_aggs(FoldSide *side, size_t waves) {
+    return reinterpret_cast<FoldAgg *>(side + waves * 64);
+}
 // lanes of a streaming fold over span positions (0: the one-lane walk: no side records)
 size_t fold_lanes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase);
 size_t fold_side_bytes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase);

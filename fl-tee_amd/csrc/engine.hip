@@ -766,7 +766,7 @@ extern "C" fltee_status_t fltee_bitonic_range_steps_device(void *d_records, size
 extern "C" size_t fltee_fold_context(size_t halo) { return fold_context(halo); }
 
 extern "C" size_t fltee_fold_side_bytes(size_t span, size_t halo) {
-    return sizeof(FoldSide) * fold_lanes(span, (size_t)1 << 62, halo, 1, 1);
+    return fold_side_bytes(span, (size_t)1 << 62, halo, 1, 1);
 }
 
 extern "C" fltee_status_t fltee_fold_range_device(const void *d_src, void *d_dst, size_t m,

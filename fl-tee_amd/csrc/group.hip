@@ -595,7 +595,7 @@ uint32_t group_advanced(Group *Gp, const GroupInput &in, size_t n, size_t k, siz
         for (int i = 0; i < W; ++i) {
             Rank &R = G.r[i];
             if (!reserve_on(R, R.fold, m * 8) || !reserve_on(R, R.fold_dst, m * 8) ||
-                !reserve_on(R, R.side, lanes * sizeof(FoldSide) + 64) ||
+                !reserve_on(R, R.side, fold_side_bytes(C, fold_len, h, X, 1) + 64) ||
                 !reserve_on(R, R.tot, (size_t)(W + 1) * sizeof(FoldAgg)))
                 return FLTEE_ERROR_OUT_OF_MEMORY;
             uint64_t *f = (uint64_t *)R.fold.ptr;

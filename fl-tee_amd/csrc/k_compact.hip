@@ -616,12 +616,11 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 // with a bounded wait that reports FLTEE_DEV_ERR_LAUNCH instead of hanging.
 // Resident blocks per CU of the fused first pass, and whether a block prefetches its next
 // window during the fold.  Round 3 (A/B in one process, `profiles/r03/ab/ab18_fold_blocks_*`):
-// three blocks (6 waves per SIMD, <= 85 VGPRs) without the prefetch — the other resident
-// blocks hide the window load, and the prefetch registers no longer spill — run C5's pass
-// in 1,065-1,077 us against 1,198-1,206 us for two prefetching blocks (three prefetching:
-// 1,153-1,157, spilling; four without: 1,149-1,150); C3 unchanged.
+// three blocks without the prefetch ran C5's pass fastest then.  Round 6: with the long-run
+// steps (three LDS arrays, the look-back) three blocks' 80 VGPRs spill 20-50 registers;
+// two blocks (128 VGPRs) do not (`profiles/r06/ab/`).
 #ifndef FLTEE_FC_BLOCKS
-#define FLTEE_FC_BLOCKS 3
+#define FLTEE_FC_BLOCKS 2
 #endif
 #ifndef FLTEE_FC_PF
 #define FLTEE_FC_PF 0
@@ -651,15 +650,39 @@ hipError_t launch_compact_extract(uint64_t *src, uint64_t *tmp, size_t L, size_t
 #endif
 constexpr uint32_t kFixedWalkMax = FLTEE_FC_WALK_MAX;
 constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
+#ifndef FLTEE_FC_LB
+#define FLTEE_FC_LB 1
+#endif
 // the bounded look-back wait: polls of ~0.25 us (about a quarter second in all)
 constexpr uint32_t kFcSpinMax = 1u << 20;
 
-// one tile's look-back slot: its piece aggregate, its inclusive prefix, and the flag
-// (epoch << 2 | 1: aggregate published, | 2: inclusive published)
+// One tile's look-back slot: its piece aggregate and its inclusive prefix, each as three
+// 64-bit words (F, K, Q) whose high halves carry the launch's epoch << 2 | fl.  Every word
+// is written and read with a relaxed agent-scope atomic: a word is valid on its own (its
+// epoch), so no release / acquire fence — on gfx950 those write back / invalidate the
+// XCD's L2 (a few us per tile, measured) — is needed between the data and a flag.
 struct FcLb {
-    FoldAgg agg, inc;
-    uint32_t flag, pad[3];
+    uint64_t agg[3], inc[3];
 };
+
+__device__ __forceinline__ void fc_put(uint64_t *w, const FoldAgg &g, uint32_t epoch) {
+    const uint64_t tag = (uint64_t)((epoch << 2) | (g.fl & 3u)) << 32;
+    __hip_atomic_store(&w[0], tag | g.F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[1], tag | g.K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&w[2], tag | __float_as_uint(g.Q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the three words of this epoch, or false
+__device__ __forceinline__ bool fc_get(uint64_t *w, uint32_t epoch, FoldAgg &g) {
+    const uint64_t a = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(&w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t c = __hip_atomic_load(&w[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ea = (uint32_t)(a >> 34), eb = (uint32_t)(b >> 34), ec = (uint32_t)(c >> 34);
+    g.F = (uint32_t)a;
+    g.K = (uint32_t)b;
+    g.Q = __uint_as_float((uint32_t)c);
+    g.fl = (uint32_t)(c >> 32) & 3u;
+    return ea == epoch && eb == epoch && ec == epoch;
+}
 
 __device__ __forceinline__ FoldAgg fa_shfl_up(const FoldAgg &x, int o) {
     FoldAgg r;
@@ -678,52 +701,73 @@ __device__ __forceinline__ FoldAgg fa_shfl_down(const FoldAgg &x, int o) {
     return r;
 }
 
-// wave 0 of tile `tile`: the aggregate of every piece before it (decoupled look-back)
-__device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t lane,
-                               uint32_t *status) {
-    FoldAgg run = fa_empty();
+// tile `tile` (the whole block): the aggregate of every piece before it (decoupled
+// look-back).  Each round reads NW * 64 predecessors, wave w the 64 from tile - 1 - 64 w
+// back: up to the nearest one with its inclusive prefix published, aggregates in front of
+// it; rounds go on further back only when none of them had it.
+template <int NW>
+__device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t t,
+                               uint32_t *status, FoldAgg *sh, uint32_t *shf) {
+    const uint32_t lane = t & 63, wave = t >> 6;
     long long base = (long long)tile - 1;
     bool done = tile == 0;
-    while (!done) {
-        const long long p = base - (long long)lane;
-        uint32_t st = 2;  // before position 0: nothing (an empty inclusive prefix)
-        bool got = false;
-        if (p >= 0) {
-            uint32_t f = __hip_atomic_load(&lb[p].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t it = 0;
-            while ((f >> 2) != epoch && it < kFcSpinMax) {
-                __builtin_amdgcn_s_sleep(8);
-                f = __hip_atomic_load(&lb[p].flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                ++it;
-            }
-            if ((f >> 2) != epoch) {
-                atomicOr(status, FLTEE_DEV_ERR_LAUNCH);
-                st = 2;
-            } else {
-                st = f & 3;
-                got = true;
-            }
-        }
-        const uint64_t incl = __ballot(st == 2);
-        const uint32_t first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+    if (t == 0) sh[NW] = fa_empty();  // the aggregate so far (sh, shf: NW + 1 entries)
+    __syncthreads();
+    while (!done) {  // block-uniform
+        const long long p = base - (long long)(wave * 64 + lane);
+        bool isinc = true;  // before position 0: nothing (an empty inclusive prefix)
         FoldAgg v = fa_empty();
-        if (got && lane < first) v = lb[p].agg;
-        else if (got && lane == first) v = lb[p].inc;
+        if (p >= 0) {
+            FoldAgg g;
+            bool ok = false;
+            uint32_t it = 0;
+#pragma unroll 1
+            for (;;) {  // the inclusive prefix if it is there, else the aggregate
+                if (fc_get(lb[p].inc, epoch, g)) { isinc = true; ok = true; break; }
+                if (fc_get(lb[p].agg, epoch, g)) { isinc = false; ok = true; break; }
+                if (++it >= kFcSpinMax) break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (!ok) {
+                atomicOr(status, FLTEE_DEV_ERR_LAUNCH);
+                g = fa_empty();
+                isinc = true;
+            }
+            v = g;
+        }
+        const uint64_t incl = __ballot(isinc);
+        const uint32_t first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+        if (lane > first) v = fa_empty();
         // the window's lanes in position order: a higher lane is an older piece
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const FoldAgg older = fa_shfl_down(v, o);
             if ((lane & (2 * o - 1)) == 0) v = fa_combine(older, v);
         }
-        FoldAgg w;  // lane 0's: the window in order
-        w.F = (uint32_t)__shfl((int)v.F, 0);
-        w.K = (uint32_t)__shfl((int)v.K, 0);
-        w.Q = __shfl(v.Q, 0);
-        w.fl = (uint32_t)__shfl((int)v.fl, 0);
-        run = fa_combine(w, run);
-        done = first < 64;
-        base -= 64;
+        if (lane == 0) {
+            sh[wave] = v;
+            shf[wave] = first < 64;
+        }
+        __syncthreads();
+        // thread 0: the windows from the newest (wave 0) back to the first with an inclusive
+        // prefix, in front of what the rounds before found
+        if (t == 0) {
+            FoldAgg blk = fa_empty();
+            uint32_t found = 0;
+#pragma unroll 1
+            for (int w = 0; w < NW && !found; ++w) {
+                blk = fa_combine(sh[w], blk);
+                found = shf[w];
+            }
+            sh[NW] = fa_combine(blk, sh[NW]);
+            shf[NW] = found;
+        }
+        __syncthreads();
+        done = shf[NW] != 0;
+        base -= 64 * NW;
     }
+    const FoldAgg run = sh[NW];
+    __syncthreads();  // sh[] is reused by the next tile
     return run;
 }
 
@@ -737,13 +781,16 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                                                             uint32_t lim, FcLb *lb, uint32_t epoch,
                                                             uint32_t *status) {
     constexpr uint32_t CAP = (uint32_t)NT * PER;
-    constexpr int CH = PER + XMAX;  // the most window slots one lane owns
     constexpr int NW = NT / 64;
     // XMAX: window slots beyond CAP per lane, ceil((Hr + 1) / NT)
     extern __shared__ __attribute__((aligned(16))) uint64_t win[];  // Hr + CAP + 1, then the sums
     __shared__ FoldAgg wtot[NW];
-    __shared__ float red[NW];
-    __shared__ FoldAgg wc_s;
+    __shared__ FoldAgg agg_s;
+    __shared__ FoldAgg lb_sh[NW + 1];
+    __shared__ uint32_t lb_shf[NW + 1];
+    __shared__ float exq[NT];
+    __shared__ bool exf[NT];
+    __shared__ uint32_t fix_s, kw0_s;
     const uint32_t H = (1u << G) - 1;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t Wn = Hr + CAP + 1;
@@ -778,31 +825,18 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         const uint32_t next = tile + gridDim.x;
         if (FLTEE_FC_PF && (!FLTEE_CP_SKIP_SELF || next < ntiles))
             prefetch(next < ntiles ? next : tile);  // lands while this tile folds and compacts
-        // the tile's piece (window slots [0, S)): the run ending it, its values summed in
-        // any order (a carry is re-associated anyway)
-        {
-            const uint32_t kS = (uint32_t)win[S - 1];
-            float qp = 0.0f;
-#pragma unroll
-            for (uint32_t i = 0; i < PER; ++i) {
-                const uint32_t y = t + i * NT;
-                if (y < S) {
-                    const uint64_t r = win[y];
-                    qp = (uint32_t)r == kS ? __fadd_rn(qp, rec_val(r)) : qp;
-                }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) qp = __fadd_rn(qp, __shfl_down(qp, o));
-            if (lane == 0) red[wave] = qp;
-        }
         // Each lane owns window slots [x0, x0 + chunk) and computes, for each, the
         // in-order sum of its run up to that slot: a walk from x0 - lim (every run of <= lim
         // entries of an owned slot starts after it), lim + chunk steps whatever the data, no
         // branch, the next slot's LDS read issued a step ahead.  The sums go to their own
         // LDS array (sums[], after the window), so no lane overwrites what another still
         // reads; a run's last slot then holds the run's sum — all the compaction reads.
+        // Over its own slots the walk also keeps the run partials from x0 (loc[]) and the
+        // lane's segmented aggregate, for the runs longer than the walk (see above).
         float *sums = reinterpret_cast<float *>(win + Wn);
+        float *loc = sums + Wn;
         const int x0 = (int)(t * chunk), ys = x0 - (int)lim;
+        FoldAgg ca = fa_empty();
         {
             const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
             auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
@@ -826,51 +860,29 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 rn = rd(ys + (int)q + 1);
                 step(r, ys + (int)q);
             }
+            uint32_t kl = 0;
+            float acc2 = 0.0f;
+            bool unb = true;
             for (uint32_t i = 0; i < chunk; ++i) {
                 const int y = x0 + (int)i;
                 const uint64_t r = rn;
                 rn = rd(y + 1);
                 step(r, y);
-                if (y < (int)Wn) sums[y] = acc;
-            }
-        }
-        __syncthreads();
-        if (t == 0) {  // publish the piece's aggregate
-            float q = 0.0f;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) q = __fadd_rn(q, red[w]);
-            FoldAgg g;
-            g.F = (uint32_t)win[0];
-            g.K = (uint32_t)win[S - 1];
-            g.Q = q;
-            g.fl = kFsPiece | (g.F == g.K ? kFsFull : 0u);
-            lb[tile].agg = g;
-            __hip_atomic_store(&lb[tile].flag, (epoch << 2) | 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // the lane's own slots again: the aggregate of their run partials from x0
-        FoldAgg ca = fa_empty();
-        const uint32_t k0 = x0 < (int)Wn ? (uint32_t)win[x0] : 0u;
-        {
-            uint32_t pk = k0;
-            float acc = 0.0f;
-            bool unb = true;
-#pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const int y = x0 + i;
-                if ((uint32_t)i < chunk && y < (int)Wn) {
-                    const uint64_t r = win[y];
-                    const uint32_t ky = (uint32_t)r;
-                    const bool cont = i > 0 && ky == pk;
-                    acc = cont ? __fadd_rn(acc, rec_val(r)) : rec_val(r);
-                    unb = unb && (i == 0 || cont);
-                    pk = ky;
+                const bool in = y < (int)Wn;
+                const uint32_t ky = (uint32_t)r;
+                const bool c2 = i > 0 && ky == kl;
+                acc2 = in ? (c2 ? __fadd_rn(acc2, rec_val(r)) : rec_val(r)) : acc2;
+                unb = unb && (!in || i == 0 || c2);
+                kl = in ? ky : kl;
+                if (in) {
+                    sums[y] = acc;
+                    loc[y] = acc2;
                 }
             }
             if (x0 < (int)Wn) {
-                ca.F = k0;
-                ca.K = pk;
-                ca.Q = acc;
+                ca.F = (uint32_t)win[x0];
+                ca.K = kl;
+                ca.Q = acc2;
                 ca.fl = kFsPiece | (unb ? kFsFull : 0u);
             }
         }
@@ -884,49 +896,40 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         if (lane == 0) wex = fa_empty();
         if (lane == 63) wtot[wave] = inc;
         __syncthreads();
-        if (wave == 0) {  // the carry from in front of the window
-            const FoldAgg wc = fc_lookback(lb, tile, epoch, lane, status);
-            if (lane == 0) {
-                wc_s = wc;
-                lb[tile].inc = fa_combine(wc, lb[tile].agg);
-                __hip_atomic_store(&lb[tile].flag, (epoch << 2) | 2u, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        {  // the window-local run prefix of every owned slot, into the slot's val
+        // the lane's exclusive aggregate within the window: the run partial in front of x0
+        {
             FoldAgg ex = fa_empty();
             for (uint32_t w = 0; w < wave; ++w) ex = fa_combine(ex, wtot[w]);
             ex = fa_combine(ex, wex);
-            const bool ec = (ex.fl & kFsPiece) && ex.K == k0;
-            // the key in front of this lane's walk: a run holding it began before the walk
-            // (more than lim entries) and takes the window-local prefix, else the walk's sum
-            const uint32_t kys = ys > 0 ? (uint32_t)win[ys - 1] : 0u;
-            uint32_t pk = k0;
-            float acc = 0.0f;
-#pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const int y = x0 + i;
-                if ((uint32_t)i < chunk && y < (int)Wn) {
-                    const uint64_t r = win[y];
-                    const uint32_t ky = (uint32_t)r;
-                    acc = (i > 0 && ky == pk) ? __fadd_rn(acc, rec_val(r)) : rec_val(r);
-                    pk = ky;
-                    const float wl = (ec && ky == k0) ? __fadd_rn(ex.Q, acc) : acc;
-                    const float v = (ys > 0 && kys == ky) ? wl : sums[y];
-                    win[y] = ((uint64_t)__float_as_uint(v) << 32) | ky;
-                }
+            const uint32_t k0 = x0 < (int)Wn ? (uint32_t)win[x0] : 0u;
+            exq[t] = ex.Q;
+            exf[t] = (ex.fl & kFsPiece) && ex.K == k0;
+            if (t == 0) {
+                fix_s = 0xFFFFFFFFu;
+                kw0_s = (uint32_t)win[0];
+            }
+            // the piece [0, S) of this tile: published by the lane owning its last slot
+            if ((uint32_t)x0 <= S - 1 && S - 1 < (uint32_t)x0 + chunk) {
+                const uint32_t kS = (uint32_t)win[S - 1];
+                FoldAgg part;
+                part.F = k0;
+                part.K = kS;
+                part.Q = loc[S - 1];
+                part.fl = kFsPiece | (k0 == kS ? kFsFull : 0u);
+                const FoldAgg g = fa_combine(ex, part);
+                fc_put(lb[tile].agg, g, epoch);
+                agg_s = g;
             }
         }
-        __syncthreads();
-        // representatives with idx < d -> (c = p - idx, sum); the rest never move.  A slot
-        // holds its run's sum from the window's start on (the walk's, bit for bit, or the
-        // re-associated window-local prefix for a run longer than its walk); a run begun
-        // before the window adds the carry.
+        // representatives with idx < d -> (c = p - idx, sum); the rest never move.  A run
+        // that began before its owner lane's walk (more than lim entries) takes the
+        // re-associated window-local prefix (the owner's partial in front of its slots +
+        // loc); the carry from before the window is added after the levels (below), to the
+        // one record it concerns: the window's head run's, wherever the levels took it.
         uint64_t v[PER];
         {
-            const FoldAgg wc = wc_s;
             const uint32_t kw0 = (uint32_t)win[0];
-            const bool wok = (wc.fl & kFsPiece) && wc.K == kw0;
+            const uint32_t gm = (1u << G) - 1;
 #pragma unroll
             for (uint32_t i = 0; i < PER; ++i) {
                 const uint32_t f = t + i * NT, x = f + Hr;
@@ -934,11 +937,15 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 const uint64_t r = win[x];
                 const uint32_t idx = (uint32_t)r;
                 const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-                const float wv = rec_val(r);
-                const float hv = (wok && idx == kw0) ? __fadd_rn(wc.Q, wv) : wv;
-                v[i] = (p < (long long)L && idx < d && end)
-                           ? (((uint64_t)__float_as_uint(hv) << 32) | (uint32_t)((uint32_t)p - idx))
-                           : CP_DUMMY;
+                const uint32_t o = x / chunk, xo = o * chunk;  // x's owner lane, its first slot
+                const int yso = (int)xo - (int)lim;
+                const bool lng = yso > 0 && (uint32_t)win[yso - 1] == idx;
+                const float wl = (exf[o] && idx == (uint32_t)win[xo]) ? __fadd_rn(exq[o], loc[x]) : loc[x];
+                const float hv = lng ? wl : sums[x];
+                const bool rep = p < (long long)L && idx < d && end;
+                const uint32_t c = (uint32_t)p - idx;
+                v[i] = rep ? (((uint64_t)__float_as_uint(hv) << 32) | c) : CP_DUMMY;
+                if (rep && idx == kw0) fix_s = f - (c & gm);  // its slot after the G levels
             }
         }
         __syncthreads();
@@ -987,15 +994,27 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             __syncthreads();
             g += two ? 2 : 1;
         }
+        // the carry from in front of the window (decoupled look-back; FLTEE_FC_LB=0: none,
+        // an A/B of its cost only) into the window head run's record, if it began before
+        FoldAgg wc = fa_empty();
+        if (FLTEE_FC_LB) {
+            wc = fc_lookback<NW>(lb, tile, epoch, t, status, lb_sh, lb_shf);
+            if (t == 0) fc_put(lb[tile].inc, fa_combine(wc, agg_s), epoch);
+        }
+        const bool wok = (wc.fl & kFsPiece) && wc.K == kw0_s;
+        const uint32_t fx = fix_s;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) {
             const uint32_t f = t + i * NT;
             if (f < S) {
                 const long long p = a + f;
+                uint64_t rv = sm[f];
+                const float fv = __fadd_rn(wc.Q, rec_val(rv));
+                rv = (wok && f == fx) ? ((rv & 0xFFFFFFFFull) | ((uint64_t)__float_as_uint(fv) << 32)) : rv;
                 if (FINAL == 0) {
-                    if (p < (long long)L) dst[p] = sm[f];
+                    if (p < (long long)L) dst[p] = rv;
                 } else if (p < (long long)d) {
-                    const float vv = cp_out(sm[f]);
+                    const float vv = cp_out(rv);
                     out[p] = FINAL == 2 ? __fadd_rn(out[p], vv) : __fmul_rn(vv, coef);
                 }
             }
@@ -1099,11 +1118,10 @@ static bool fc_shape(size_t M, size_t L, size_t d, size_t halo, FcShape &o) {
     const uint32_t CAP = NT * o.per;
     o.S = CAP - H;
     o.ntiles = (L + o.S - 1) / o.S;
-    // the window and the run sums beside it; the resident blocks per CU must fit the
-    // 160 KiB LDS at the largest window
-    const size_t lds = (o.Hr + CAP + 1) * 12;
-    static_assert(FLTEE_FC_BLOCKS * (1023 + 8 * 512 + 1) * 8 <= 160 * 1024, "fused fold LDS per CU");
-    return lds * FLTEE_FC_BLOCKS <= 160 * 1024;
+    // the window, the walks' run sums and the run partials beside it; the resident blocks
+    // per CU must fit the 160 KiB LDS (lim <= 320: 71 KiB a block)
+    const size_t lds = (o.Hr + CAP + 1) * 16;
+    return lds * FLTEE_FC_BLOCKS <= 160 * 1024 && lds <= 80 * 1024;
 }
 
 size_t fc_lookback_bytes(size_t M, size_t L, size_t d, size_t halo) {
@@ -1123,7 +1141,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const uint32_t nlev = bitlen(L - d);
     const uint32_t CAP = NT * o.per;
     const bool last = o.G == nlev;
-    const size_t lds = (o.Hr + CAP + 1) * 12;
+    const size_t lds = (o.Hr + CAP + 1) * 16;
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
     const bool x1 = o.Hr + 1 <= NT;  // one window slot past CAP per lane, else two
     const int F = !last ? 0 : (accumulate ? 2 : 1);

@@ -192,13 +192,14 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             in_head = in_head && !hend && !copy;
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
-            if (q >= 0 && qg >= 0) {
-                if (!started) {  // the walk's first position (b, or 0 at the array's start)
-                    pf_key = ci;
-                    in_head = hasprev && ci == kprev;
-                } else {
-                    unbroken = unbroken && eq;
-                }
+            // (value selects, one assignment each: a store through a selected address
+            // would put these flags on the stack)
+            const bool valid = q >= 0 && qg >= 0;
+            const bool first = valid && !started;  // the walk's first position (b, or 0)
+            pf_key = first ? ci : pf_key;
+            in_head = first ? (hasprev && ci == kprev) : in_head;
+            unbroken = (valid && started) ? (unbroken && eq) : unbroken;
+            if (valid) {
                 pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
                 pre_idx = ci;
                 started = true;
@@ -235,16 +236,36 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         for (int q = 0; q < DEPTH; ++q)
             if (s + (uint32_t)q < nstage) stage(pf[q], s + (uint32_t)q);
     }
-    if (side && a < end) {
-        const uint32_t fl = (piece ? kFsPiece : 0u) | (pfull ? kFsFull : 0u) |
-                            (corr ? kFsCorr : 0u);
-        FoldSide *o = side + (size_t)blockIdx.x * 64 + l;
-        o->F = pf_key;
-        o->K = pk;
-        o->Q = pq;
-        o->fl = fl;
-        o->ck = ck;
-        o->S = cs;
+    if (side) {
+        const bool live = a < end;
+        const uint32_t fl = live ? ((piece ? kFsPiece : 0u) | (pfull ? kFsFull : 0u) |
+                                    (corr ? kFsCorr : 0u))
+                                 : 0u;
+        if (live) {
+            FoldSide *o = side + (size_t)blockIdx.x * 64 + l;
+            o->F = pf_key;
+            o->K = pk;
+            o->Q = pq;
+            o->fl = fl;
+            o->ck = ck;
+            o->S = cs;
+        }
+        // the wave's aggregate of its 64 pieces (in lane order), for the patch's carries
+        FoldAgg g;
+        g.F = pf_key;
+        g.K = pk;
+        g.Q = pq;
+        g.fl = fl & (kFsPiece | kFsFull);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            FoldAgg y;
+            y.F = (uint32_t)__shfl_up((int)g.F, o);
+            y.K = (uint32_t)__shfl_up((int)g.K, o);
+            y.Q = __shfl_up(g.Q, o);
+            y.fl = (uint32_t)__shfl_up((int)g.fl, o);
+            if (l >= (uint32_t)o) g = fa_combine(y, g);
+        }
+        if (l == 63) fold_wave_aggs(side, gridDim.x)[blockIdx.x] = g;
     }
 }
 
@@ -332,29 +353,18 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
 }
 
 // ---- the long-run patch (see the header) ----------------------------------------
-// One block of 1024 threads over the G lanes' side records: thread t takes lanes
-// [t * per, (t + 1) * per); an exclusive block scan of the threads' aggregates, the
-// carry from the ranges before (prev[0, nprev): their totals, in order) in front.
-// PATCH: dst[a_j] for every lane j (read, then written back or replaced: fixed
-// addresses); else: *total = the aggregate of all G pieces.
-constexpr int kFpNT = 1024;
-template <bool PATCH, bool CEMIT>
-__global__ __launch_bounds__(kFpNT) void fold_patch_kernel(const FoldSide *__restrict__ side,
-                                                           uint32_t G, uint64_t *__restrict__ dst,
-                                                           long long origin, uint32_t C,
-                                                           long long pbase,
-                                                           const FoldAgg *__restrict__ prev,
-                                                           uint32_t nprev, FoldAgg *total,
-                                                           uint32_t dsel, uint64_t cdummy) {
-    __shared__ FoldAgg part[kFpNT];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (G + kFpNT - 1) / kFpNT;
-    const uint32_t j0 = t * per, j1 = min(j0 + per, G);
-    FoldAgg acc = fa_empty();
-    for (uint32_t j = j0; j < j1; ++j) acc = fa_combine(acc, fa_of(side[j]));
-    part[t] = acc;
+// The patch: lanes of 1,024 per block (256 threads x 4).  A block's carry = the totals of
+// the ranges before (prev[0, nprev), in order) then the wave aggregates of every wave in
+// front of its lanes (the fold kernel's, 64 lanes each; read in slices by the block's
+// threads, combined in order by a block scan), then its own lanes' exclusive scan.
+// PATCH: dst[a_j] for every lane j (read, then written back or replaced: fixed addresses);
+// else (one block): *total = the aggregate of all the waves.
+constexpr int kFpNT = 256, kFpPer = 4, kFpLanes = kFpNT * kFpPer;
+
+// the inclusive scan of part[0, kFpNT) in LDS (x before y: order kept); returns part[t]
+__device__ FoldAgg fp_block_scan(FoldAgg *part, uint32_t t, FoldAgg v) {
+    part[t] = v;
     __syncthreads();
-    // Hillis-Steele inclusive scan over the 1024 thread aggregates (order kept: x before y)
     for (uint32_t o = 1; o < kFpNT; o <<= 1) {
         const FoldAgg y = part[t];
         const FoldAgg x = t >= o ? part[t - o] : fa_empty();
@@ -362,42 +372,85 @@ __global__ __launch_bounds__(kFpNT) void fold_patch_kernel(const FoldSide *__res
         part[t] = fa_combine(x, y);
         __syncthreads();
     }
+    return part[t];
+}
+
+template <bool PATCH, bool CEMIT>
+__global__ __launch_bounds__(kFpNT) void fold_patch_kernel(const FoldSide *__restrict__ side,
+                                                           uint32_t G, uint32_t W,
+                                                           uint64_t *__restrict__ dst,
+                                                           long long origin, uint32_t C,
+                                                           long long pbase,
+                                                           const FoldAgg *__restrict__ prev,
+                                                           uint32_t nprev, FoldAgg *total,
+                                                           uint32_t dsel, uint64_t cdummy) {
+    __shared__ FoldAgg part[kFpNT];
+    const uint32_t t = threadIdx.x;
+    const FoldAgg *wagg = fold_wave_aggs(const_cast<FoldSide *>(side), W);
+    // the waves in front of this block's lanes (all of them for the total)
+    const uint32_t wb = PATCH ? blockIdx.x * (kFpLanes / 64) : W;
+    FoldAgg acc = fa_empty();
+    {
+        const uint32_t w0 = (uint32_t)((uint64_t)wb * t / kFpNT);
+        const uint32_t w1 = (uint32_t)((uint64_t)wb * (t + 1) / kFpNT);
+        for (uint32_t w = w0; w < w1; ++w) acc = fa_combine(acc, wagg[w]);
+    }
+    const FoldAgg front = fp_block_scan(part, t, acc), allw = part[kFpNT - 1];
+    (void)front;
     if constexpr (!PATCH) {
-        if (t == 0) *total = part[kFpNT - 1];
+        if (t == 0) *total = allw;
         return;
     } else {
-        FoldAgg run = fa_empty();
-        for (uint32_t i = 0; i < nprev; ++i) run = fa_combine(run, prev[i]);
-        if (t > 0) run = fa_combine(run, part[t - 1]);
-        for (uint32_t j = j0; j < j1; ++j) {
-            const FoldSide sd = side[j];
+        FoldAgg carry = fa_empty();
+        for (uint32_t i = 0; i < nprev; ++i) carry = fa_combine(carry, prev[i]);
+        carry = fa_combine(carry, allw);
+        __syncthreads();  // part[] is reused
+        const uint32_t j0 = blockIdx.x * kFpLanes + t * kFpPer;
+        FoldSide sd[kFpPer];
+        FoldAgg mine = fa_empty();
+#pragma unroll
+        for (int i = 0; i < kFpPer; ++i) {
+            if (j0 + i < G) {
+                sd[i] = side[j0 + i];
+                mine = fa_combine(mine, fa_of(sd[i]));
+            }
+        }
+        const FoldAgg inc = fp_block_scan(part, t, mine);
+        (void)inc;
+        FoldAgg run = fa_combine(carry, t > 0 ? part[t - 1] : fa_empty());
+#pragma unroll
+        for (int i = 0; i < kFpPer; ++i) {
+            const uint32_t j = j0 + i;
+            if (j >= G) break;
             const long long aj = origin + (long long)j * C;
             const uint64_t was = dst[aj];
             // a lane with a run begun before its walk: the run's key is the one in front of
             // the walk, the last key of the pieces before (run.K)
-            const bool c = (sd.fl & kFsCorr) && (run.fl & kFsPiece) && run.K == sd.ck;
-            const float tot = __fadd_rn(run.Q, sd.S);
+            const bool c = (sd[i].fl & kFsCorr) && (run.fl & kFsPiece) && run.K == sd[i].ck;
+            const float tot = __fadd_rn(run.Q, sd[i].S);
             uint64_t rec;
             if constexpr (CEMIT)
-                rec = sd.ck < dsel ? make_rec((uint32_t)(aj + pbase) - sd.ck, tot) : cdummy;
+                rec = sd[i].ck < dsel ? make_rec((uint32_t)(aj + pbase) - sd[i].ck, tot) : cdummy;
             else
-                rec = make_rec(sd.ck, tot);
+                rec = make_rec(sd[i].ck, tot);
             dst[aj] = c ? rec : was;
-            run = fa_combine(run, fa_of(sd));
+            run = fa_combine(run, fa_of(sd[i]));
         }
     }
 }
 
 size_t fold_side_bytes(size_t span, size_t fold_len, size_t halo, size_t origin, long long pbase) {
-    return fold_lanes(span, fold_len, halo, origin, pbase) * sizeof(FoldSide);
+    const size_t waves = (fold_lanes(span, fold_len, halo, origin, pbase) + 63) / 64;
+    return waves * (64 * sizeof(FoldSide) + sizeof(FoldAgg));
 }
 
 hipError_t launch_fold_range_total(const FoldSide *side, size_t lanes, FoldAgg *total,
                                    hipStream_t s) {
-    if (lanes > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const size_t waves = (lanes + 63) / 64;
+    if (waves > 0xFFFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fold_patch_kernel<false, false>), dim3(1), dim3(kFpNT), 0, s, side,
-                       (uint32_t)lanes, (uint64_t *)nullptr, 0ll, 0u, 0ll, (const FoldAgg *)nullptr,
-                       0u, total, 0u, 0ull);
+                       (uint32_t)lanes, (uint32_t)waves, (uint64_t *)nullptr, 0ll, 0u, 0ll,
+                       (const FoldAgg *)nullptr, 0u, total, 0u, 0ull);
     return hipGetLastError();
 }
 
@@ -409,15 +462,18 @@ hipError_t launch_fold_range_patch(uint64_t *dst, size_t span, size_t origin, lo
     if (lanes == 0) return hipSuccess;  // the one-lane walk: nothing to patch
     if (lanes > 0xFFFFFFFFull || nprev > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const size_t C = fold_chunk(span, fold_context(halo));
+    const size_t waves = (lanes + 63) / 64;
+    const unsigned blocks = (unsigned)((lanes + kFpLanes - 1) / kFpLanes);
     net_account((uint64_t)sizeof(FoldSide) * lanes + 16 * lanes, "fold_patch_kernel", s);
     if (cemit_d)
-        hipLaunchKernelGGL((fold_patch_kernel<true, true>), dim3(1), dim3(kFpNT), 0, s, side,
-                           (uint32_t)lanes, dst, (long long)origin, (uint32_t)C, pbase, prev,
-                           (uint32_t)nprev, (FoldAgg *)nullptr, (uint32_t)cemit_d, cdummy);
+        hipLaunchKernelGGL((fold_patch_kernel<true, true>), dim3(blocks), dim3(kFpNT), 0, s, side,
+                           (uint32_t)lanes, (uint32_t)waves, dst, (long long)origin, (uint32_t)C,
+                           pbase, prev, (uint32_t)nprev, (FoldAgg *)nullptr, (uint32_t)cemit_d,
+                           cdummy);
     else
-        hipLaunchKernelGGL((fold_patch_kernel<true, false>), dim3(1), dim3(kFpNT), 0, s, side,
-                           (uint32_t)lanes, dst, (long long)origin, (uint32_t)C, pbase, prev,
-                           (uint32_t)nprev, (FoldAgg *)nullptr, 0u, 0ull);
+        hipLaunchKernelGGL((fold_patch_kernel<true, false>), dim3(blocks), dim3(kFpNT), 0, s, side,
+                           (uint32_t)lanes, (uint32_t)waves, dst, (long long)origin, (uint32_t)C,
+                           pbase, prev, (uint32_t)nprev, (FoldAgg *)nullptr, 0u, 0ull);
     return hipGetLastError();
 }
 
