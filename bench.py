@@ -70,6 +70,12 @@ def compact_line(full):
     cb = full.get("cpu_baseline")
     if cb:
         line["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("value", "unit", "cores", "kind", "sample")}
+        # cores = the threads the timed restatement used (the enclave had one TCS); the host
+        # it ran on, beside it (north_star: "core count stated")
+        host = cb.get("host") or {}
+        line["cpu_baseline"]["host_cores"] = host.get("logical_cpus")
+        line["cpu_baseline"]["host_cores_available"] = host.get("cpus_available_to_process")
+        line["cpu_baseline"]["host_model"] = host.get("model")
     e2e = full.get("e2e_host_inclusive")
     if e2e:
         line["e2e_host_inclusive"] = {"value": _r(e2e["value"]), "ms_per_call": _r(e2e["ms_per_call"]),

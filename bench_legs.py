@@ -200,7 +200,8 @@ def rocprof_kernel(name, kernel):
     config (profiles/r0N/<name>_kernel_stats.csv, newest round first), for the
     cross-check, or None."""
     import csv
-    paths = [os.path.join(ROOT, "profiles", r, f"{name}_kernel_stats.csv") for r in ("r04", "r03")]
+    paths = [os.path.join(ROOT, "profiles", r, f"{name}_kernel_stats.csv")
+             for r in ("r06", "r05", "r04", "r03")]
     path = next((p for p in paths if os.path.exists(p)), paths[-1])
     try:
         with open(path) as f:

@@ -79,6 +79,57 @@ static inline uint32_t log2_pow2(size_t x) {
     return l;
 }
 
+// ---- the launch trace (obliviousness tests) ---------------------------------------
+// Every kernel launch, copy, memset and host synchronisation of the library goes through
+// these (tests/test_abi.py rejects a raw hipLaunchKernelGGL / hipMemcpy* / hipMemset* /
+// hip*Synchronize in csrc/): with fltee_debug_trace(1) each appends one line — what, the
+// call site (the kernel expression as written), grid / block / LDS or the byte count — to
+// a process-wide log that tests/test_gpu_oblivious.py compares between inputs of the same
+// public sizes.  Off (the default), a relaxed load per call.
+namespace fltee {
+bool trace_on();
+void trace_event(const char *what, const char *site, uint64_t a, uint64_t b, uint64_t c);
+}  // namespace fltee
+#define FLTEE_LAUNCH(K, GRID, BLOCK, LDS, S, ...)                                              \
+    do {                                                                                       \
+        const dim3 fltee_g_ = dim3(GRID), fltee_b_ = dim3(BLOCK);                              \
+        if (::fltee::trace_on())                                                               \
+            ::fltee::trace_event("launch", #K, ((uint64_t)fltee_g_.x << 32) | fltee_g_.y,      \
+                                 ((uint64_t)fltee_g_.z << 32) | fltee_b_.x, (uint64_t)(LDS));  \
+        hipLaunchKernelGGL(K, fltee_g_, fltee_b_, LDS, S, __VA_ARGS__);                        \
+    } while (0)
+namespace fltee {
+inline hipError_t fl_memcpy_async(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st) {
+    if (trace_on()) trace_event("memcpy", "", n, (uint64_t)k, 0);
+    return hipMemcpyAsync(d, s, n, k, st);
+}
+inline hipError_t fl_memcpy2d_async(void *d, size_t dp, const void *s, size_t sp, size_t w, size_t h,
+                                    hipMemcpyKind k, hipStream_t st) {
+    if (trace_on()) trace_event("memcpy2d", "", w, h, (uint64_t)k);
+    return hipMemcpy2DAsync(d, dp, s, sp, w, h, k, st);
+}
+inline hipError_t fl_memcpy(void *d, const void *s, size_t n, hipMemcpyKind k) {
+    if (trace_on()) trace_event("memcpy_sync", "", n, (uint64_t)k, 0);
+    return hipMemcpy(d, s, n, k);
+}
+inline hipError_t fl_memset_async(void *d, int v, size_t n, hipStream_t st) {
+    if (trace_on()) trace_event("memset", "", n, (uint64_t)(uint32_t)v, 0);
+    return hipMemsetAsync(d, v, n, st);
+}
+inline hipError_t fl_memset(void *d, int v, size_t n) {
+    if (trace_on()) trace_event("memset_sync", "", n, (uint64_t)(uint32_t)v, 0);
+    return hipMemset(d, v, n);
+}
+inline hipError_t fl_stream_sync(hipStream_t st) {
+    if (trace_on()) trace_event("sync", "stream", 0, 0, 0);
+    return hipStreamSynchronize(st);
+}
+inline hipError_t fl_device_sync() {
+    if (trace_on()) trace_event("sync", "device", 0, 0, 0);
+    return hipDeviceSynchronize();
+}
+}  // namespace fltee
+
 // ---- kernel launchers (implemented in the k_*.hip files) ------------------
 namespace fltee {
 

@@ -132,7 +132,7 @@ static uint32_t load_and_decrypt(DeviceCtx *c, const uint32_t *ids, size_t n, co
         return FLTEE_ERROR_OUT_OF_MEMORY;
     std::vector<uint32_t> rk;
     client_round_keys(ids, n, rk);
-    if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    if (fl_memcpy_async(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     size_t per = bpc ? kLoadChunkBytes / bpc : n;
     if (per == 0) per = 1;
@@ -141,7 +141,7 @@ static uint32_t load_and_decrypt(DeviceCtx *c, const uint32_t *ids, size_t n, co
     int ev = 0;
     for (size_t c0 = 0; c0 < n && bpc; c0 += per, ++ev) {
         const size_t nc = c0 + per < n ? per : n - c0;
-        if (hipMemcpyAsync((uint8_t *)c->cipher.ptr + c0 * bpc, enc + c0 * bpc, nc * bpc,
+        if (fl_memcpy_async((uint8_t *)c->cipher.ptr + c0 * bpc, enc + c0 * bpc, nc * bpc,
                            hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
             hipEventRecord(c->copy_ev[ev], c->copy_stream) != hipSuccess ||
             hipStreamWaitEvent(c->stream, c->copy_ev[ev], 0) != hipSuccess)
@@ -150,18 +150,18 @@ static uint32_t load_and_decrypt(DeviceCtx *c, const uint32_t *ids, size_t n, co
                            (uint8_t *)c->records.ptr + c0 * rpc * 8, c->stream) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
     }
-    if (hipStreamSynchronize(c->copy_stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (fl_stream_sync(c->copy_stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     const double t1 = now_s();
     if (t_load) *t_load = (float)(t1 - t0);
     // rk lives on this stack frame: the decrypt (and the key upload) must finish here
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (fl_stream_sync(c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     if (t_dec) *t_dec = (float)(now_s() - t1);
     return FLTEE_SUCCESS;
 }
 
 static uint32_t read_status(DeviceCtx *c, uint32_t *st) {
-    if (hipMemcpyAsync(st, c->status, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    if (fl_memcpy_async(st, c->status, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        fl_stream_sync(c->stream) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     return FLTEE_SUCCESS;
 }
@@ -223,7 +223,7 @@ static uint32_t aggregate_records(DeviceCtx *c, uint32_t alg, size_t n, size_t r
     fltee_device_opts o = ecall_opts(alg, n, rpc, d, k_req, batch, seed);
     if (alg == FLTEE_ALG_OPTIMIZED) o.flags &= ~FLTEE_OPT_K_REQ;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        if (hipMemsetAsync(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        if (fl_memset_async(c->status, 0, 4, c->stream) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         uint32_t st = aggregate(alg, c->records.ptr, n, rpc, d, d_out, o, c->stream, c->status);
         if (st != FLTEE_SUCCESS) return st;
         uint32_t dev_st = 0;
@@ -266,7 +266,7 @@ static hipError_t launch_copy_out(const void *src, void *dst, size_t bytes, hipS
     const size_t n16 = (bytes + 15) / 16;  // both ends 16-B aligned, padded
     size_t blocks = (n16 + 255) / 256;
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(copy_out_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4 *)src,
+    FLTEE_LAUNCH(copy_out_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4 *)src,
                        (uint4 *)dst, n16);
     return hipGetLastError();
 }
@@ -299,15 +299,15 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     const uint8_t *d_cipher = zero_copy ? (const uint8_t *)d_rk + rkb : stage + d4 + 16;
     // (no H2D to time on the zero-copy path: no marker in front of the first kernel)
     if ((!zero_copy && hipEventRecord(c->call_ev[0], s) != hipSuccess) ||
-        (!zero_copy && hipMemcpyAsync(stage + d4 + 16, enc, cb, hipMemcpyHostToDevice, s) != hipSuccess) ||
-        (!cb && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess))
+        (!zero_copy && fl_memcpy_async(stage + d4 + 16, enc, cb, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (!cb && fl_memset_async(d_st, 0, 4, s) != hipSuccess))
         return FLTEE_ERROR_UNEXPECTED;
     fltee_device_opts o = ecall_opts(alg == FLTEE_ALG_OPTIMIZED ? FLTEE_ALG_ADVANCED : alg, n, rpc, d,
                                      k_req, batch, seed);
     if (alg == FLTEE_ALG_OPTIMIZED) o.flags &= ~FLTEE_OPT_K_REQ;
     // the call's device work: AES (timed by events) -> aggregation (-> DP) -> copy-out
     auto enqueue = [&](bool retry_pass) -> uint32_t {
-        if (retry_pass && hipMemsetAsync(d_st, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        if (retry_pass && fl_memset_async(d_st, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         if (!retry_pass &&
             (hipEventRecord(c->call_ev[1], s) != hipSuccess ||
              (cb && launch_aes_ctr(d_cipher, n, bpc, rpc, d_rk, (uint8_t *)c->records.ptr, s, d_st) !=
@@ -329,7 +329,7 @@ static uint32_t staged_ecall(DeviceCtx *c, uint32_t alg, const uint32_t *ids, si
     for (int attempt = 0; attempt < 2; ++attempt) {
         st = enqueue(attempt > 0);
         if (st != FLTEE_SUCCESS) return st;
-        if (hipStreamSynchronize(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+        if (fl_stream_sync(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
         bool retry = false;
         st = status_to_retval(*(const volatile uint32_t *)((const uint8_t *)c->pin_out.ptr + d4), alg,
                               &retry);
@@ -402,7 +402,7 @@ extern "C" fltee_status_t fltee_device_fini(fltee_eid_t eid) {
         group_destroy(G);
         g_groups.erase(eid);
     }
-    if (hipSetDevice(dev) == hipSuccess) (void)hipDeviceSynchronize();
+    if (hipSetDevice(dev) == hipSuccess) (void)fl_device_sync();
     return FLTEE_SUCCESS;
 }
 
@@ -590,9 +590,9 @@ extern "C" fltee_status_t ecall_secure_aggregation(
         if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
             st = FLTEE_ERROR_UNEXPECTED;
     }
-    if (!st && hipMemcpyAsync(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    if (!st && fl_memcpy_async(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         st = FLTEE_ERROR_UNEXPECTED;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
+    if (fl_stream_sync(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
     if (st) {
         std::memset(updated_parameters_data, 0, d * sizeof(float));
         return fail(st);
@@ -681,9 +681,9 @@ extern "C" fltee_status_t ecall_client_size_optimized_secure_aggregation(
         if (launch_dp_noise(d_out, d, cfg.sigma, cfg.clipping, n, next_seed(), c->stream) != hipSuccess)
             st = FLTEE_ERROR_UNEXPECTED;
     }
-    if (!st && hipMemcpyAsync(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    if (!st && fl_memcpy_async(updated_parameters_data, d_out, d * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         st = FLTEE_ERROR_UNEXPECTED;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
+    if (fl_stream_sync(c->stream) != hipSuccess) st = FLTEE_ERROR_UNEXPECTED;
     if (st) {
         std::memset(updated_parameters_data, 0, d * sizeof(float));
         return fail(st);
@@ -705,13 +705,13 @@ static fltee_status_t aes_ctr_device(const uint32_t *client_ids, size_t n, const
     if (!c->round_keys.reserve(n * 44 * 4)) return FLTEE_ERROR_OUT_OF_MEMORY;
     std::vector<uint32_t> rk(n * 44);
     aes128_session_round_keys(client_ids, n, rk.data());
-    if (hipMemcpyAsync(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (fl_memcpy_async(c->round_keys.ptr, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     if (launch_aes_ctr((const uint8_t *)d_in, n, bytes_per_client, bytes_per_client / 8,
                        (const uint32_t *)c->round_keys.ptr, (uint8_t *)d_out, s) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
     // rk lives on this stack frame: wait for the (tiny) copy + kernel
-    return hipStreamSynchronize(s) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
+    return fl_stream_sync(s) == hipSuccess ? FLTEE_SUCCESS : FLTEE_ERROR_UNEXPECTED;
 }
 
 extern "C" fltee_status_t fltee_decrypt_device(const uint32_t *client_ids, size_t n,

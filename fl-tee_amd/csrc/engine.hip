@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -64,7 +65,28 @@ static std::vector<NetLaunch> g_net_log;
 static std::atomic<bool> g_net_timing{false};
 constexpr size_t kNetLogCap = 16384;
 
+// the launch trace (common.h): one text line per launch / copy / memset / sync / RCCL op
+static std::atomic<bool> g_trace{false};
+static std::mutex g_trace_mu;
+static std::string g_trace_text;
+static size_t g_trace_lines = 0;
+constexpr size_t kTraceCap = (size_t)64 << 20;
+
+bool trace_on() { return g_trace.load(std::memory_order_relaxed); }
+
+void trace_event(const char *what, const char *site, uint64_t a, uint64_t b, uint64_t c) {
+    char line[512];
+    const int len = std::snprintf(line, sizeof line, "%s|%s|%llu|%llu|%llu\n", what, site,
+                                  (unsigned long long)a, (unsigned long long)b, (unsigned long long)c);
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    if (len > 0 && g_trace_text.size() + (size_t)len < kTraceCap) {
+        g_trace_text.append(line, (size_t)len < sizeof line ? (size_t)len : sizeof line - 1);
+        ++g_trace_lines;
+    }
+}
+
 void net_account(uint64_t bytes, const char *kernel, hipStream_t s) {
+    if (trace_on()) trace_event("bytes", kernel, bytes, 0, 0);
     g_net_launches.fetch_add(1, std::memory_order_relaxed);
     g_net_bytes.fetch_add(bytes, std::memory_order_relaxed);
     if (!g_net_timing.load(std::memory_order_relaxed)) return;
@@ -101,7 +123,7 @@ DeviceCtx *device_ctx(int dev) {
     if (!c.ready) {
         if (hipSetDevice(dev) != hipSuccess) return nullptr;
         if (hipMalloc(&c.status, 256) != hipSuccess) return nullptr;
-        if (hipMemset(c.status, 0, 256) != hipSuccess) return nullptr;
+        if (fl_memset(c.status, 0, 256) != hipSuccess) return nullptr;
         c.device = dev;
         c.ready = true;
     }
@@ -236,7 +258,7 @@ static Plan plan_for(uint32_t alg, size_t n, size_t k, size_t d, const fltee_dev
 // epoch), the epochs starting over
 static bool reserve_lb(DeviceCtx *c, size_t bytes) {
     if (bytes <= c->ws_lb.cap) return true;
-    if (!c->ws_lb.reserve(bytes) || hipMemset(c->ws_lb.ptr, 0, c->ws_lb.cap) != hipSuccess) return false;
+    if (!c->ws_lb.reserve(bytes) || fl_memset(c->ws_lb.ptr, 0, c->ws_lb.cap) != hipSuccess) return false;
     c->fc_epoch = 0;
     return true;
 }
@@ -268,7 +290,7 @@ bool oram_tree_default() { return g_oram_tree; }
 static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, size_t d,
                                        float coef, float *out, bool acc, uint32_t *status,
                                        hipStream_t s, bool network_order = false) {
-    if (n == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    if (n == 0) return acc ? hipSuccess : fl_memset_async(out, 0, d * 4, s);
     if (!c->ws_keys.reserve(n * 8)) return hipErrorOutOfMemory;
     uint64_t *sorted = (uint64_t *)c->ws_keys.ptr;
     hipError_t e;
@@ -283,7 +305,7 @@ static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, 
         e = launch_composite_init(rec, n, d, mc, keys, status, s);
         if (e == hipSuccess) e = bitonic_sort(keys, mc, 1, 0, s, n);  // ~0 keys past n
         if (e == hipSuccess) e = launch_gather_by_keys(keys, n, rec, sorted, s);
-        if (e == hipSuccess && !acc) e = hipMemsetAsync(out, 0, d * 4, s);
+        if (e == hipSuccess && !acc) e = fl_memset_async(out, 0, d * 4, s);
     }
     if (e == hipSuccess) e = launch_fold_sorted(sorted, n, d, coef, out, acc, s);
     return e;
@@ -293,7 +315,7 @@ static hipError_t ordered_fold_records(DeviceCtx *c, const void *rec, size_t n, 
 // order by idx (list position within an index), then the ordered fold
 hipError_t ordered_from_list(DeviceCtx *c, const uint64_t *sel, size_t lc, size_t d, float coef,
                              float *out, bool acc, uint32_t *status, hipStream_t s) {
-    if (lc == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    if (lc == 0) return acc ? hipSuccess : fl_memset_async(out, 0, d * 4, s);
     return ordered_fold_records(c, sel, lc, d, coef, out, acc, status, s);
 }
 
@@ -302,8 +324,8 @@ hipError_t read_device_word(DeviceCtx *c, const uint32_t *dev_word, size_t *out,
         c->host_word = nullptr;
         return hipErrorOutOfMemory;
     }
-    hipError_t e = hipMemcpyAsync(c->host_word, dev_word, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipError_t e = fl_memcpy_async(c->host_word, dev_word, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = fl_stream_sync(s);
     if (e == hipSuccess) *out = *c->host_word;
     return e;
 }
@@ -312,7 +334,7 @@ hipError_t safe_aggregate_ordered(DeviceCtx *c, const uint64_t *src, size_t m, s
                                   float coef, float *out, bool acc, uint32_t *status,
                                   hipStream_t s) {
     if (d == 0) return hipSuccess;
-    if (m == 0) return acc ? hipSuccess : hipMemsetAsync(out, 0, d * 4, s);
+    if (m == 0) return acc ? hipSuccess : fl_memset_async(out, 0, d * 4, s);
     const size_t nb = select_tiles(m);
     if (!c->ws_cnt.reserve((2 * nb + 2) * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + nb + 1;
@@ -339,7 +361,7 @@ static hipError_t nips19_shuffle_aggregate(DeviceCtx *c, uint64_t *A, size_t M, 
     if (!c->ws_cnt.reserve((2 * ntl + 2) * 4)) return hipErrorOutOfMemory;
     uint32_t *cnt = (uint32_t *)c->ws_cnt.ptr, *base = cnt + ntl + 1;
     // tiles of pads alone are skipped by the last pass and keep a zero count
-    hipError_t e = hipMemsetAsync(cnt, 0, ntl * 4, s);
+    hipError_t e = fl_memset_async(cnt, 0, ntl * 4, s);
     if (e == hipSuccess) e = bitonic_sort_nips19_select(A, M, key, rec, nrec, r, d, tf, cnt, s);
     if (e != hipSuccess) return e;
     e = launch_select_scan(cnt, ntl, base, s);
@@ -380,7 +402,7 @@ static hipError_t run_advanced(DeviceCtx *c, const void *rec, size_t n, size_t k
         const size_t lbb = fc_lookback_bytes(M, L, d, halo ? halo : n);
         if (lbb && (lbb > c->ws_lb.cap || c->fc_epoch >= (1u << 30) - 1)) {
             // new slots hold whatever was there: zero them (the epochs start over)
-            if (!c->ws_lb.reserve(lbb) || hipMemsetAsync(c->ws_lb.ptr, 0, c->ws_lb.cap, s) != hipSuccess)
+            if (!c->ws_lb.reserve(lbb) || fl_memset_async(c->ws_lb.ptr, 0, c->ws_lb.cap, s) != hipSuccess)
                 return hipErrorOutOfMemory;
             c->fc_epoch = 0;
         }
@@ -474,7 +496,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
             return FLTEE_ERROR_UNEXPECTED;
         ccoef = cf;
         if (!dense || tree) {  // plan_for reserved ws_rec on the same predicate
-            if (hipMemcpyAsync(c->ws_rec.ptr, rec, n * k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            if (fl_memcpy_async(c->ws_rec.ptr, rec, n * k * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
                 launch_apply_clip(c->ws_rec.ptr, n, k, cf, s) != hipSuccess)
                 return FLTEE_ERROR_UNEXPECTED;
             rec = c->ws_rec.ptr;
@@ -539,7 +561,7 @@ fltee_status_t aggregate(uint32_t alg, const void *rec, size_t n, size_t k, size
     }
     case FLTEE_ALG_OPTIMIZED: {
         const size_t batch = o.batch ? o.batch : n;
-        if (!acc) e = hipMemsetAsync(out, 0, d * 4, s);
+        if (!acc) e = fl_memset_async(out, 0, d * 4, s);
         for (size_t c0 = 0; e == hipSuccess && c0 < n; c0 += batch) {
             const size_t nb = (c0 + batch < n) ? batch : n - c0;
             e = run_advanced(c, (const uint8_t *)rec + c0 * k * 8, nb, k, d, k, o.fold_halo, 1.0f,
@@ -622,7 +644,7 @@ extern "C" fltee_status_t fltee_aggregate_device(uint32_t alg, const void *d_rec
     if (!c) return FLTEE_ERROR_UNEXPECTED;
     uint32_t *status = o.d_status ? o.d_status : c->status;
     hipStream_t s = (hipStream_t)stream;
-    if (!o.d_status && hipMemsetAsync(c->status, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (!o.d_status && fl_memset_async(c->status, 0, 4, s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     return aggregate(alg, d_records, n, k, d, d_out, o, s, status);
 }
 
@@ -644,10 +666,10 @@ extern "C" fltee_status_t fltee_device_status(void *stream, uint32_t *status) {
     DeviceCtx *c = current_ctx();
     if (!c || !status) return FLTEE_ERROR_UNEXPECTED;
     hipStream_t s = (hipStream_t)stream;
-    if (hipStreamSynchronize(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
-    if (hipMemcpy(status, c->status, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    if (fl_stream_sync(s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (fl_memcpy(status, c->status, 4, hipMemcpyDeviceToHost) != hipSuccess)
         return FLTEE_ERROR_UNEXPECTED;
-    if (hipMemset(c->status, 0, 4) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+    if (fl_memset(c->status, 0, 4) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
     return FLTEE_SUCCESS;
 }
 
@@ -882,6 +904,29 @@ extern "C" fltee_status_t fltee_ordered_list_device(const void *d_list, size_t l
 }
 
 extern "C" void fltee_debug_set_seed(uint64_t seed) { set_debug_seed(seed); }
+
+// test hook: the launch trace (common.h).  on = 1 clears it and starts recording, 0 stops.
+extern "C" void fltee_debug_trace(int on) {
+    std::lock_guard<std::mutex> lk(fltee::g_trace_mu);
+    if (on) {
+        fltee::g_trace_text.clear();
+        fltee::g_trace_lines = 0;
+    }
+    fltee::g_trace.store(on != 0);
+}
+
+// the trace so far as text (one line per event: what|site|a|b|c); returns its length
+// (copies at most cap - 1 bytes and a NUL into buf when buf is given)
+extern "C" size_t fltee_debug_trace_text(char *buf, size_t cap) {
+    std::lock_guard<std::mutex> lk(fltee::g_trace_mu);
+    const std::string &t = fltee::g_trace_text;
+    if (buf && cap) {
+        const size_t n = t.size() < cap - 1 ? t.size() : cap - 1;
+        std::memcpy(buf, t.data(), n);
+        buf[n] = 0;
+    }
+    return t.size();
+}
 
 // the planned network schedule (k_bitonic.hip plan_network), 8 words per launch
 extern "C" size_t fltee_debug_network_plan(uint32_t mlog, uint32_t tlog, uint32_t nt, int rmax,

@@ -175,7 +175,7 @@ static void group_free(Group *G) {
     for (size_t i = 0; i < G->r.size(); ++i) {
         Rank &R = G->r[i];
         if (hipSetDevice(R.dev) != hipSuccess) continue;
-        if (R.s && (G->rccl || i == 0)) (void)hipStreamSynchronize(R.s);
+        if (R.s && (G->rccl || i == 0)) (void)fl_stream_sync(R.s);
         for (Buffer *b : {&R.cipher, &R.rec, &R.rk, &R.out, &R.chunk, &R.spare, &R.fold, &R.fold_dst,
                           &R.cbuf, &R.ctmp, &R.lap, &R.list, &R.cnt, &R.st})
             b->release();
@@ -206,7 +206,7 @@ static hipError_t sync_all(Group &G) {
     for (int i = 0; i < G.W; ++i) {
         if (!G.rccl && i) break;
         if (hipSetDevice(G.r[i].dev) != hipSuccess) return hipErrorInvalidDevice;
-        const hipError_t e = hipStreamSynchronize(G.r[i].s);
+        const hipError_t e = fl_stream_sync(G.r[i].s);
         if (e != hipSuccess) return e;
     }
     (void)hipSetDevice(G.r[0].dev);
@@ -228,7 +228,7 @@ static hipError_t p2p(Group &G, const std::vector<P2P> &ops) {
     if (!G.rccl) {
         for (const P2P &o : ops) {
             if (!o.bytes || o.sp == o.dp) continue;
-            const hipError_t e = hipMemcpyAsync(o.dp, o.sp, o.bytes, hipMemcpyDeviceToDevice, G.r[0].s);
+            const hipError_t e = fl_memcpy_async(o.dp, o.sp, o.bytes, hipMemcpyDeviceToDevice, G.r[0].s);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
@@ -237,7 +237,7 @@ static hipError_t p2p(Group &G, const std::vector<P2P> &ops) {
         if (!o.bytes || o.src != o.dst || o.sp == o.dp) continue;
         if (hipSetDevice(G.r[o.src].dev) != hipSuccess) return hipErrorInvalidDevice;
         const hipError_t e =
-            hipMemcpyAsync(o.dp, o.sp, o.bytes, hipMemcpyDeviceToDevice, G.r[o.src].s);
+            fl_memcpy_async(o.dp, o.sp, o.bytes, hipMemcpyDeviceToDevice, G.r[o.src].s);
         if (e != hipSuccess) return e;
     }
     const RcclApi &nc = *rccl();
@@ -245,6 +245,7 @@ static hipError_t p2p(Group &G, const std::vector<P2P> &ops) {
     for (const P2P &o : ops) {
         if (nr != ncclSuccess) break;
         if (!o.bytes || o.src == o.dst) continue;
+        if (trace_on()) trace_event("rccl_sendrecv", "", o.bytes, (uint64_t)o.src, (uint64_t)o.dst);
         nr = nc.Send(o.sp, o.bytes, ncclUint8, o.dst, G.r[o.src].comm, G.r[o.src].s);
         if (nr == ncclSuccess)
             nr = nc.Recv(o.dp, o.bytes, ncclUint8, o.src, G.r[o.dst].comm, G.r[o.dst].s);
@@ -266,6 +267,7 @@ static hipError_t reduce_to_root(Group &G, size_t count, float *out_root) {
         return launch_rows_accumulate((const float *)G.rows.ptr, G.W, count, 1.0f, out_root, false,
                                       G.r[0].s);
     const RcclApi &nc = *rccl();
+    if (trace_on()) trace_event("rccl_reduce", "", count * 4, (uint64_t)G.W, 0);
     ncclResult_t nr = nc.GroupStart();
     for (int i = 0; i < G.W && nr == ncclSuccess; ++i)
         nr = nc.Reduce(G.r[i].out.ptr, i == 0 ? (void *)out_root : nullptr, count, ncclFloat,
@@ -297,7 +299,7 @@ static hipError_t fill_pads(uint64_t *p, size_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     size_t b = (n + 255) / 256;
     if (b > 4096) b = 4096;
-    hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)b), dim3(256), 0, s, p, n, (uint64_t)0xFFFFFFFFu);
+    FLTEE_LAUNCH(fill_u64_kernel, dim3((unsigned)b), dim3(256), 0, s, p, n, (uint64_t)0xFFFFFFFFu);
     return hipGetLastError();
 }
 
@@ -307,7 +309,7 @@ static uint32_t read_words(Group &G, const std::vector<const uint32_t *> &words,
     for (size_t i = 0; i < words.size(); ++i) {
         const Rank &R = G.r[G.rccl ? i : 0];
         if (hipSetDevice(R.dev) != hipSuccess ||
-            hipMemcpyAsync(G.host + i, words[i], 4, hipMemcpyDeviceToHost, R.s) != hipSuccess)
+            fl_memcpy_async(G.host + i, words[i], 4, hipMemcpyDeviceToHost, R.s) != hipSuccess)
             return FLTEE_ERROR_UNEXPECTED;
     }
     if (sync_all(G) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
@@ -367,10 +369,10 @@ static uint32_t group_records(Group &G, const GroupInput &in, size_t n, size_t r
         if (!R.cipher.reserve(nc * in.bpc + 16) || !R.rec.reserve(nc * rpc * 8 + 16) ||
             !R.rk.reserve(nc * 44 * 4 + 16)) { errs[i] = 3; return; }
         if (nc == 0) return;
-        if (hipMemcpyAsync(R.rk.ptr, in.rk + c_lo[i] * 44, nc * 44 * 4, hipMemcpyHostToDevice, R.s) != hipSuccess ||
-            hipMemcpyAsync(R.cipher.ptr, in.enc + c_lo[i] * in.bpc, nc * in.bpc, hipMemcpyHostToDevice,
+        if (fl_memcpy_async(R.rk.ptr, in.rk + c_lo[i] * 44, nc * 44 * 4, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+            fl_memcpy_async(R.cipher.ptr, in.enc + c_lo[i] * in.bpc, nc * in.bpc, hipMemcpyHostToDevice,
                            R.s) != hipSuccess ||
-            hipStreamSynchronize(R.s) != hipSuccess)
+            fl_stream_sync(R.s) != hipSuccess)
             errs[i] = 1;
     };
     std::vector<std::thread> th;
@@ -418,9 +420,9 @@ uint32_t group_dense_ecall(Group *Gp, const uint32_t *rk_host, size_t n, const u
         if (dg == 0) return;
         if (!R.cipher.reserve(n * dg * 8) || !R.rec.reserve(n * dg * 8) || !R.rk.reserve(n * 44 * 4) ||
             !R.st.reserve(64)) { errs[i] = 3; return; }
-        if (hipMemsetAsync(R.st.ptr, 0, 4, R.s) != hipSuccess ||
-            hipMemcpyAsync(R.rk.ptr, rk_host, n * 44 * 4, hipMemcpyHostToDevice, R.s) != hipSuccess ||
-            hipMemcpy2DAsync(R.cipher.ptr, dg * 8, enc + p[i] * 8, bpc, dg * 8, n, hipMemcpyHostToDevice,
+        if (fl_memset_async(R.st.ptr, 0, 4, R.s) != hipSuccess ||
+            fl_memcpy_async(R.rk.ptr, rk_host, n * 44 * 4, hipMemcpyHostToDevice, R.s) != hipSuccess ||
+            fl_memcpy2d_async(R.cipher.ptr, dg * 8, enc + p[i] * 8, bpc, dg * 8, n, hipMemcpyHostToDevice,
                              R.s) != hipSuccess) { errs[i] = 1; return; }
     };
     std::vector<std::thread> th;
@@ -745,7 +747,7 @@ uint32_t group_optimized(Group *Gp, const GroupInput &in, size_t n, size_t k, si
                 myrows = (float *)R.out.ptr;
                 ops.push_back({i, 0, myrows, rows + b0[i] * d, nb_i * d * 4});
             }
-            if (hipMemsetAsync(R.st.ptr, 0, 4, R.s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
+            if (fl_memset_async(R.st.ptr, 0, 4, R.s) != hipSuccess) return FLTEE_ERROR_UNEXPECTED;
             for (size_t b = b0[i]; b < b1[i]; ++b) {
                 const size_t c0 = b * batch, nb = (c0 + batch < n ? batch : n - c0);
                 if (advanced_batch(rec[i] + (c0 * k - lo[i]), nb, k, d, h, myrows + (b - b0[i]) * d,

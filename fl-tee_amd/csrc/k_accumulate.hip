@@ -521,13 +521,13 @@ template <int V, int U, bool CLIP, bool ACC, bool NT, int NTH = 256>
 static void launch_v(const void *rec, size_t n, size_t d2, float coef, float *out,
                      const float *ccoef, uint32_t *status, hipStream_t s) {
     const unsigned blocks = (unsigned)((d2 + NTH * V - 1) / (NTH * V));
-    hipLaunchKernelGGL((dense_accumulate_v<V, U, CLIP, ACC, NT, NTH>), dim3(blocks), dim3(NTH), 0, s,
+    FLTEE_LAUNCH((dense_accumulate_v<V, U, CLIP, ACC, NT, NTH>), dim3(blocks), dim3(NTH), 0, s,
                        (const uint4 *)rec, d2, (uint32_t)n, coef, out, ccoef, status);
 }
 template <int U, bool CLIP, bool ACC>
 static void launch_r(const void *rec, size_t n, size_t d, float coef, float *out,
                      const float *ccoef, uint32_t *status, hipStream_t s) {
-    hipLaunchKernelGGL((dense_accumulate_r<U, CLIP, ACC>), dim3((unsigned)((d + 255) / 256)), dim3(256),
+    FLTEE_LAUNCH((dense_accumulate_r<U, CLIP, ACC>), dim3((unsigned)((d + 255) / 256)), dim3(256),
                        0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
 }
 
@@ -536,17 +536,17 @@ static void launch_lds(bool vec, const void *rec, size_t n, size_t d, float coef
                        const float *ccoef, uint32_t *status, hipStream_t s) {
     const unsigned blocks = (unsigned)((d + OB - 1) / OB);
     if (vec)
-        hipLaunchKernelGGL((dense_accumulate_lds<true, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0, s,
+        FLTEE_LAUNCH((dense_accumulate_lds<true, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0, s,
                            (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
     else
-        hipLaunchKernelGGL((dense_accumulate_lds<false, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0,
+        FLTEE_LAUNCH((dense_accumulate_lds<false, CLIP, ACC, OB, CC>), dim3(blocks), dim3(DS_NT), 0,
                            s, (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
 }
 
 template <int U, bool REM, bool ACC>
 static void dw_launch(unsigned blocks, const void *rec, size_t n, size_t d, float coef, float *out,
                       uint32_t *status, hipStream_t s) {
-    hipLaunchKernelGGL((dense_accumulate_w<U, REM, false, ACC>), dim3(blocks), dim3(64), 0, s,
+    FLTEE_LAUNCH((dense_accumulate_w<U, REM, false, ACC>), dim3(blocks), dim3(64), 0, s,
                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status);
 }
 
@@ -566,7 +566,7 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         case 40: case 41: case 42: case 43:
             if (vec) {
                 const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
-#define DW_GO(U_) hipLaunchKernelGGL((dense_accumulate_w<U_, true, CLIP, ACC>), dim3(blocks), dim3(64), 0, s, \
+#define DW_GO(U_) FLTEE_LAUNCH((dense_accumulate_w<U_, true, CLIP, ACC>), dim3(blocks), dim3(64), 0, s, \
                                      (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, ccoef, status)
                 if (g_dense_variant == 40) DW_GO(100);
                 else if (g_dense_variant == 41) DW_GO(32);
@@ -582,13 +582,13 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
             if (vec && !CLIP && n <= 100) {
                 const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
                 if (g_dense_variant == 44)
-                    hipLaunchKernelGGL((dense_accumulate_wk<2, 50, ACC>), dim3(blocks), dim3(128), 0, s,
+                    FLTEE_LAUNCH((dense_accumulate_wk<2, 50, ACC>), dim3(blocks), dim3(128), 0, s,
                                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
                 else if (g_dense_variant == 45)
-                    hipLaunchKernelGGL((dense_accumulate_wk<4, 25, ACC>), dim3(blocks), dim3(256), 0, s,
+                    FLTEE_LAUNCH((dense_accumulate_wk<4, 25, ACC>), dim3(blocks), dim3(256), 0, s,
                                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
                 else
-                    hipLaunchKernelGGL((dense_accumulate_wk<3, 34, ACC>), dim3(blocks), dim3(192), 0, s,
+                    FLTEE_LAUNCH((dense_accumulate_wk<3, 34, ACC>), dim3(blocks), dim3(192), 0, s,
                                        (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, status);
                 break;
             }
@@ -598,7 +598,7 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         case 49:
             if (vec && !CLIP && n <= 100) {
                 const unsigned blocks = (unsigned)((d / 2 + 63) / 64);
-                hipLaunchKernelGGL((dense_accumulate_w<100, true, false, ACC, false>), dim3(blocks), dim3(64), 0, s,
+                FLTEE_LAUNCH((dense_accumulate_w<100, true, false, ACC, false>), dim3(blocks), dim3(64), 0, s,
                                    (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status);
                 break;
             }
@@ -609,10 +609,10 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
             if (!CLIP && ((uintptr_t)rec % 8 == 0)) {
                 const unsigned blocks = (unsigned)((d + 63) / 64);
                 if (g_dense_variant == 47)
-                    hipLaunchKernelGGL((dense_accumulate_w1<100, ACC>), dim3(blocks), dim3(64), 0, s,
+                    FLTEE_LAUNCH((dense_accumulate_w1<100, ACC>), dim3(blocks), dim3(64), 0, s,
                                        (const uint2 *)rec, d, (uint32_t)n, coef, out, status);
                 else
-                    hipLaunchKernelGGL((dense_accumulate_w1<50, ACC>), dim3(blocks), dim3(64), 0, s,
+                    FLTEE_LAUNCH((dense_accumulate_w1<50, ACC>), dim3(blocks), dim3(64), 0, s,
                                        (const uint2 *)rec, d, (uint32_t)n, coef, out, status);
                 break;
             }
@@ -620,7 +620,7 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
             break;
         case 24:
             if (vec && d >= 2) {
-                hipLaunchKernelGGL((dense_accumulate_glds<CLIP, ACC>), dim3((unsigned)((d + 63) / 64)),
+                FLTEE_LAUNCH((dense_accumulate_glds<CLIP, ACC>), dim3((unsigned)((d + 63) / 64)),
                                    dim3(256), 0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out,
                                    ccoef, status);
                 break;
@@ -662,7 +662,7 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
         }
     } else {
         const unsigned blocks = (unsigned)((d + 255) / 256);
-        hipLaunchKernelGGL((dense_accumulate_s<CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
+        FLTEE_LAUNCH((dense_accumulate_s<CLIP, ACC>), dim3(blocks), dim3(256), 0, s,
                            (const uint2 *)rec, d, (uint32_t)n, coef, out, ccoef, status);
     }
     return hipGetLastError();
@@ -822,18 +822,18 @@ hipError_t launch_rows_accumulate(const float *mat, size_t n, size_t d, float co
         const size_t d4 = d / 4;
         const unsigned blocks = (unsigned)((d4 + 255) / 256);
         if (accumulate)
-            hipLaunchKernelGGL((rows_accumulate<8, true>), dim3(blocks), dim3(256), 0, s,
+            FLTEE_LAUNCH((rows_accumulate<8, true>), dim3(blocks), dim3(256), 0, s,
                                (const float4 *)mat, d4, (uint32_t)n, coef, (float4 *)out);
         else
-            hipLaunchKernelGGL((rows_accumulate<8, false>), dim3(blocks), dim3(256), 0, s,
+            FLTEE_LAUNCH((rows_accumulate<8, false>), dim3(blocks), dim3(256), 0, s,
                                (const float4 *)mat, d4, (uint32_t)n, coef, (float4 *)out);
     } else {
         const unsigned blocks = (unsigned)((d + 255) / 256);
         if (accumulate)
-            hipLaunchKernelGGL(rows_accumulate_s<true>, dim3(blocks), dim3(256), 0, s, mat, d,
+            FLTEE_LAUNCH(rows_accumulate_s<true>, dim3(blocks), dim3(256), 0, s, mat, d,
                                (uint32_t)n, coef, out);
         else
-            hipLaunchKernelGGL(rows_accumulate_s<false>, dim3(blocks), dim3(256), 0, s, mat, d,
+            FLTEE_LAUNCH(rows_accumulate_s<false>, dim3(blocks), dim3(256), 0, s, mat, d,
                                (uint32_t)n, coef, out);
     }
     return hipGetLastError();
@@ -849,7 +849,7 @@ hipError_t launch_sweep_accumulate(const void *rec, size_t nrec, size_t d, float
     const bool wide = d >= (size_t)256 * 64;
     const unsigned blocks = (unsigned)((d + (wide ? 255 : 63)) / (wide ? 256 : 64));
 #define SO_GO(NT_, ACC_)                                                                         \
-    hipLaunchKernelGGL((sweep_ordered<NT_, ACC_>), dim3(blocks), dim3(NT_), 0, s,                \
+    FLTEE_LAUNCH((sweep_ordered<NT_, ACC_>), dim3(blocks), dim3(NT_), 0, s,                \
                        (const uint2 *)rec, (uint32_t)nrec, (uint32_t)d, coef, out)
     if (wide) {
         if (accumulate) SO_GO(256, true);
@@ -973,23 +973,23 @@ hipError_t launch_scatter_sum(const void *rec, size_t n, size_t k, size_t d, uin
     // the rows [0, n*d) must hold the sentinel: filled once per buffer, then kept so by
     // scatter_rows_sum, which empties every slot it consumed
     if (*mat_clean < n * d * 4) {
-        hipError_t e = hipMemsetAsync(mat, 0xFF, n * d * 4, s);
+        hipError_t e = fl_memset_async(mat, 0xFF, n * d * 4, s);
         if (e != hipSuccess) return e;
         *mat_clean = n * d * 4;
     }
     if (k) {
         const size_t bx = (k + 255) / 256 < 1024 ? (k + 255) / 256 : 1024;
         const size_t by = n < 65535 ? n : 65535;
-        hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, s,
+        FLTEE_LAUNCH(scatter_rows_kernel, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, s,
                            (const uint2 *)rec, n, k, d, mat, dup, epoch, status);
     }
     const unsigned blocks = (unsigned)((d + 255) / 256);
     const size_t nrec = n * k;
     if (accumulate)
-        hipLaunchKernelGGL((scatter_rows_sum<true, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
+        FLTEE_LAUNCH((scatter_rows_sum<true, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
                            (uint32_t)n, (const uint2 *)rec, nrec, dup, epoch, coef, out);
     else
-        hipLaunchKernelGGL((scatter_rows_sum<false, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
+        FLTEE_LAUNCH((scatter_rows_sum<false, 32>), dim3(blocks), dim3(256), 0, s, mat, d,
                            (uint32_t)n, (const uint2 *)rec, nrec, dup, epoch, coef, out);
     return hipGetLastError();
 }
@@ -1024,14 +1024,14 @@ __global__ __launch_bounds__(256) void read_floor_kernel(const uint4 *__restrict
 
 hipError_t launch_read_floor(const void *src, size_t bytes, uint32_t *sink, unsigned blocks,
                              hipStream_t s) {
-    hipLaunchKernelGGL(read_floor_kernel, dim3(blocks), dim3(256), 0, s, (const uint4 *)src, bytes / 16,
+    FLTEE_LAUNCH(read_floor_kernel, dim3(blocks), dim3(256), 0, s, (const uint4 *)src, bytes / 16,
                        sink);
     return hipGetLastError();
 }
 
 hipError_t launch_scale(float *out, size_t d, float coef, hipStream_t s) {
     if (d == 0) return hipSuccess;
-    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, out, d,
+    FLTEE_LAUNCH(scale_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, out, d,
                        coef);
     return hipGetLastError();
 }
@@ -1050,7 +1050,7 @@ hipError_t launch_check_range(const void *rec, size_t nrec, uint32_t limit, uint
     if (nrec == 0) return hipSuccess;
     size_t blocks = (nrec + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(check_range_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+    FLTEE_LAUNCH(check_range_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint2 *)rec, nrec, limit, status);
     return hipGetLastError();
 }

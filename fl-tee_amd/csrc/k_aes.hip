@@ -533,7 +533,7 @@ hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_pe
                                 uint32_t *zero_word) {
     const size_t bpcl = (rec_per_client + 1) / 2;
     if (n == 0 || bpcl == 0)  // nothing to decrypt; the word still has to read 0
-        return zero_word ? hipMemsetAsync(zero_word, 0, 4, s) : hipSuccess;
+        return zero_word ? fl_memset_async(zero_word, 0, 4, s) : hipSuccess;
     const bool aligned = bytes_per_client % 8 == 0 && (uintptr_t)cipher % 8 == 0;
     // windows of 512 counter blocks (absolute counter space) touching each client's slice
     const uint64_t wpc = (block_off + bpcl - 1) / kAesWindow4 - block_off / kAesWindow4 + 1;
@@ -545,11 +545,11 @@ hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_pe
         uint64_t rblocks = ((uint64_t)n * wpcr + 3) / 4;
         if (rblocks > 16384) rblocks = 16384;
         if (aligned)
-            hipLaunchKernelGGL(aes_ctr_row_kernel<true>, dim3((unsigned)rblocks), dim3(256), 0, s,
+            FLTEE_LAUNCH(aes_ctr_row_kernel<true>, dim3((unsigned)rblocks), dim3(256), 0, s,
                                cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
                                block_off, idx_sub, wpcr, zero_word);
         else
-            hipLaunchKernelGGL(aes_ctr_row_kernel<false>, dim3((unsigned)rblocks), dim3(256), 0, s,
+            FLTEE_LAUNCH(aes_ctr_row_kernel<false>, dim3((unsigned)rblocks), dim3(256), 0, s,
                                cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
                                block_off, idx_sub, wpcr, zero_word);
         return hipGetLastError();
@@ -557,11 +557,11 @@ hipError_t launch_aes_ctr_slice(const uint8_t *cipher, size_t n, size_t bytes_pe
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 16384) blocks = 16384;  // grid-stride beyond 16 waves per SIMD
     if (aligned)
-        hipLaunchKernelGGL(aes_ctr_bs4_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
+        FLTEE_LAUNCH(aes_ctr_bs4_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s,
                            cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
                            block_off, idx_sub, wpc, zero_word);
     else
-        hipLaunchKernelGGL(aes_ctr_bs4_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
+        FLTEE_LAUNCH(aes_ctr_bs4_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s,
                            cipher, n, bytes_per_client, rec_per_client, round_keys, plain,
                            block_off, idx_sub, wpc, zero_word);
     return hipGetLastError();

@@ -265,7 +265,7 @@ static hipError_t keyed_table_prepare(uint32_t seed, hipStream_t s) {
         t.valid = false;
     }
     if (t.valid && t.seed == seed) return hipSuccess;
-    hipLaunchKernelGGL(keyed_table_kernel, dim3(kKeyedTabEntries / 256), dim3(256), 0, s, t.ptr, seed);
+    FLTEE_LAUNCH(keyed_table_kernel, dim3(kKeyedTabEntries / 256), dim3(256), 0, s, t.ptr, seed);
     e = hipGetLastError();
     t.seed = seed;
     t.valid = e == hipSuccess;
@@ -1345,9 +1345,9 @@ static hipError_t launch_global(uint64_t *data, uint32_t mlog, uint32_t ilog, ui
     net_account((uint64_t)16 * ngroups << R, "bitonic_global", s);
 #define BG_GO(R_)                                                                                  \
     do {                                                                                           \
-        if (sw) hipLaunchKernelGGL((bitonic_global<MODE, R_, true>), dim3(blocks), dim3(256), 0, s, \
+        if (sw) FLTEE_LAUNCH((bitonic_global<MODE, R_, true>), dim3(blocks), dim3(256), 0, s, \
                                    data, ilog, jtop, seed, ngroups, pbase, hole_at, hole_len);     \
-        else hipLaunchKernelGGL((bitonic_global<MODE, R_>), dim3(blocks), dim3(256), 0, s, data,    \
+        else FLTEE_LAUNCH((bitonic_global<MODE, R_>), dim3(blocks), dim3(256), 0, s, data,    \
                                 ilog, jtop, seed, ngroups, pbase, hole_at, hole_len);              \
     } while (0)
     switch (R) {
@@ -1410,7 +1410,7 @@ static hipError_t launch_tiles_pr(unsigned grid, size_t lds, hipStream_t s, uint
         attr = true;
     }
     net_account((uint64_t)16 * tiles << tlog, "bitonic_tiles", s);
-    hipLaunchKernelGGL((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW, PR>), dim3(grid), dim3(NT), lds, s,
+    FLTEE_LAUNCH((bitonic_tiles<MODE, SORT, E, NT, TL, WL, LPF, SW, PR>), dim3(grid), dim3(NT), lds, s,
                        data, tlog, ilog, wlog, dtile, seed, tiles, pbase, seg0, hole_at, hole_len);
     return hipGetLastError();
 }
@@ -1509,7 +1509,7 @@ static hipError_t launch_direct(const TileCfg &c, hipStream_t s, uint64_t *data,
                 160 * 1024 - (SEL_ ? 256 : 0)); /* static wtot[] counts against the 160 KB */      \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_, SWI_, SWO_>), \
+        FLTEE_LAUNCH((bitonic_merge_direct<MODE, E, NT, RL_, STRIDED, SEL_, TL_, SWI_, SWO_>), \
                            dim3(c.grid), dim3(NT), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, \
                            c.tiles, pbase, sink.d, sink.cnt, c.hole_at, c.hole_len);               \
     } while (0)
@@ -1580,7 +1580,7 @@ static hipError_t launch_sort_direct(const TileCfg &c, hipStream_t s, uint64_t *
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);     \
             attr = true;                                                                           \
         }                                                                                          \
-        hipLaunchKernelGGL((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_, SWO_>), dim3(grid), \
+        FLTEE_LAUNCH((bitonic_sort_direct<MODE, E, NT, RL_, GEN, TL_, LPF_, SWO_>), dim3(grid), \
                            dim3(NT), c.lds, s, data, c.tlog, seed, c.tiles, pbase, gg);            \
     } while (0)
 #define BS_GO_PF(RL_, TL_, LPF_) BS_GO_SW(RL_, TL_, LPF_, false)
@@ -1649,7 +1649,7 @@ static hipError_t launch_tiles(const TileCfg &c, hipStream_t s, uint64_t *data, 
                 attr = true;
             }
             net_account((uint64_t)16 * c.tiles << c.tlog, "bitonic_tiles", s);
-            hipLaunchKernelGGL((bitonic_tiles<MODE, false, 16, 1024, 14, 0, true, true, false, true>), dim3(c.grid),
+            FLTEE_LAUNCH((bitonic_tiles<MODE, false, 16, 1024, 14, 0, true, true, false, true>), dim3(c.grid),
                                dim3(1024), c.lds, s, data, c.tlog, ilog, wlog, dtile, seed, c.tiles, pbase, 0u,
                                c.hole_at, c.hole_len);
             return hipGetLastError();
@@ -2389,7 +2389,7 @@ hipError_t bitonic_exchange(uint64_t *mine, const uint64_t *theirs, size_t m, ui
     const uint32_t key = mode == 2 ? shuffle_step_key(seed, ilog, jlog) : 0u;
     net_account((uint64_t)24 * m, "bitonic_exchange_kernel", s);
 #define BX_GO(MD)                                                                                  \
-    hipLaunchKernelGGL((bitonic_exchange_kernel<MD>), dim3((unsigned)blocks), dim3(256), 0, s,     \
+    FLTEE_LAUNCH((bitonic_exchange_kernel<MD>), dim3((unsigned)blocks), dim3(256), 0, s,     \
                        (uint4 *)mine, (const uint4 *)theirs, m2, pos_lo, lower, ilog, key)
     if (mode == 0) BX_GO(0); else if (mode == 1) BX_GO(1); else BX_GO(2);
 #undef BX_GO

@@ -68,19 +68,19 @@ hipError_t launch_client_topk(const float *values, size_t n, size_t d, size_t k,
                               uint64_t *rec, hipStream_t s) {
     const size_t segp = next_pow2_sz(d < 2 ? 2 : d);
     const uint32_t slog = log2_pow2(segp);
-    hipLaunchKernelGGL(client_keys_kernel, dim3(grid_for(n * segp)), dim3(256), 0, s, values, n,
+    FLTEE_LAUNCH(client_keys_kernel, dim3(grid_for(n * segp)), dim3(256), 0, s, values, n,
                        d, slog, keys);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // n segments padded to a power of two (pad segments of all-pad keys are inert)
     const size_t m = next_pow2_sz(n * segp);
     if (m > n * segp) {
-        e = hipMemsetAsync(keys + n * segp, 0xFF, (m - n * segp) * 8, s);
+        e = fl_memset_async(keys + n * segp, 0xFF, (m - n * segp) * 8, s);
         if (e != hipSuccess) return e;
     }
     e = bitonic_sort_segments(keys, m, segp, 1, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(client_topk_extract_kernel, dim3(grid_for(n * k)), dim3(256), 0, s, keys,
+    FLTEE_LAUNCH(client_topk_extract_kernel, dim3(grid_for(n * k)), dim3(256), 0, s, keys,
                        values, n, d, k, slog, rec);
     return hipGetLastError();
 }
@@ -91,7 +91,7 @@ size_t client_topk_workspace(size_t n, size_t d) {
 
 hipError_t launch_client_dense(const float *values, size_t n, size_t d, uint64_t *rec,
                                hipStream_t s) {
-    hipLaunchKernelGGL(client_dense_kernel, dim3(grid_for(n * d)), dim3(256), 0, s, values, n, d,
+    FLTEE_LAUNCH(client_dense_kernel, dim3(grid_for(n * d)), dim3(256), 0, s, values, n, d,
                        rec);
     return hipGetLastError();
 }

@@ -400,10 +400,10 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
                               uint32_t logW, uint32_t S, uint32_t rows, uint32_t ngroups,
                               float coef, float *out, uint32_t ntiles, bool nh = false) {
 #define CP_GO(F, X, V)                                                                           \
-    hipLaunchKernelGGL((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
+    FLTEE_LAUNCH((compact_pass<NT, PER, F, X, MINB, V>), dim3(grid), dim3(NT), 0, s, src, dst, L, \
                        d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
 #define CP_GO_CT(V, G_, LW_, SH_)                                                                \
-    hipLaunchKernelGGL((compact_pass<NT, PER, false, 0, MINB, V, G_, LW_, SH_>), dim3(grid), dim3(NT), 0, s, \
+    FLTEE_LAUNCH((compact_pass<NT, PER, false, 0, MINB, V, G_, LW_, SH_>), dim3(grid), dim3(NT), 0, s, \
                        src, dst, L, d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
     // 16-B slot pairs: rows of >= 2 residues (or a contiguous tile of an even S: the
     // converted first pass), L even, both buffers 16-B aligned
@@ -420,7 +420,7 @@ static hipError_t launch_pass(bool first, int fin, unsigned grid, hipStream_t s,
         }
     }
 #define CP_GO_NH(X, V)                                                                           \
-    hipLaunchKernelGGL((compact_pass<NT, PER, false, X, MINB, V, 0, 0, 0, true>), dim3(grid), dim3(NT), 0, s, \
+    FLTEE_LAUNCH((compact_pass<NT, PER, false, X, MINB, V, 0, 0, 0, true>), dim3(grid), dim3(NT), 0, s, \
                        src, dst, L, d, j0, G, logW, S, rows, ngroups, coef, out, ntiles)
     if (FLTEE_CP_NOHALO && nh && !first) {  // one band: no halo rows (compact_pass NH)
         if (v2) {
@@ -653,6 +653,10 @@ constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
 #ifndef FLTEE_FC_LB
 #define FLTEE_FC_LB 1
 #endif
+// the look-back's first-round words loaded before the compaction levels (1) or after (0)
+#ifndef FLTEE_FC_LBPRE
+#define FLTEE_FC_LBPRE 1
+#endif
 // the bounded look-back wait: polls of ~0.25 us (about a quarter second in all)
 constexpr uint32_t kFcSpinMax = 1u << 20;
 
@@ -705,9 +709,21 @@ __device__ __forceinline__ FoldAgg fa_shfl_down(const FoldAgg &x, int o) {
 // look-back).  Each round reads NW * 64 predecessors, wave w the 64 from tile - 1 - 64 w
 // back: up to the nearest one with its inclusive prefix published, aggregates in front of
 // it; rounds go on further back only when none of them had it.
+// the three words of this epoch already loaded (w), or false
+__device__ __forceinline__ bool fc_have(const uint64_t *w, uint32_t epoch, FoldAgg &g) {
+    g.F = (uint32_t)w[0];
+    g.K = (uint32_t)w[1];
+    g.Q = __uint_as_float((uint32_t)w[2]);
+    g.fl = (uint32_t)(w[2] >> 32) & 3u;
+    return (uint32_t)(w[0] >> 34) == epoch && (uint32_t)(w[1] >> 34) == epoch &&
+           (uint32_t)(w[2] >> 34) == epoch;
+}
+
+// pre: this thread's first-round predecessor (tile - 1 - t) words, loaded ahead (inc[3],
+// agg[3]): used when they are already this epoch's, else polled again
 template <int NW>
 __device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t t,
-                               uint32_t *status, FoldAgg *sh, uint32_t *shf) {
+                               uint32_t *status, FoldAgg *sh, uint32_t *shf, const uint64_t *pre) {
     const uint32_t lane = t & 63, wave = t >> 6;
     long long base = (long long)tile - 1;
     bool done = tile == 0;
@@ -721,8 +737,12 @@ __device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t
             FoldAgg g;
             bool ok = false;
             uint32_t it = 0;
+            if (base == (long long)tile - 1) {  // the first round: the words loaded ahead
+                if (fc_have(pre, epoch, g)) { isinc = true; ok = true; }
+                else if (fc_have(pre + 3, epoch, g)) { isinc = false; ok = true; }
+            }
 #pragma unroll 1
-            for (;;) {  // the inclusive prefix if it is there, else the aggregate
+            while (!ok) {  // the inclusive prefix if it is there, else the aggregate
                 if (fc_get(lb[p].inc, epoch, g)) { isinc = true; ok = true; break; }
                 if (fc_get(lb[p].agg, epoch, g)) { isinc = false; ok = true; break; }
                 if (++it >= kFcSpinMax) break;
@@ -930,6 +950,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         {
             const uint32_t kw0 = (uint32_t)win[0];
             const uint32_t gm = (1u << G) - 1;
+            const float rchunk = 1.0f / (float)chunk + 1e-6f;
 #pragma unroll
             for (uint32_t i = 0; i < PER; ++i) {
                 const uint32_t f = t + i * NT, x = f + Hr;
@@ -937,7 +958,9 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 const uint64_t r = win[x];
                 const uint32_t idx = (uint32_t)r;
                 const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-                const uint32_t o = x / chunk, xo = o * chunk;  // x's owner lane, its first slot
+                // x's owner lane and its first slot (x < 2^14, chunk <= 16: the f32 quotient
+                // truncates exactly)
+                const uint32_t o = (uint32_t)((float)x * rchunk), xo = o * chunk;
                 const int yso = (int)xo - (int)lim;
                 const bool lng = yso > 0 && (uint32_t)win[yso - 1] == idx;
                 const float wl = (exf[o] && idx == (uint32_t)win[xo]) ? __fadd_rn(exq[o], loc[x]) : loc[x];
@@ -952,6 +975,18 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         uint64_t *sm = win;
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) sm[t + i * NT] = v[i];
+        // the look-back's first-round words, loaded now: they arrive while the levels run
+        uint64_t lw[6] = {0, 0, 0, 0, 0, 0};
+        {
+            const long long p1 = (long long)tile - 1 - (long long)t;
+            if (FLTEE_FC_LB && FLTEE_FC_LBPRE && p1 >= 0) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    lw[i] = __hip_atomic_load(&lb[p1].inc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    lw[3 + i] = __hip_atomic_load(&lb[p1].agg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
         __syncthreads();
         // the first G levels, exactly compact_pass's (contiguous: W = 1, j0 = 0); all nine at
         // compile time when the array has that many (FLTEE_CP_CT, cp_levels_ct)
@@ -998,7 +1033,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         // an A/B of its cost only) into the window head run's record, if it began before
         FoldAgg wc = fa_empty();
         if (FLTEE_FC_LB) {
-            wc = fc_lookback<NW>(lb, tile, epoch, t, status, lb_sh, lb_shf);
+            wc = fc_lookback<NW>(lb, tile, epoch, t, status, lb_sh, lb_shf, lw);
             if (t == 0) fc_put(lb[tile].inc, fa_combine(wc, agg_s), epoch);
         }
         const bool wok = (wc.fl & kFsPiece) && wc.K == kw0_s;
@@ -1059,7 +1094,7 @@ static hipError_t fc_launch(uint64_t ntiles, size_t lds, hipStream_t s, const ui
         res_lds = lds;
     }
     const unsigned grid = (unsigned)(ntiles < (uint64_t)resident ? ntiles : (uint64_t)resident);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, s, A, B, (uint32_t)L, (uint32_t)M,
+    FLTEE_LAUNCH(kern, dim3(grid), dim3(NT), lds, s, A, B, (uint32_t)L, (uint32_t)M,
                        (uint32_t)d, G, S, (uint32_t)Hr, (uint32_t)ntiles, coef, out, lim, lb, epoch,
                        status);
     return hipGetLastError();
@@ -1182,7 +1217,7 @@ hipError_t launch_compact_offset(const uint64_t *chunk, size_t c, size_t d, uint
     if (L >= ((size_t)1 << 29)) return hipErrorInvalidValue;
     size_t blocks = (L + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(offset_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, chunk, c, d,
+    FLTEE_LAUNCH(offset_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, chunk, c, d,
                        buf);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -32,7 +32,7 @@ hipError_t launch_dp_noise(float *out, size_t d, float sigma, float clipping, si
                            uint64_t seed, hipStream_t s) {
     if (d == 0) return hipSuccess;
     const double stddev = (double)(clipping * sigma);  // (clipping * sigma) as f64
-    hipLaunchKernelGGL(dp_noise_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, out,
+    FLTEE_LAUNCH(dp_noise_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, out,
                        d, stddev, (double)n, (uint32_t)seed, (uint32_t)(seed >> 32));
     return hipGetLastError();
 }
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void client_norm_kernel(const uint2 *__restric
 hipError_t launch_client_clip_coef(const void *rec, size_t n, size_t k, float clipping,
                                    float *coef, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(client_norm_kernel, dim3((unsigned)n), dim3(256), 0, s, (const uint2 *)rec,
+    FLTEE_LAUNCH(client_norm_kernel, dim3((unsigned)n), dim3(256), 0, s, (const uint2 *)rec,
                        k, clipping, coef);
     return hipGetLastError();
 }
@@ -82,7 +82,7 @@ hipError_t launch_apply_clip(void *rec, size_t n, size_t k, const float *coef, h
     if (total == 0) return hipSuccess;
     size_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(apply_clip_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint2 *)rec, n,
+    FLTEE_LAUNCH(apply_clip_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint2 *)rec, n,
                        k, coef);
     return hipGetLastError();
 }

@@ -64,7 +64,7 @@ hipError_t launch_advanced_init_range(const void *rec, size_t nrec, size_t d, si
     if (m == 0) return hipSuccess;
     size_t blocks = (m + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(advanced_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+    FLTEE_LAUNCH(advanced_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint64_t *)rec, nrec, d, pbase, m, dst);
     return hipGetLastError();
 }
@@ -110,12 +110,16 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     const uint32_t nstage = (Hr + C + FS_W) / FS_W;
     const uint32_t hw = Hr / FS_W;  // stage s holds window u = s - hw of the chunk
 
-    // the key in front of the walk: does the run at b begin before it?
-    bool hasprev = false;
-    uint32_t kprev = 0;
-    if (side && a < end && b - 1 >= 0 && b - 1 + pbase >= 0) {
-        kprev = rec_idx(src[b - 1]);
-        hasprev = true;
+    // the side record's walk-invariant inputs: the key at the walk's first real position
+    // (b, or global position 0 for the array's first lanes) and whether the run there began
+    // before the walk (the key in front of it)
+    uint32_t pf_key = 0;
+    bool in_head = false;
+    if (side && a < end) {
+        long long fp = b + pbase < 0 ? -pbase : b;
+        fp = fp < 0 ? 0 : fp;
+        if (fp < m) pf_key = rec_idx(src[fp]);
+        if (b - 1 >= 0 && b - 1 + pbase >= 0) in_head = rec_idx(src[b - 1]) == pf_key;
     }
 
     // cooperative window loads: piece p = l + 64 i -> window w = p >> 3, 16-B part p & 7
@@ -145,8 +149,8 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     bool started = false;
     uint64_t prev = 0;
     // the side record: the piece [b, b + C) and the head run (the one holding b)
-    bool in_head = false, unbroken = true, corr = false, piece = false, pfull = false;
-    uint32_t pf_key = 0, pk = 0, ck = 0;
+    bool corr = false, piece = false;
+    uint32_t pk = 0;
     float pq = 0.0f, cs = 0.0f;
     auto stage = [&](fs_u32x4 (&pf)[8], uint32_t s) {
         uint64_t *cur = win[s & 1], *old = win[(s + 1) & 1];
@@ -162,6 +166,10 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
 #pragma unroll
         for (uint32_t t = 0; t < FS_W; ++t) r[t] = cur[l * FS_ROW + t];
         const long long q0 = a - (long long)Hr + (long long)s * FS_W;
+        // step t of stage s emits b + 16 s + t - 1, inside the chunk for 16 s + t in
+        // [Hr + 1, Hr + C] (Hr and C multiples of 16): stage-uniform flags for t = 0 and t > 0
+        const uint32_t cs_end = hw + C / FS_W;
+        const bool in1 = s >= hw && s < cs_end, in0 = s > hw && s <= cs_end;
 #pragma unroll
         for (uint32_t t = 0; t < FS_W; ++t) {
             const long long q = q0 + t;  // this step reads position q, emits position q - 1
@@ -169,10 +177,11 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             const uint32_t ci = rec_idx(r[t]);
             const bool eq = started && ci == pre_idx;
             const bool copy = qg - 1 >= fold_len, dmy = qg < fold_len && eq;
-            // the head run ends at q - 1: inside the chunk it is the one the side record
-            // carries (emitted as a dummy here, its record written by fold_patch_kernel)
-            const bool hend = in_head && !copy && !dmy;
-            const bool sup = hend && q - 1 >= a && q - 1 < a + (long long)C;
+            // the head run ends at q - 1: inside the chunk (step si in [Hr + 1, Hr + C], a
+            // wave-uniform test) it is the one the side record carries (emitted as a dummy
+            // here, its record written by fold_patch_kernel)
+            const bool inchunk = t == 0 ? in0 : in1;  // emits inside [a, a + C)
+            const bool sup = in_head && !copy && !dmy && inchunk;
             uint64_t emit;
             if constexpr (CEMIT) {
                 emit = copy ? prev
@@ -184,30 +193,22 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
                        : dmy || sup ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
                                     : make_rec(pre_idx, pre_val);
             }
-            if (sup) {
-                corr = true;
-                ck = pre_idx;
-                cs = pre_val;
-            }
-            in_head = in_head && !hend && !copy;
+            // (value selects: a store through a selected address would put these flags on
+            // the stack)
+            cs = sup ? pre_val : cs;
+            corr = corr || sup;
+            in_head = in_head && (dmy || (t == 0 && s == 0));  // (step 0 emits b - 1)
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
-            // (value selects, one assignment each: a store through a selected address
-            // would put these flags on the stack)
             const bool valid = q >= 0 && qg >= 0;
-            const bool first = valid && !started;  // the walk's first position (b, or 0)
-            pf_key = first ? ci : pf_key;
-            in_head = first ? (hasprev && ci == kprev) : in_head;
-            unbroken = (valid && started) ? (unbroken && eq) : unbroken;
             if (valid) {
                 pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
                 pre_idx = ci;
                 started = true;
             }
             // the piece's last position b + C - 1: its run partial
-            if (t == FS_W - 1 && s == C / FS_W - 1 && started && q >= 0 && qg >= 0) {
-                piece = true;
-                pfull = unbroken;  // one key from the walk's start to here
+            if (t == FS_W - 1 && s == C / FS_W - 1) {
+                piece = valid;
                 pk = pre_idx;
                 pq = pre_val;
             }
@@ -238,7 +239,8 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     }
     if (side) {
         const bool live = a < end;
-        const uint32_t fl = live ? ((piece ? kFsPiece : 0u) | (pfull ? kFsFull : 0u) |
+        // (sorted: the piece is one key iff its first and last keys are equal)
+        const uint32_t fl = live ? ((piece ? kFsPiece : 0u) | (piece && pk == pf_key ? kFsFull : 0u) |
                                     (corr ? kFsCorr : 0u))
                                  : 0u;
         if (live) {
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             o->K = pk;
             o->Q = pq;
             o->fl = fl;
-            o->ck = ck;
+            o->ck = pf_key;  // the head run's key
             o->S = cs;
         }
         // the wave's aggregate of its 64 pieces (in lane order), for the patch's carries
@@ -314,11 +316,11 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
         if (C1 > 0x7FFFFFFFull) return hipErrorInvalidValue;
         net_account((uint64_t)16 * span, "fold_stream_kernel", s);
         if (cemit)
-            hipLaunchKernelGGL((fold_stream_kernel<2, true>), dim3(1), dim3(64), 0, s, src, dst,
+            FLTEE_LAUNCH((fold_stream_kernel<2, true>), dim3(1), dim3(64), 0, s, src, dst,
                                (long long)m, 0ll, (long long)end, 0ll, (long long)fold_len, 0u,
                                (uint32_t)C1, (FoldSide *)nullptr, (uint32_t)cemit_d, cdummy);
         else
-            hipLaunchKernelGGL(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
+            FLTEE_LAUNCH(fold_stream_kernel<2>, dim3(1), dim3(64), 0, s, src, dst, (long long)m,
                                0ll, (long long)end, 0ll, (long long)fold_len, 0u, (uint32_t)C1,
                                (FoldSide *)nullptr, 0u, 0ull);
         return hipGetLastError();
@@ -337,7 +339,7 @@ hipError_t launch_fold_range(const uint64_t *src, uint64_t *dst, size_t m, size_
     // on the large arrays, profiles/r01/ab/fold_chunk_depth*.jsonl)
     const int depth = blocks <= 256 ? 2 : 1;
 #define FS_GO(D_, E_)                                                                              \
-    hipLaunchKernelGGL((fold_stream_kernel<D_, E_>), dim3((unsigned)blocks), dim3(64), 0, s, src,  \
+    FLTEE_LAUNCH((fold_stream_kernel<D_, E_>), dim3((unsigned)blocks), dim3(64), 0, s, src,  \
                        dst, (long long)m, (long long)origin, (long long)end, pbase,                \
                        (long long)fold_len, (uint32_t)Hr, (uint32_t)C, side, (uint32_t)cemit_d,    \
                        cdummy)
@@ -448,7 +450,7 @@ hipError_t launch_fold_range_total(const FoldSide *side, size_t lanes, FoldAgg *
                                    hipStream_t s) {
     const size_t waves = (lanes + 63) / 64;
     if (waves > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fold_patch_kernel<false, false>), dim3(1), dim3(kFpNT), 0, s, side,
+    FLTEE_LAUNCH((fold_patch_kernel<false, false>), dim3(1), dim3(kFpNT), 0, s, side,
                        (uint32_t)lanes, (uint32_t)waves, (uint64_t *)nullptr, 0ll, 0u, 0ll,
                        (const FoldAgg *)nullptr, 0u, total, 0u, 0ull);
     return hipGetLastError();
@@ -466,12 +468,12 @@ hipError_t launch_fold_range_patch(uint64_t *dst, size_t span, size_t origin, lo
     const unsigned blocks = (unsigned)((lanes + kFpLanes - 1) / kFpLanes);
     net_account((uint64_t)sizeof(FoldSide) * lanes + 16 * lanes, "fold_patch_kernel", s);
     if (cemit_d)
-        hipLaunchKernelGGL((fold_patch_kernel<true, true>), dim3(blocks), dim3(kFpNT), 0, s, side,
+        FLTEE_LAUNCH((fold_patch_kernel<true, true>), dim3(blocks), dim3(kFpNT), 0, s, side,
                            (uint32_t)lanes, (uint32_t)waves, dst, (long long)origin, (uint32_t)C,
                            pbase, prev, (uint32_t)nprev, (FoldAgg *)nullptr, (uint32_t)cemit_d,
                            cdummy);
     else
-        hipLaunchKernelGGL((fold_patch_kernel<true, false>), dim3(blocks), dim3(kFpNT), 0, s, side,
+        FLTEE_LAUNCH((fold_patch_kernel<true, false>), dim3(blocks), dim3(kFpNT), 0, s, side,
                            (uint32_t)lanes, (uint32_t)waves, dst, (long long)origin, (uint32_t)C,
                            pbase, prev, (uint32_t)nprev, (FoldAgg *)nullptr, 0u, 0ull);
     return hipGetLastError();
@@ -481,7 +483,7 @@ hipError_t launch_fold(const uint64_t *src, uint64_t *dst, size_t m, size_t fold
                        void *side_ws, size_t side_cap, hipStream_t s, size_t cemit_d,
                        uint64_t cdummy) {
     if (m == 1 && !cemit_d)  // nothing to fold: position 0 receives itself (:102-103)
-        return hipMemcpyAsync(dst, src, 8, hipMemcpyDeviceToDevice, s);
+        return fl_memcpy_async(dst, src, 8, hipMemcpyDeviceToDevice, s);
     if (m == 0 || (m & 1)) return hipErrorInvalidValue;  // m = next_pow2: 16-B windows
     if (side_cap < fold_side_bytes(m, fold_len, halo, 0, 0)) return hipErrorInvalidValue;
     FoldSide *side = (FoldSide *)side_ws;
@@ -505,9 +507,9 @@ hipError_t launch_extract(const uint64_t *src, size_t d, float coef, float *out,
     if (d == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((d + 255) / 256);
     if (accumulate)
-        hipLaunchKernelGGL(extract_kernel<true>, dim3(blocks), dim3(256), 0, s, src, d, coef, out);
+        FLTEE_LAUNCH(extract_kernel<true>, dim3(blocks), dim3(256), 0, s, src, d, coef, out);
     else
-        hipLaunchKernelGGL(extract_kernel<false>, dim3(blocks), dim3(256), 0, s, src, d, coef, out);
+        FLTEE_LAUNCH(extract_kernel<false>, dim3(blocks), dim3(256), 0, s, src, d, coef, out);
     return hipGetLastError();
 }
 
@@ -533,7 +535,7 @@ hipError_t launch_composite_init(const void *rec, size_t nrec, size_t d, size_t 
                                  uint32_t *status, hipStream_t s) {
     size_t blocks = (m + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(composite_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+    FLTEE_LAUNCH(composite_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint2 *)rec, nrec, d, m, keys, status);
     return hipGetLastError();
 }

@@ -40,7 +40,7 @@ hipError_t launch_laplace_r(size_t d, size_t k, float T, uint64_t seed, uint32_t
                             hipStream_t s) {
     if (d == 0) return hipSuccess;
     const float b = 2.0f * (float)k / 100.0f;
-    hipLaunchKernelGGL(laplace_r_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, d, b,
+    FLTEE_LAUNCH(laplace_r_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, d, b,
                        T, (uint32_t)seed, (uint32_t)(seed >> 32), r);
     return hipGetLastError();
 }
@@ -74,7 +74,7 @@ hipError_t launch_nips19_build_range(const void *rec, size_t nrec, const uint32_
     if (m == 0) return hipSuccess;
     size_t blocks = (m + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(nips19_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+    FLTEE_LAUNCH(nips19_build_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint64_t *)rec, nrec, r, d, tf, pbase, m, dst);
     return hipGetLastError();
 }
@@ -206,12 +206,12 @@ hipError_t launch_select_count(const uint64_t *src, size_t m, size_t d, uint32_t
     const bool vec = ((uintptr_t)src & 15) == 0;
     const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
     if (vec)
-        hipLaunchKernelGGL(select_count_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+        FLTEE_LAUNCH(select_count_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
                            (const uint2 *)src, m, dd, cnt);
     else
-        hipLaunchKernelGGL(select_count_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+        FLTEE_LAUNCH(select_count_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
                            (const uint2 *)src, m, dd, cnt);
-    hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
+    FLTEE_LAUNCH(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
     return hipGetLastError();
 }
 
@@ -222,10 +222,10 @@ hipError_t launch_select_write(const uint64_t *src, size_t m, size_t d, const ui
     const bool vec = ((uintptr_t)src & 15) == 0;
     const uint32_t dd = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
     if (vec)
-        hipLaunchKernelGGL(select_write_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+        FLTEE_LAUNCH(select_write_kernel<true>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
                            (const uint2 *)src, m, dd, base, (uint2 *)dst);
     else
-        hipLaunchKernelGGL(select_write_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
+        FLTEE_LAUNCH(select_write_kernel<false>, dim3((unsigned)nb), dim3(SEL_NT), 0, s,
                            (const uint2 *)src, m, dd, base, (uint2 *)dst);
     return hipGetLastError();
 }
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void select_gather_kernel(const uint64_t *__re
 }
 
 hipError_t launch_select_scan(const uint32_t *cnt, size_t nb, uint32_t *base, hipStream_t s) {
-    hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
+    FLTEE_LAUNCH(select_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (uint32_t)nb, base);
     return hipGetLastError();
 }
 
@@ -254,7 +254,7 @@ hipError_t launch_select_gather(const uint64_t *data, uint32_t tlog, size_t ntil
                                 const uint32_t *cnt, const uint32_t *base, uint64_t *sel,
                                 hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(select_gather_kernel, dim3((unsigned)ntiles), dim3(256), 0, s, data, tlog,
+    FLTEE_LAUNCH(select_gather_kernel, dim3((unsigned)ntiles), dim3(256), 0, s, data, tlog,
                        cnt, base, sel);
     return hipGetLastError();
 }

@@ -481,10 +481,10 @@ hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, v
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     size_t blocks = (ns + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(oram_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4 *)tree, ns);
+    FLTEE_LAUNCH(oram_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint4 *)tree, ns);
     if (A == 0) {
         if (lazy)
-            hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+            FLTEE_LAUNCH(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                                (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
         return hipGetLastError();
     }
@@ -492,18 +492,18 @@ hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, v
     const size_t MA = next_pow2_sz(A);
     size_t kb = (MA + 255) / 256;
     if (kb > 65536) kb = 65536;
-    hipLaunchKernelGGL(oram_keys_kernel, dim3((unsigned)kb), dim3(256), 0, s, (const uint2 *)rec,
+    FLTEE_LAUNCH(oram_keys_kernel, dim3((unsigned)kb), dim3(256), 0, s, (const uint2 *)rec,
                        (uint32_t)nrec, (uint32_t)d, (uint32_t)A, (uint32_t)MA, mask, lazy ? 0 : 1, keys);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = bitonic_sort(keys, MA, 1, 0, s, A);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(oram_link_kernel, dim3((unsigned)kb), dim3(256), 0, s, keys, (uint32_t)A,
+    FLTEE_LAUNCH(oram_link_kernel, dim3((unsigned)kb), dim3(256), 0, s, keys, (uint32_t)A,
                        (uint32_t)MA, k0, k1, mask, keys2);
     e = hipGetLastError();
     if (e == hipSuccess) e = bitonic_sort(keys2, MA, 1, 0, s, A);
     if (e != hipSuccess) return e;
 #define OT_GO(REF_, ACC_)                                                                          \
-    hipLaunchKernelGGL((oram_tree_kernel<REF_, ACC_>), dim3(1), dim3(64), 0, s, (const uint2 *)rec, \
+    FLTEE_LAUNCH((oram_tree_kernel<REF_, ACC_>), dim3(1), dim3(64), 0, s, (const uint2 *)rec, \
                        (uint32_t)nrec, (uint32_t)d, (uint32_t)A, (const uint64_t *)keys2, Lh,       \
                        (uint4 *)tree, k0, k1, g_oram_zlim, coef, out, status)
     if (lazy) OT_GO(false, false);
@@ -511,7 +511,7 @@ hipError_t launch_oram_tree(const void *rec, size_t nrec, size_t d, bool lazy, v
     else OT_GO(true, false);
 #undef OT_GO
     if (lazy)
-        hipLaunchKernelGGL(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+        FLTEE_LAUNCH(oram_records_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                            (const uint4 *)tree, ns, (uint32_t)N, (uint2 *)records);
     return hipGetLastError();
 }

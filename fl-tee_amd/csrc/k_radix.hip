@@ -269,9 +269,9 @@ hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void 
     uint32_t *totals = counts + (((size_t)p.passes * kCsBins * p.tiles * 4 + 255) & ~(size_t)255) / 4;
     const uint32_t nt = (uint32_t)p.tiles, nb = 1u << p.width;
     const uint64_t *src = (const uint64_t *)rec;
-    hipLaunchKernelGGL(cs_hist<true>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d, 0u,
+    FLTEE_LAUNCH(cs_hist<true>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d, 0u,
                        p.width, p.passes, nt, counts, status, zero, (uint32_t)(zero ? nzero : 0));
-    hipLaunchKernelGGL(cs_rowsum, dim3(nb, p.passes), dim3(kCsNT), 0, s, (const uint32_t *)counts, nt,
+    FLTEE_LAUNCH(cs_rowsum, dim3(nb, p.passes), dim3(kCsNT), 0, s, (const uint32_t *)counts, nt,
                        totals);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -280,10 +280,10 @@ hipError_t launch_sort_records_by_idx(const void *rec, size_t n, size_t d, void 
         uint64_t *dst = ((p.passes - 1 - q) & 1) ? tmp : sorted;
         const uint32_t shift = q * p.width;
         if (q > 0)  // this pass's counts by ITS tiles (pass 0's came with the totals)
-            hipLaunchKernelGGL(cs_hist<false>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n,
+            FLTEE_LAUNCH(cs_hist<false>, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n,
                                (uint32_t)d, shift, p.width, p.passes, nt, counts, status, nullptr, 0u);
-        hipLaunchKernelGGL(cs_scan, dim3(nb), dim3(kCsNT), 0, s, counts, nt, totals + q * kCsBins);
-        hipLaunchKernelGGL(cs_scatter, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d,
+        FLTEE_LAUNCH(cs_scan, dim3(nb), dim3(kCsNT), 0, s, counts, nt, totals + q * kCsBins);
+        FLTEE_LAUNCH(cs_scatter, dim3(nt), dim3(kCsNT), 0, s, src, (uint32_t)n, (uint32_t)d,
                            shift, p.width, nt, (const uint32_t *)counts, dst);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         src = dst;
@@ -377,10 +377,10 @@ hipError_t launch_fold_sorted(const uint64_t *sorted, size_t n, size_t d, float 
     if (n > 0x7FFFFFFFull || d > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((n + 256 * kFoldCh - 1) / (256 * kFoldCh));
     if (accumulate)
-        hipLaunchKernelGGL(fold_chunks_kernel<true>, dim3(blocks), dim3(256), 0, s, sorted,
+        FLTEE_LAUNCH(fold_chunks_kernel<true>, dim3(blocks), dim3(256), 0, s, sorted,
                            (uint32_t)n, (uint32_t)d, coef, out);
     else
-        hipLaunchKernelGGL(fold_chunks_kernel<false>, dim3(blocks), dim3(256), 0, s, sorted,
+        FLTEE_LAUNCH(fold_chunks_kernel<false>, dim3(blocks), dim3(256), 0, s, sorted,
                            (uint32_t)n, (uint32_t)d, coef, out);
     return hipGetLastError();
 }
@@ -398,7 +398,7 @@ hipError_t launch_gather_by_keys(const uint64_t *keys, size_t n, const void *rec
     if (n == 0) return hipSuccess;
     size_t blocks = (n + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(gather_by_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, n,
+    FLTEE_LAUNCH(gather_by_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, s, keys, n,
                        (const uint64_t *)rec, dst);
     return hipGetLastError();
 }

@@ -137,3 +137,36 @@ def test_session_round_keys_aesni_equals_portable():
     w = a.reshape(n, 44)
     assert (w[:, 0] == 0).all() and (w[:, 2] == 0).all() and (w[:, 3] == 0).all()
     assert np.array_equal(w[:, 1], ids)
+
+
+RAW_GPU_CALLS = ("hipLaunchKernelGGL", "hipMemcpyAsync", "hipMemcpy2DAsync", "hipMemcpy",
+                 "hipMemsetAsync", "hipMemset", "hipStreamSynchronize", "hipDeviceSynchronize",
+                 "hipEventSynchronize")
+
+
+def test_every_launch_copy_and_sync_goes_through_the_trace():
+    """the obliviousness test (tests/test_gpu_oblivious.py) compares launch
+    traces; a launch, copy, memset or host synchronisation that bypassed the trace
+    wrappers of csrc/common.h (FLTEE_LAUNCH, fl_memcpy_async, fl_memset_async,
+    fl_stream_sync, ...) would be invisible to it.  Every .hip source is scanned (comments
+    stripped); the raw calls may appear only inside those wrappers in common.h."""
+    csrc = os.path.join(ROOT, "fl-tee_amd", "csrc")
+    pat = re.compile(r"(?<![A-Za-z0-9_])(" + "|".join(RAW_GPU_CALLS) + r")\s*\(")
+    bad = []
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".hip", ".cpp")):
+            continue
+        text = open(os.path.join(csrc, f)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for i, line in enumerate(text.splitlines(), 1):
+            code = line.split("//", 1)[0]
+            for m in pat.finditer(code):
+                bad.append(f"{f}:{i}: {m.group(1)}")
+    assert not bad, "raw GPU calls outside the trace wrappers:\n" + "\n".join(bad)
+    common = open(os.path.join(csrc, "common.h")).read()
+    for w in ("FLTEE_LAUNCH", "fl_memcpy_async", "fl_memset_async", "fl_stream_sync", "fl_device_sync"):
+        assert w in common
+    # and the library exports the trace hooks the GPU test drives
+    from fltee import _lib as L
+    for sym in ("fltee_debug_trace", "fltee_debug_trace_text"):
+        assert hasattr(L.lib(), sym)

@@ -57,6 +57,9 @@ def test_line_is_compact_and_complete(make, tmp_path, capsys):
     assert 0 < line["roofline"]["frac"] < 1
     if line["n_gpus"] == 1:
         assert CPU <= set(line["cpu_baseline"])
+        # the threads used, and the host's core count and model beside them
+        cb = line["cpu_baseline"]
+        assert cb["cores"] == 1 and cb["host_cores"] >= cb["cores"] and cb["host_model"]
         for key in ("e2e_host_inclusive", "metric_literal_config", "configs", "exp5"):
             assert key in line
         assert {"c3", "c4", "c5"} <= set(line["configs"])
@@ -87,3 +90,16 @@ def test_unwritable_detail_still_prints(capsys):
     bench.emit(full, "/proc/no/such/dir/detail.json")
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["detail"].startswith("not written")
+
+
+def test_rocprof_cross_check_reads_the_newest_round():
+    """bench_legs.rocprof_kernel takes the newest committed rocprofv3 summary of a config
+    (VERDICT r5 #6: it read round 4's while round 5's existed)."""
+    import glob
+
+    import bench_legs
+    rounds = sorted(os.path.basename(os.path.dirname(p)) for p in
+                    glob.glob(os.path.join(ROOT, "profiles", "r0*", "ns_kernel_stats.csv")))
+    rp = bench_legs.rocprof_kernel("ns", "dense_accumulate_v")
+    assert rp is not None and rounds
+    assert rp["source"] == os.path.join("profiles", rounds[-1], "ns_kernel_stats.csv")
