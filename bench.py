@@ -29,6 +29,8 @@ import sys
 import threading
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "fl-tee_amd"))
@@ -86,7 +88,8 @@ def compact_line(full):
         line["metric_literal_config"] = {
             "value": _r(lit["value"]), "kernel_ms": _r(lit["kernel_ms"]),
             "kernel_ms_median": _r(lit.get("kernel_ms_median")),
-            "frac": _r(lit["roofline"]["frac"]), "trials": lit.get("trials")}
+            "frac": _r(lit["roofline"]["frac"]), "trials": lit.get("trials"),
+            "launch_ms_pct": {k: _r(v) for k, v in (lit.get("launch_ms_pct") or {}).items()}}
         rf = lit.get("read_floor")
         if rf:  # the same bytes read by a plain streaming kernel in the same run
             line["metric_literal_config"]["read_floor_ms"] = _r(rf["us"] / 1e3)
@@ -383,13 +386,18 @@ def main():
             # inputs rotated through > 1.5 x the Infinity Cache so every launch reads HBM;
             # 3 trials, each warming every rotating buffer once: best and median reported
             trials = sorted((bench_workload(torch, D, "mnist100", steps=max(20, args.steps),
-                                            warmup=12, device=device, cold=True)
+                                            warmup=12, device=device, cold=True, per_launch=True)
                              for _ in range(3)), key=lambda r: r["kernel_s"])
             lit = trials[0]
+            # the spread of single launches: every trial's per-launch event
+            # times, p10 / p50 / p90
+            lts = np.array([x for t in trials for x in t.get("launch_ms", [])])
+            pct = {f"p{q}": float(np.percentile(lts, q)) for q in (10, 50, 90)} if lts.size else {}
             floor = read_floor(torch, lit["bytes"], device)
             full["metric_literal_config"] = dict(
                 workload=WORKLOADS["mnist100"]["desc"], value=lit["rate"], unit="client-params/s",
                 kernel_ms=lit["kernel_s"] * 1e3, kernel_ms_median=trials[1]["kernel_s"] * 1e3,
+                launch_ms_pct=pct, launches=int(lts.size),
                 kernel_ms_trials=[t["kernel_s"] * 1e3 for t in trials],
                 input_buffers=lit["nbuf"], trials=len(trials),
                 roofline=dict(bound="hbm", achieved=lit["bytes"] / lit["kernel_s"] / 1e9,

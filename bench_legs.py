@@ -84,9 +84,24 @@ def time_steps(torch, fn, steps, warmup, stream):
     return wall, kern
 
 
-def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False):
+def launch_times(torch, fn, steps, start, stream):
+    """per-launch durations (ms): an event pair around each launch, back to back (each
+    pair's own gap included — for the distribution, not the headline)"""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        fn(start + i)
+        b.record(stream)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False, per_launch=False):
     """cold=True: rotate through enough input buffers (> 1.5 x the 256 MiB Infinity
-    Cache) that every launch reads its records from HBM."""
+    Cache) that every launch reads its records from HBM.  per_launch: also each launch's
+    own event time (launch_ms)."""
     w = WORKLOADS[name]
     n, d, k = w["n"], w["d"], w["k"]
     kk = d if k is None else k
@@ -107,11 +122,15 @@ def bench_workload(torch, D, name, steps, warmup, device, nbuf=3, cold=False):
         D.aggregate(w["alg"], recs[i % nbuf], n, kk, d, out=out, **kw)
 
     wall, kern = time_steps(torch, step, steps, warmup, stream)
+    lt = launch_times(torch, step, steps, warmup + steps, stream) if per_launch else None
     assert int(status.item()) == 0, f"device status {int(status.item()):#x}"
     net = net_stats(torch, lambda: step(0))
     del recs
-    return dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
-                rate=n * kk / kern, bytes=algorithmic_bytes(w), nbuf=nbuf, net=net)
+    r = dict(n=n, d=d, k=kk, alg=ALG_NAMES[w["alg"]], wall_s=wall, kernel_s=kern,
+             rate=n * kk / kern, bytes=algorithmic_bytes(w), nbuf=nbuf, net=net)
+    if lt is not None:
+        r["launch_ms"] = lt
+    return r
 
 
 def read_floor(torch, bytes_per_step, device, reps=3, steps=40):

@@ -90,12 +90,15 @@ __device__ __forceinline__ void dw_batch(const uint4 *__restrict__ p, size_t d2,
     }
 }
 
+// per (< 64: the balanced-grid A/B, variants 50-52): output pairs per wave, so that the
+// waves spread evenly over the CUs (MLP-MNIST: 398 full waves leave 142 CUs with two and
+// 114 with one)
 template <int U, bool REM, bool CLIP, bool ACC, bool NTL = true>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void dense_accumulate_w(
     const uint4 *__restrict__ rec, size_t d2, uint32_t n, float coef, float *__restrict__ out,
-    const float *__restrict__ ccoef, uint32_t *status) {
-    const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x;
-    if (j >= d2) return;
+    const float *__restrict__ ccoef, uint32_t *status, uint32_t per = 64) {
+    const size_t j = (size_t)blockIdx.x * per + threadIdx.x;
+    if (threadIdx.x >= per || j >= d2) return;
     const uint4 *p = rec + j;
     const uint32_t jx = (uint32_t)(2 * j);
     float a0 = 0.0f, a1 = 0.0f;
@@ -545,9 +548,20 @@ static void launch_lds(bool vec, const void *rec, size_t n, size_t d, float coef
 
 template <int U, bool REM, bool ACC>
 static void dw_launch(unsigned blocks, const void *rec, size_t n, size_t d, float coef, float *out,
-                      uint32_t *status, hipStream_t s) {
+                      uint32_t *status, hipStream_t s, uint32_t per = 64) {
     FLTEE_LAUNCH((dense_accumulate_w<U, REM, false, ACC>), dim3(blocks), dim3(64), 0, s,
-                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status);
+                       (const uint4 *)rec, d / 2, (uint32_t)n, coef, out, nullptr, status, per);
+}
+
+static int cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
 }
 
 template <bool CLIP, bool ACC>
@@ -624,6 +638,22 @@ static hipError_t dense_dispatch(const void *rec, size_t n, size_t d, float coef
                                    dim3(256), 0, s, (const uint2 *)rec, d, (uint32_t)n, coef, out,
                                    ccoef, status);
                 break;
+            }
+            launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
+            break;
+        // 50-52: dense_accumulate_w on a grid of 2 / 3 / 4 waves per CU (balanced)
+        case 50: case 51: case 52:
+            if (vec && !CLIP && n > 32 && n <= 100) {
+                const size_t waves = (size_t)cu_count() * (size_t)(g_dense_variant - 48);
+                const uint32_t per = (uint32_t)((d / 2 + waves - 1) / waves);
+                if (per <= 64 && per > 0) {
+                    const unsigned blocks = (unsigned)((d / 2 + per - 1) / per);
+                    if (n == 100) dw_launch<100, false, ACC>(blocks, rec, n, d, coef, out, status, s, per);
+                    else if (n > 64) dw_launch<100, true, ACC>(blocks, rec, n, d, coef, out, status, s, per);
+                    else if (n == 64) dw_launch<64, false, ACC>(blocks, rec, n, d, coef, out, status, s, per);
+                    else dw_launch<64, true, ACC>(blocks, rec, n, d, coef, out, status, s, per);
+                    break;
+                }
             }
             launch_lds<CLIP, ACC, 128, 32>(vec, rec, n, d, coef, out, ccoef, status, s);
             break;
