@@ -653,9 +653,11 @@ constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
 #ifndef FLTEE_FC_LB
 #define FLTEE_FC_LB 1
 #endif
-// the look-back's first-round words loaded before the compaction levels (1) or after (0)
+// the look-back's first-round words loaded before the compaction levels (1) or after (0).
+// Round 6 A/B (`profiles/r06/ab/ab2_*`): 28.9 vs 27.1 us per C3 pass — the 12 VGPRs held
+// across the levels cost more than the load latency they hide
 #ifndef FLTEE_FC_LBPRE
-#define FLTEE_FC_LBPRE 1
+#define FLTEE_FC_LBPRE 0
 #endif
 // the bounded look-back wait: polls of ~0.25 us (about a quarter second in all)
 constexpr uint32_t kFcSpinMax = 1u << 20;
