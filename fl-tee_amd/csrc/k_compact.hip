@@ -653,6 +653,10 @@ constexpr uint32_t kFixedWalkMaxSmall = FLTEE_FC_WALK_MAX_SMALL;
 #ifndef FLTEE_FC_LB
 #define FLTEE_FC_LB 1
 #endif
+// tiles per CU the per-lane slot count aims for (the fewest slots with at most this many)
+#ifndef FLTEE_FC_TILES_PER_CU
+#define FLTEE_FC_TILES_PER_CU 1
+#endif
 // the look-back's first-round words loaded before the compaction levels (1) or after (0).
 // Round 6 A/B (`profiles/r06/ab/ab2_*`): 28.9 vs 27.1 us per C3 pass — the 12 VGPRs held
 // across the levels cost more than the load latency they hide
@@ -677,19 +681,6 @@ __device__ __forceinline__ void fc_put(uint64_t *w, const FoldAgg &g, uint32_t e
     __hip_atomic_store(&w[1], tag | g.K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&w[2], tag | __float_as_uint(g.Q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the three words of this epoch, or false
-__device__ __forceinline__ bool fc_get(uint64_t *w, uint32_t epoch, FoldAgg &g) {
-    const uint64_t a = __hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t b = __hip_atomic_load(&w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t c = __hip_atomic_load(&w[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t ea = (uint32_t)(a >> 34), eb = (uint32_t)(b >> 34), ec = (uint32_t)(c >> 34);
-    g.F = (uint32_t)a;
-    g.K = (uint32_t)b;
-    g.Q = __uint_as_float((uint32_t)c);
-    g.fl = (uint32_t)(c >> 32) & 3u;
-    return ea == epoch && eb == epoch && ec == epoch;
-}
-
 __device__ __forceinline__ FoldAgg fa_shfl_up(const FoldAgg &x, int o) {
     FoldAgg r;
     r.F = (uint32_t)__shfl_up((int)x.F, o);
@@ -745,8 +736,15 @@ __device__ FoldAgg fc_lookback(FcLb *lb, uint32_t tile, uint32_t epoch, uint32_t
             }
 #pragma unroll 1
             while (!ok) {  // the inclusive prefix if it is there, else the aggregate
-                if (fc_get(lb[p].inc, epoch, g)) { isinc = true; ok = true; break; }
-                if (fc_get(lb[p].agg, epoch, g)) { isinc = false; ok = true; break; }
+                // (all six words in flight at once: one memory round trip a poll)
+                uint64_t w[6];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    w[i] = __hip_atomic_load(&lb[p].inc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    w[3 + i] = __hip_atomic_load(&lb[p].agg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (fc_have(w, epoch, g)) { isinc = true; ok = true; break; }
+                if (fc_have(w + 3, epoch, g)) { isinc = false; ok = true; break; }
                 if (++it >= kFcSpinMax) break;
                 __builtin_amdgcn_s_sleep(8);
             }
@@ -1147,7 +1145,7 @@ static bool fc_shape(size_t M, size_t L, size_t d, size_t halo, FcShape &o) {
     o.per = 8;
     for (uint32_t p : {4u, 6u}) {
         if (NT * p <= 2 * H) continue;  // the halo rows would swamp the tile
-        if ((L + NT * p - H - 1) / (NT * p - H) <= 256) {
+        if ((L + NT * p - H - 1) / (NT * p - H) <= 256 * FLTEE_FC_TILES_PER_CU) {
             o.per = p;
             break;
         }
