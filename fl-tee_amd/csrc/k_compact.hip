@@ -808,8 +808,6 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
     __shared__ FoldAgg agg_s;
     __shared__ FoldAgg lb_sh[NW + 1];
     __shared__ uint32_t lb_shf[NW + 1];
-    __shared__ float exq[NT];
-    __shared__ bool exf[NT];
     __shared__ uint32_t fix_s, kw0_s;
     const uint32_t H = (1u << G) - 1;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -922,8 +920,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             for (uint32_t w = 0; w < wave; ++w) ex = fa_combine(ex, wtot[w]);
             ex = fa_combine(ex, wex);
             const uint32_t k0 = x0 < (int)Wn ? (uint32_t)win[x0] : 0u;
-            exq[t] = ex.Q;
-            exf[t] = (ex.fl & kFsPiece) && ex.K == k0;
+            const bool exf = (ex.fl & kFsPiece) && ex.K == k0;
             if (t == 0) {
                 fix_s = 0xFFFFFFFFu;
                 kw0_s = (uint32_t)win[0];
@@ -940,7 +937,21 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 fc_put(lb[tile].agg, g, epoch);
                 agg_s = g;
             }
+            // The lane's head run, when it began before the lane's walk (more than lim
+            // entries: the walk's sums miss its front): its slots take the re-associated
+            // window-local prefix — the partial in front of x0 (ex) + the partial from x0
+            // (loc).  Only the head run can be such a run; the owner lane fixes its own
+            // slots (a fixed trip count), so the representative loop below reads sums[]
+            // alone.  (Round 6 first had every slot test its owner's head run there: six
+            // LDS reads a slot, and a read of the owner's ex without a barrier.)
+            const bool lngL = ys > 0 && x0 < (int)Wn && (uint32_t)win[ys - 1] == k0;
+            for (uint32_t i = 0; i < chunk; ++i) {
+                const int y = x0 + (int)i;
+                const bool fix = lngL && y < (int)Wn && (uint32_t)win[min(y, (int)Wn - 1)] == k0;
+                if (fix) sums[y] = exf ? __fadd_rn(ex.Q, loc[y]) : loc[y];
+            }
         }
+        __syncthreads();  // every lane's sums[] final before any lane reads another's
         // representatives with idx < d -> (c = p - idx, sum); the rest never move.  A run
         // that began before its owner lane's walk (more than lim entries) takes the
         // re-associated window-local prefix (the owner's partial in front of its slots +
@@ -950,7 +961,6 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         {
             const uint32_t kw0 = (uint32_t)win[0];
             const uint32_t gm = (1u << G) - 1;
-            const float rchunk = 1.0f / (float)chunk + 1e-6f;
 #pragma unroll
             for (uint32_t i = 0; i < PER; ++i) {
                 const uint32_t f = t + i * NT, x = f + Hr;
@@ -958,13 +968,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 const uint64_t r = win[x];
                 const uint32_t idx = (uint32_t)r;
                 const bool end = p == (long long)L - 1 || (uint32_t)win[x + 1] != idx;
-                // x's owner lane and its first slot (x < 2^14, chunk <= 16: the f32 quotient
-                // truncates exactly)
-                const uint32_t o = (uint32_t)((float)x * rchunk), xo = o * chunk;
-                const int yso = (int)xo - (int)lim;
-                const bool lng = yso > 0 && (uint32_t)win[yso - 1] == idx;
-                const float wl = (exf[o] && idx == (uint32_t)win[xo]) ? __fadd_rn(exq[o], loc[x]) : loc[x];
-                const float hv = lng ? wl : sums[x];
+                const float hv = sums[x];
                 const bool rep = p < (long long)L && idx < d && end;
                 const uint32_t c = (uint32_t)p - idx;
                 v[i] = rep ? (((uint64_t)__float_as_uint(hv) << 32) | c) : CP_DUMMY;
