@@ -849,12 +849,12 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
         // branch, the next slot's LDS read issued a step ahead.  The sums go to their own
         // LDS array (sums[], after the window), so no lane overwrites what another still
         // reads; a run's last slot then holds the run's sum — all the compaction reads.
-        // Over its own slots the walk also keeps the run partials from x0 (loc[]) and the
+        // Over its own slots the walk also keeps the run partial from x0 (acc2) and the
         // lane's segmented aggregate, for the runs longer than the walk (see above).
         float *sums = reinterpret_cast<float *>(win + Wn);
-        float *loc = sums + Wn;
         const int x0 = (int)(t * chunk), ys = x0 - (int)lim;
         FoldAgg ca = fa_empty();
+        float qS = 0.0f;  // acc2 at the tile's last slot S - 1 (its owner lane's)
         {
             const int pw = (int)wlo;  // |positions| < 2^29 (launch guard)
             auto rd = [&](int y) { return win[min((uint32_t)max(y, 0), Wn - 1)]; };
@@ -890,11 +890,11 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 const uint32_t ky = (uint32_t)r;
                 const bool c2 = i > 0 && ky == kl;
                 acc2 = in ? (c2 ? __fadd_rn(acc2, rec_val(r)) : rec_val(r)) : acc2;
+                qS = y == (int)S - 1 ? acc2 : qS;
                 unb = unb && (!in || i == 0 || c2);
                 kl = in ? ky : kl;
                 if (in) {
                     sums[y] = acc;
-                    loc[y] = acc2;
                 }
             }
             if (x0 < (int)Wn) {
@@ -931,7 +931,7 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
                 FoldAgg part;
                 part.F = k0;
                 part.K = kS;
-                part.Q = loc[S - 1];
+                part.Q = qS;
                 part.fl = kFsPiece | (k0 == kS ? kFsFull : 0u);
                 const FoldAgg g = fa_combine(ex, part);
                 fc_put(lb[tile].agg, g, epoch);
@@ -939,23 +939,27 @@ __global__ __launch_bounds__(NT, BPC * NT >= 1024 ? BPC * NT / 256 : 1) void fol
             }
             // The lane's head run, when it began before the lane's walk (more than lim
             // entries: the walk's sums miss its front): its slots take the re-associated
-            // window-local prefix — the partial in front of x0 (ex) + the partial from x0
-            // (loc).  Only the head run can be such a run; the owner lane fixes its own
+            // window-local prefix — the partial in front of x0 (ex) + the partial from x0.  Only the head run can be such a run; the owner lane fixes its own
             // slots (a fixed trip count), so the representative loop below reads sums[]
             // alone.  (Round 6 first had every slot test its owner's head run there: six
             // LDS reads a slot, and a read of the owner's ex without a barrier.)
+            // (the partial from x0 recomputed here, in the walk's order: the head run is
+            // contiguous from x0, so a2 is the walk's acc2 on its slots)
             const bool lngL = ys > 0 && x0 < (int)Wn && (uint32_t)win[ys - 1] == k0;
+            float a2 = 0.0f;
             for (uint32_t i = 0; i < chunk; ++i) {
                 const int y = x0 + (int)i;
-                const bool fix = lngL && y < (int)Wn && (uint32_t)win[min(y, (int)Wn - 1)] == k0;
-                if (fix) sums[y] = exf ? __fadd_rn(ex.Q, loc[y]) : loc[y];
+                const uint64_t r = win[min(y, (int)Wn - 1)];
+                a2 = i == 0 ? rec_val(r) : __fadd_rn(a2, rec_val(r));
+                const bool fix = lngL && y < (int)Wn && (uint32_t)r == k0;
+                if (fix) sums[y] = exf ? __fadd_rn(ex.Q, a2) : a2;
             }
         }
         __syncthreads();  // every lane's sums[] final before any lane reads another's
         // representatives with idx < d -> (c = p - idx, sum); the rest never move.  A run
         // that began before its owner lane's walk (more than lim entries) takes the
-        // re-associated window-local prefix (the owner's partial in front of its slots +
-        // loc); the carry from before the window is added after the levels (below), to the
+        // re-associated window-local prefix (fixed by the owner lane above); the carry from
+        // before the window is added after the levels (below), to the
         // one record it concerns: the window's head run's, wherever the levels took it.
         uint64_t v[PER];
         {
@@ -1159,7 +1163,7 @@ static bool fc_shape(size_t M, size_t L, size_t d, size_t halo, FcShape &o) {
     o.ntiles = (L + o.S - 1) / o.S;
     // the window, the walks' run sums and the run partials beside it; the resident blocks
     // per CU must fit the 160 KiB LDS (lim <= 320: 71 KiB a block)
-    const size_t lds = (o.Hr + CAP + 1) * 16;
+    const size_t lds = (o.Hr + CAP + 1) * 12;  // the window (8 B a slot), its sums (4 B)
     return lds * FLTEE_FC_BLOCKS <= 160 * 1024 && lds <= 80 * 1024;
 }
 
@@ -1180,7 +1184,7 @@ hipError_t launch_fold_compact_extract(uint64_t *A, uint64_t *B, size_t M, size_
     const uint32_t nlev = bitlen(L - d);
     const uint32_t CAP = NT * o.per;
     const bool last = o.G == nlev;
-    const size_t lds = (o.Hr + CAP + 1) * 16;
+    const size_t lds = (o.Hr + CAP + 1) * 12;  // the window (8 B a slot), its sums (4 B)
     net_account((uint64_t)(last ? 8 : 16) * L, "fold_compact_first", s);
     const bool x1 = o.Hr + 1 <= NT;  // one window slot past CAP per lane, else two
     const int F = !last ? 0 : (accumulate ? 2 : 1);
