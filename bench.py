@@ -39,7 +39,7 @@ from bench_legs import (ALG_NAMES, HBM_PEAK_GBS, WORKLOADS, algorithmic_bytes,  
                         bench_c4_index_sharded, bench_c5_index_sharded, bench_c5_sharded,
                         bench_exp5, bench_next_rows, bench_oram_tree, bench_reference_configs, bench_workload,
                         bench_ns_strong, c_abi_multi_gpu, cpu_baseline_configs, cpu_baseline_sample,
-                        dominant_kernel, e2e_sample, launch_times, make_records, network_records,
+                        dominant_kernel, e2e_sample, make_records, network_records,
                         read_floor, rocprof_kernel, traffic_from_profiles, _build_id)
 
 
@@ -393,10 +393,6 @@ def main():
             # times, p10 / p50 / p90
             lts = np.array([x for t in trials for x in t.get("launch_ms", [])])
             pct = {f"p{q}": float(np.percentile(lts, q)) for q in (10, 50, 90)} if lts.size else {}
-            # what an event pair alone measures behind the same spin (its share of each time)
-            if pct:
-                pct["pair"] = float(np.median(launch_times(torch, lambda i: None, 50, 0,
-                                                           torch.cuda.current_stream())))
             floor = read_floor(torch, lit["bytes"], device)
             full["metric_literal_config"] = dict(
                 workload=WORKLOADS["mnist100"]["desc"], value=lit["rate"], unit="client-params/s",

@@ -84,18 +84,13 @@ def time_steps(torch, fn, steps, warmup, stream):
     return wall, kern
 
 
-def launch_times(torch, fn, steps, start, stream, hold_cycles=400_000):
-    """per-launch durations (ms): an event pair around each launch.  Each pair sits behind
-    a GPU-side spin (torch.cuda._sleep) long enough for the host to enqueue the pair and
-    the launch, so the pair times the kernel (+ the events' own gap), not the host's
-    submission: back-to-back pairs without it measured the Python call (the GPU idles
-    between the first event and the kernel)."""
+def launch_times(torch, fn, steps, start, stream):
+    """per-launch durations (ms): an event pair around each launch, back to back (each
+    pair's own gap included — for the distribution, not the headline)"""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     torch.cuda.synchronize()
     for i, (a, b) in enumerate(ev):
-        if hold_cycles:
-            torch.cuda._sleep(hold_cycles)
         a.record(stream)
         fn(start + i)
         b.record(stream)
