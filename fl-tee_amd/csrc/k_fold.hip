@@ -144,9 +144,11 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
     for (int q = 0; q < DEPTH; ++q)
         if ((uint32_t)q < nstage) load_stage(pf[q], (uint32_t)q);
 
-    uint32_t pre_idx = 0;
+    // pre_idx starts as a key no run has before the walk's first real record: an index
+    // >= d (0xFFFFFFFE: a client's out-of-range index at worst, whose sums never reach the
+    // output) instead of a separate `started` flag
+    uint32_t pre_idx = 0xFFFFFFFEu;
     float pre_val = 0.0f;
-    bool started = false;
     uint64_t prev = 0;
     // the side record: the piece [b, b + C) and the head run (the one holding b)
     bool corr = false, piece = false;
@@ -170,13 +172,23 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
         // [Hr + 1, Hr + C] (Hr and C multiples of 16): stage-uniform flags for t = 0 and t > 0
         const uint32_t cs_end = hw + C / FS_W;
         const bool in1 = s >= hw && s < cs_end, in0 = s > hw && s <= cs_end;
+        // the step's position tests as thresholds on t, once a stage (step t reads q = q0 + t,
+        // global qg = qg0 + t): copy <=> qg - 1 >= fold_len, live <=> qg < fold_len, valid
+        // <=> q >= 0 && qg >= 0 — a 32-bit compare with the step's constant each instead of
+        // 64-bit position arithmetic a step
+        const long long qg0 = q0 + pbase;
+        auto tclamp = [](long long x) -> uint32_t { return x < 0 ? 0u : (x > 17 ? 17u : (uint32_t)x); };
+        uint32_t t_copy = tclamp(fold_len + 1 - qg0), t_live = tclamp(fold_len - qg0);
+        uint32_t t_valid = tclamp(-q0 > -qg0 ? -q0 : -qg0);
+        // (opaque to the optimizer, which otherwise folds each test back into a 64-bit
+        // compare of the unclamped difference)
+        asm volatile("" : "+v"(t_copy), "+v"(t_live), "+v"(t_valid));
+        const uint32_t pe0 = (uint32_t)(qg0 - 1);  // (uint32_t)(qg - 1) = pe0 + t
 #pragma unroll
         for (uint32_t t = 0; t < FS_W; ++t) {
-            const long long q = q0 + t;  // this step reads position q, emits position q - 1
-            const long long qg = q + pbase;
             const uint32_t ci = rec_idx(r[t]);
-            const bool eq = started && ci == pre_idx;
-            const bool copy = qg - 1 >= fold_len, dmy = qg < fold_len && eq;
+            const bool eq = ci == pre_idx;
+            const bool copy = t >= t_copy, dmy = t < t_live && eq;
             // the head run ends at q - 1: inside the chunk (step si in [Hr + 1, Hr + C], a
             // wave-uniform test) it is the one the side record carries (emitted as a dummy
             // here, its record written by fold_patch_kernel)
@@ -184,13 +196,14 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             const bool sup = in_head && !copy && !dmy && inchunk;
             uint64_t emit;
             if constexpr (CEMIT) {
-                emit = copy ? prev
-                       : dmy || sup || pre_idx >= dsel
-                           ? cdummy
-                           : make_rec((uint32_t)(qg - 1) - pre_idx, pre_val);  // (c, sum)
+                // (the record computed whatever the case, then selected: no EXEC-mask
+                // branch around it)
+                uint64_t rec = make_rec(pe0 + t - pre_idx, pre_val);  // (c, sum)
+                asm volatile("" : "+v"(rec));
+                emit = copy ? prev : dmy || sup || pre_idx >= dsel ? cdummy : rec;
             } else {
                 emit = copy ? prev
-                       : dmy || sup ? (uint64_t)(0xFFFFFFFFu - (uint32_t)(qg - 1))  // (MAX-p, +0.0)
+                       : dmy || sup ? (uint64_t)(0xFFFFFFFFu - (pe0 + t))  // (MAX-p, +0.0)
                                     : make_rec(pre_idx, pre_val);
             }
             // (value selects: a store through a selected address would put these flags on
@@ -200,12 +213,11 @@ __global__ __launch_bounds__(64) void fold_stream_kernel(const uint64_t *__restr
             in_head = in_head && (dmy || (t == 0 && s == 0));  // (step 0 emits b - 1)
             if (t == 0) old[l * FS_ROW + FS_W - 1] = emit;
             else cur[l * FS_ROW + t - 1] = emit;
-            const bool valid = q >= 0 && qg >= 0;
-            if (valid) {
-                pre_val = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
-                pre_idx = ci;
-                started = true;
-            }
+            const bool valid = t >= t_valid;
+            // (selects: no EXEC-mask branch a step)
+            const float nv = eq ? __fadd_rn(pre_val, rec_val(r[t])) : rec_val(r[t]);
+            pre_val = valid ? nv : pre_val;
+            pre_idx = valid ? ci : pre_idx;
             // the piece's last position b + C - 1: its run partial
             if (t == FS_W - 1 && s == C / FS_W - 1) {
                 piece = valid;
