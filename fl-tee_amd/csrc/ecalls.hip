@@ -181,14 +181,14 @@ static fltee_device_opts ecall_opts(uint32_t alg, size_t n, size_t rpc, size_t d
     if (alg == FLTEE_ALG_PATH_ORAM && oram_tree_default() && oram_fits(n * rpc, d, false))
         o.flags |= FLTEE_OPT_ORAM_TREE;  // (a shape past the tree's bounds takes the sweep)
     if (alg == FLTEE_ALG_NIPS19) o.seed = seed ? seed : next_seed();
-    // advanced's fold (advanced.rs:66-101) runs once with halo = n: exact for every run of
-    // up to n + 1 entries — every upload whose clients each send distinct indices (n
-    // records + the initial entry) — and a run of more (some client repeated an index)
-    // is reported by the same pass (fold_run_limit): the call is rejected with 0x2,
-    // like an out-of-range index, instead of rerunning with a wider halo.  With the
+    // advanced's fold (advanced.rs:66-101) runs once with halo = n: bit for bit for every
+    // run of up to n + 1 entries — every upload whose clients each send distinct indices
+    // (n records + the initial entry) — and a run of more (some client repeated an index)
+    // is finished by the fold's long-run carry in the same fixed-cost sequence (round 6,
+    // k_fold.hip / k_compact.hip), its sum re-associated at the walk boundaries.  With the
     // exact-runs policy the halo is the public worst case (every record one index): one
-    // sequential walk, exact for any run.  Either way the cost is fixed by the public
-    // sizes; no data-dependent relaunch.
+    // sequential walk, bit for bit for any run.  Either way the cost is fixed by the
+    // public sizes; no data-dependent relaunch.
     o.fold_halo = exact_runs_default() ? n * rpc + d : n;
     return o;
 }

@@ -118,7 +118,8 @@ def set_path_oram_tree(on):
 
 def set_advanced_exact_runs(on):
     """aggregation_alg 1 and 6 through the ECALLs when some index has a run of more than
-    n + 1 entries (a client repeated an index): off (default) rejects the call with 0x2
-    after the one fixed-cost fold; on folds any run exactly, as advanced.rs:66-101 does,
-    at the public worst-case cost (fltee_set_advanced_exact_runs)."""
+    n + 1 entries (a client repeated an index): off (default) answers at the fixed cost of
+    the halo fold plus its long-run carry (that run's sum re-associated at the walk
+    boundaries); on folds any run exactly, as advanced.rs:66-101 does, at the public
+    worst-case cost (fltee_set_advanced_exact_runs)."""
     L.lib().fltee_set_advanced_exact_runs(1 if on else 0)

@@ -354,9 +354,10 @@ fltee_status_t fltee_ordered_list_device(const void *d_list, size_t lc, size_t d
 void fltee_set_path_oram_tree(int on);
 /* The ECALLs' advanced and alg 6 when some index has a run of more than n + 1 entries
  * (a client repeated an index inside its upload; fl_main.py's top-k never does):
- * off (default) = the call is rejected with 0x2 after the one fixed-cost fold pass;
- * on = the enclave's exact fold for ANY run length (advanced.rs:66-101), at the public
- * worst-case cost: one sequential walk of the whole sorted array whatever the data. */
+ * off (default) = the fixed-cost fold with its long-run carry: such a run's sum is the
+ * enclave's re-associated at the fold's walk boundaries (runs of <= n + 1 entries bit for
+ * bit); on = the enclave's exact fold for ANY run length (advanced.rs:66-101), at the
+ * public worst-case cost: one sequential walk of the whole sorted array whatever the data. */
 void fltee_set_advanced_exact_runs(int on);
 void fltee_debug_set_seed(uint64_t seed);
 /* Library build/version string. */
